@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""make_golden.py -- generate tests/golden/*.npz from the REFERENCE shader.
+
+TEST INFRASTRUCTURE ONLY; runs in the build container (needs /root/reference,
+node and the SwiftShader libraries bundled with kaleido).  Nothing here runs on
+the GPU box.
+
+For every config of tests/golden/configs.json:
+  1. node make_shader.js expands raytracer.glsl with the reference's own
+     parseShader / GlslViewport defaults (oracle/_gen/<name>.frag, ignored by git);
+  2. glrun (oracle/gen/glrun.c, built to oracle/_ref/glrun) renders `frames`
+     passes at 64x64 with the accumulator input bound to zero (--single), so each
+     output is exactly one sample per pixel of pass k (u_frame = k);
+  3. the RGBA32F outputs are stored as <name>.npz: samples[F,H,W,4] (row 0 =
+     bottom row, gl_FragCoord.y = 0.5), and for ReSTIR configs the two reservoir
+     MRTs restir_main/restir_aux[F,H,W,4].
+A known-answer shader (make_shader.js --kat) is run once for the RNG stream:
+rng_kat.npz.  manifest.json records the effective host state and NaN counts.
+
+usage: python3 oracle/gen/make_golden.py [config-name ...]
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+GOLD = os.path.join(REPO, "tests", "golden")
+GEN = os.path.join(REPO, "oracle", "_gen")
+REFBIN = os.path.join(REPO, "oracle", "_ref")
+W = H = 64
+
+
+def sh(cmd, **kw):
+    return subprocess.run(cmd, check=True, capture_output=True, text=True, **kw)
+
+
+def build_glrun():
+    os.makedirs(REFBIN, exist_ok=True)
+    out = os.path.join(REFBIN, "glrun")
+    sh(["gcc", "-O2", "-o", out, os.path.join(HERE, "glrun.c"), "-ldl"])
+    return out
+
+
+def cam_args(cfg, cfgs):
+    c = cfg["camera"] or cfgs["default_camera"]
+    v = list(c["origin"]) + list(c["lookat"]) + [c["fov"], c["aperture"], c["focalLength"]]
+    return ["--cam"] + ["%r" % float(x) for x in v]
+
+
+def parse_host_state(state):
+    """defines/constants strings -> {name: value} (no reference text kept)."""
+    defs = {}
+    for d in state["defines"]:
+        name = d.split("#define")[1].strip()
+        defs[name] = not d.lstrip().startswith("//")
+    consts = {}
+    for c in state["constants"]:
+        lhs, rhs = c.split("=")
+        name = lhs.split()[-1]
+        v = rhs.strip().rstrip(";").strip()
+        consts[name] = True if v == "true" else False if v == "false" else (float(v) if "." in v else int(v))
+    return defs, consts
+
+
+def run_config(glrun, cfgs, cfg):
+    name = cfg["name"]
+    frag = os.path.join(GEN, name + ".frag")
+    st = sh(["node", os.path.join(HERE, "make_shader.js"), os.path.join(GOLD, "configs.json"), name, frag])
+    defs, consts = parse_host_state(json.loads(st.stdout))
+    frames = int(cfg["frames"])
+    restir = bool(defs.get("USE_RESTIR"))
+    prefix = os.path.join(GEN, name)
+    cmd = [glrun, "--frag", frag, "--w", str(W), "--h", str(H), "--frames", str(frames),
+           "--single", "--out", prefix] + cam_args(cfg, cfgs)
+    if restir:
+        cmd.append("--restir-out")
+    sh(cmd, timeout=1800)
+
+    def load(tag):
+        return np.stack([np.fromfile("%s_f%d_%s.bin" % (prefix, k, tag), dtype=np.float32).reshape(H, W, 4)
+                         for k in range(1, frames + 1)])
+
+    out = {"samples": load("c")}
+    if restir:
+        out["restir_main"] = load("r")
+        out["restir_aux"] = load("a")
+    np.savez_compressed(os.path.join(GOLD, name + ".npz"), **out)
+    nan = int(np.isnan(out["samples"][..., :3]).any(axis=-1).sum())
+    return {"defines": defs, "constants": consts, "frames": frames, "width": W, "height": H,
+            "restir": restir, "nan_pixels": nan,
+            "mean_rgb": [float(x) for x in np.nanmean(out["samples"][..., :3], axis=(0, 1, 2))]}
+
+
+def run_kat(glrun, cfgs):
+    frag = os.path.join(GEN, "rng_kat.frag")
+    sh(["node", os.path.join(HERE, "make_shader.js"), os.path.join(GOLD, "configs.json"),
+        "c1_cornell_cos", frag, "--kat"])
+    prefix = os.path.join(GEN, "rng_kat")
+    frames = 3
+    sh([glrun, "--frag", frag, "--w", str(W), "--h", str(H), "--frames", str(frames), "--single",
+        "--restir-out", "--out", prefix] + cam_args(cfgs["configs"][0], cfgs))
+    arr = {}
+    for tag in "cra":
+        arr["kat_" + tag] = np.stack([np.fromfile("%s_f%d_%s.bin" % (prefix, k, tag), dtype=np.float32)
+                                      .reshape(H, W, 4) for k in range(1, frames + 1)])
+    np.savez_compressed(os.path.join(GOLD, "rng_kat.npz"), **arr)
+
+
+def main():
+    cfgs = json.load(open(os.path.join(GOLD, "configs.json")))
+    only = set(sys.argv[1:])
+    glrun = build_glrun()
+    os.makedirs(GEN, exist_ok=True)
+    man_path = os.path.join(GOLD, "manifest.json")
+    manifest = json.load(open(man_path)) if os.path.exists(man_path) else {}
+    manifest["_generator"] = ("oracle/gen/make_golden.py: reference raytracer.glsl expanded by the reference's "
+                              "parseShader (tools.js:22-61) + GlslViewport defaults (index.js), executed by "
+                              "SwiftShader 4.1 GLES3 (kaleido bundle) via oracle/gen/glrun.c; single-sample "
+                              "passes (u_bufferA = 0), 64x64, unpatched powerHeuristic")
+    manifest.setdefault("configs", {})
+    if not only or "rng_kat" in only:
+        run_kat(glrun, cfgs)
+    for cfg in cfgs["configs"]:
+        if only and cfg["name"] not in only:
+            continue
+        info = run_config(glrun, cfgs, cfg)
+        manifest["configs"][cfg["name"]] = info
+        print(cfg["name"], info["nan_pixels"], info["mean_rgb"], flush=True)
+    json.dump(manifest, open(man_path, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
