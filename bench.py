@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py -- Msamples/s of the rt0 HIP integrator on BASELINE.json's workload.
+
+Workload (BASELINE.json configs[1], SURVEY 8d "C2"): 1024x1024 Cornell box
+(index.js:54-85, camera index.js:89-95), MIS power heuristic on, 8 bounces
+(MAX_BOUNCES = MAX_DIFF_BOUNCES = 8: a true 8-bounce path; the reference's
+default MAX_DIFF_BOUNCES=4 variant is reported beside it), 64 spp.
+One step = one 64-pass progressive render of the whole image (u_frame 1..64,
+i.e. 64 GlslViewport.render() calls) with scene + accumulator resident in HBM.
+
+N GPUs (one process per GPU, torch.distributed.run): the image is split into
+16-row bands dealt round-robin over ranks (rt0_set_shard); each rank renders
+its bands into a torch-owned accumulator and rank 0 gathers the bands over
+RCCL inside the timed region ("strong" scaling: total work fixed).
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with
+`roofline` (VALU FP32: algorithmic FLOP/sample from SURVEY 8d x counted events,
+over the kernel's HIP-event time) and `cpu_baseline` (the C restatement
+oracle/rt0_oracle.c, OpenMP on host cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "raytracer-0_amd"))
+sys.path.insert(0, os.path.join(HERE, "oracle"))
+
+import numpy as np  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
+PEAK_HBM_GBS = 8000.0
+W = H = 1024
+SPP = 64
+
+
+def flop_per_sample(c, mis=True):
+    """SURVEY 8d algorithmic FLOP model: 140 + 150*isect + 130*iter + (140+54*mis)*nee per sample."""
+    n = max(1, c["samples"])
+    return 140.0 + 150.0 * c["isect"] / n + 130.0 * c["iter"] / n + (140.0 + 54.0 * mis) * c["nee"] / n
+
+
+def cpu_baseline(cfgs, cfg, budget_s=12.0):
+    """Time the C restatement (OpenMP, all host threads we are allowed) on a
+    bounded sample of the same workload: full-width 1024 rows x a band of rows,
+    8-bounce MIS passes, scaled by samples."""
+    import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    rows = 64
+    o = O.Oracle(cfg, cfgs, width=W, height=H)
+    o.frame(1, rows=(480, 480 + 8), threads=threads)  # warm
+    n = 0
+    t0 = time.time()
+    while time.time() - t0 < budget_s:
+        o.frame(1 + n, rows=(480, 480 + rows), threads=threads)
+        n += 1
+    dt = time.time() - t0
+    samples = n * rows * W
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": "oracle/rt0_oracle.c (OpenMP x%d), rows 480..%d of the 1024^2 bench image, %d passes "
+                      "(%d samples, %.1f s)" % (threads, 480 + rows, n, samples, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2_cornell_mis_8")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", action="store_true", help="also time the MAX_DIFF_BOUNCES=4 variant")
+    args = ap.parse_args()
+
+    import torch
+    import rt0
+    import oracle as O
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")  # RCCL on ROCm
+    cfgs = O.load_configs()
+    cfg = [c for c in cfgs["configs"] if c["name"] == args.config][0]
+
+    r = rt0.Renderer(W, H, device=local)
+    rt0.configure(r, cfg, cfgs)
+    band = 16
+    nb = H // band
+    owned = [b for b in range(nb) if b % world == rank]
+    acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
+    r.set_accum_buffer(acc.data_ptr())
+    if world > 1:
+        r.set_shard(rank, world, band)
+        own_idx = torch.tensor(owned, device=acc.device)
+        max_owned = (nb + world - 1) // world
+        gather_bufs = [torch.zeros((max_owned, band, W, 4), device=acc.device) for _ in range(world)] \
+            if rank == 0 else None
+        image = torch.zeros((H, W, 4), device=acc.device) if rank == 0 else None
+
+    def step(frame0):
+        acc.zero_()
+        torch.cuda.synchronize()
+        r.render(frame0, SPP)  # synchronous: returns after the kernels finished
+        if world > 1:
+            send = torch.zeros((max_owned, band, W, 4), device=acc.device)
+            send[:len(owned)] = acc.view(nb, band, W, 4).index_select(0, own_idx)
+            dist.gather(send, gather_bufs, dst=0)
+            if rank == 0:
+                for src in range(world):
+                    ob = [b for b in range(nb) if b % world == src]
+                    image.view(nb, band, W, 4)[ob] = gather_bufs[src][:len(ob)]
+
+    for i in range(args.warmup):
+        step(1)
+    kernel_ms = []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(1)
+        kernel_ms.append(r.last_kernel_ms()[0])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=acc.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt * 1000.0 / args.steps
+    total_samples = W * H * SPP * args.steps
+    value = total_samples / dt / 1e6
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    # algorithmic FLOPs of the dominant kernel: counted events of the same
+    # workload (separate counting kernel instance, outside the timed region)
+    r.set_counting(True)
+    acc.zero_()
+    r.render(1, SPP)
+    cnt = r.counters()
+    r.set_counting(False)
+    fps = flop_per_sample(cnt)
+    owned_samples = len(owned) * band * W * SPP
+    kern_s = float(np.mean(kernel_ms)) / 1000.0
+    achieved_tflops = fps * owned_samples / kern_s / 1e12
+    out = {
+        "metric": "Msamples/sec (pixels x spp / s) at 1024^2 Cornell, 8 bounces",
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (the reference's own Cornell scene, index.js:54-85; no external data)",
+        "config": {"workload": "%s: 1024x1024 Cornell, MIS power heuristic, MAX_BOUNCES=8, MAX_DIFF_BOUNCES=%d, "
+                               "64 spp per step (u_frame 1..64)" % (args.config, cfg["constants"].get(
+                                   "MAX_DIFF_BOUNCES", 4)),
+                   "width": W, "height": H, "spp": SPP, "parallelism": "row-band x%d (16-row bands)" % world},
+        "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_FP32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                     "flop_per_sample": round(fps, 1),
+                     "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3)
+                                           for k in ("isect", "iter", "nee")},
+                     "kernel_ms_per_launch": round(kern_s * 1000.0, 3),
+                     "hbm_bytes_per_launch": W * H * 16 * 2 // world,
+                     "note": "FP32 vector kernel (no MFMA): peak = MI355X FP32 vector 157.3 TF; "
+                             "FLOP model SURVEY 8d x counted events"},
+    }
+    if args.secondary:
+        sec = [c for c in cfgs["configs"] if c["name"] == "c2_cornell_mis_refcaps"][0]
+        rt0.configure(r, sec, cfgs)
+        acc.zero_()
+        r.render(1, SPP)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            acc.zero_()
+            r.render(1, SPP)
+        out["secondary_refcaps_Msamples_s"] = round(W * H * SPP * args.steps / (time.perf_counter() - t1) / 1e6 *
+                                                    (world if world > 1 else 1), 3)
+    if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
+        out["cpu_baseline"] = cpu_baseline(cfgs, cfg)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

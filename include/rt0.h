@@ -1,0 +1,177 @@
+/*
+ * rt0.h -- C ABI of the MI355X (gfx950) path-tracing backend for raytracer-0.
+ *
+ * Drop-in boundary.  The reference drives its integrator through WebGL2
+ * (index.js `class GlslViewport`): compile-time strings spliced into the shader
+ * by parseShader (tools.js:22-61), per-pass uniforms and one gl.drawArrays per
+ * pass (index.js:986-1105).  This header replaces that GL boundary with plain
+ * C entry points; a GlslViewport-compatible host class (JS over N-API, or
+ * Python over ctypes) calls them.  Every function returns RT0_OK (0) or a
+ * negative RT0_E* code; rt0_last_error() gives the message.  Handles are not
+ * reentrant; calls are synchronous unless stated.
+ *
+ * Pixel layout everywhere: RGBA32F, row-major, row 0 = bottom row
+ * (gl_FragCoord.y = 0.5), exactly what glReadPixels returns in the reference.
+ */
+#ifndef RT0_H
+#define RT0_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT0_OK 0
+#define RT0_E_ARG (-1)     /* bad argument / parse error */
+#define RT0_E_HIP (-2)     /* HIP runtime failure */
+#define RT0_E_UNSUPPORTED (-3) /* feature outside the supported set */
+#define RT0_E_STATE (-4)   /* call order (e.g. render before set_scene) */
+
+/* defines[] flags, index.js:11-19 (same order) */
+#define RT0_USE_CUBEMAP (1u << 0)
+#define RT0_USE_PROCEDURAL_SKY (1u << 1)
+#define RT0_USE_BIASED_SAMPLING (1u << 2)
+#define RT0_USE_BIDIRECTIONAL (1u << 3)
+#define RT0_USE_RESTIR (1u << 4)
+#define RT0_USE_SPECTRAL (1u << 5)
+#define RT0_USE_VOLUMETRICS (1u << 6)
+
+/* constants[], index.js:21-35 (same order and meaning) */
+typedef struct rt0_config {
+  uint32_t defines;            /* RT0_USE_* bits */
+  int32_t max_bounces;         /* MAX_BOUNCES */
+  int32_t max_diff_bounces;    /* MAX_DIFF_BOUNCES */
+  int32_t max_spec_bounces;    /* MAX_SPEC_BOUNCES */
+  int32_t max_trans_bounces;   /* MAX_TRANS_BOUNCES */
+  int32_t max_scattering_events; /* MAX_SCATTERING_EVENTS */
+  int32_t marching_steps;      /* MARCHING_STEPS */
+  float fudge_factor;          /* FUDGE_FACTOR */
+  int32_t sample_lights;       /* sample_lights */
+  int32_t use_mis;             /* use_mis */
+  int32_t use_restir;          /* use_restir */
+  int32_t light_path_length;   /* LIGHT_PATH_LENGTH (unused by the integrator) */
+  int32_t restir_samples;      /* RESTIR_SAMPLES */
+  int32_t render_mode;         /* RENDER_MODE (0 = progressive; 1 unsupported) */
+} rt0_config;
+
+/* Mesh record = the reference's `Mesh` struct (raytracer.glsl:239-244) with its
+ * `Material` (157-163) flattened.  type: 0 SPHERE 1 PLANE 2 BOX 3 SDF.
+ * mat_type: 0 LIGHT 1 DIR_LIGHT 2 DIFF 3 SPEC 4 REFR_FRESNEL 5 REFR_SCHLICK 6 COAT.
+ * tex_type: -1 = NULL_TEX (the only value supported so far).
+ * sdf_kind (type == SDF only): the index.html:702-717 selector value
+ * (0 sdBox 1 udRoundBox 2 sdSphere 3 sdTriPrism 4 sdCone 5 MengerSponge 6 Mandelbulb). */
+typedef struct rt0_mesh {
+  float c[3];
+  float e[3];
+  float nt;
+  int32_t mat_type;
+  int32_t tex_type;
+  int32_t type;
+  float pos[3];
+  float joker[4];
+  int32_t sdf_kind;
+} rt0_mesh;
+
+typedef struct rt0_ctx rt0_ctx;
+
+/* Replaces `new GlslViewport(canvas, opts)` (index.js:4-382): allocates the
+ * accumulator + ReSTIR buffers for a width x height canvas on `device`, with
+ * GlslViewport's default defines/constants/camera (index.js:11-35, 89-95). */
+int rt0_create(int width, int height, int device, rt0_ctx **out);
+void rt0_destroy(rt0_ctx *ctx);
+const char *rt0_last_error(const rt0_ctx *ctx);
+
+/* Parses GlslViewport's `defines` / `constants` string arrays (index.js:11-35,
+ * the text parseShader splices at `#constants`) into *out. */
+int rt0_parse_config(const char *const *defines, int n_defines, const char *const *constants,
+                     int n_constants, rt0_config *out);
+/* Replaces the recompile after a defines/constants change (index.html:1167-1196). */
+int rt0_set_config(rt0_ctx *ctx, const rt0_config *cfg);
+int rt0_get_config(const rt0_ctx *ctx, rt0_config *out);
+
+/* Replaces `#scene` + `#sdf_meshes` substitution (tools.js:48-55): parses
+ * GlslViewport.scene (the GLSL `Mesh[]` / `light_index[]` text of index.js:54-85
+ * or index.html:657-676) and the sdf_meshes statements (index.html:702-717). */
+int rt0_set_scene_glsl(rt0_ctx *ctx, const char *scene_text, const char *const *sdf_meshes, int n_sdf);
+/* Same from already-flattened records; meshes[0..n_meshes) are Euclidean,
+ * meshes[n_meshes..n_meshes+n_sdfs) SDFs; light_index as in the GLSL scene. */
+int rt0_set_scene(rt0_ctx *ctx, const rt0_mesh *meshes, int n_meshes, int n_sdfs, const int32_t *light_index,
+                  int n_lights);
+/* Pure parser (no device needed): scene text + sdf statements -> records.
+ * Fails with RT0_E_ARG if max_meshes / max_lights are too small. */
+int rt0_parse_scene_glsl(const char *scene_text, const char *const *sdf_meshes, int n_sdf, rt0_mesh *meshes,
+                         int max_meshes, int *n_meshes, int *n_sdfs, int32_t *light_index, int max_lights,
+                         int *n_lights);
+int rt0_get_scene(const rt0_ctx *ctx, rt0_mesh *meshes, int max_meshes, int *n_meshes, int *n_sdfs,
+                  int32_t *light_index, int max_lights, int *n_lights);
+
+/* Uniforms u_camPos, u_camLookAt (a direction), u_camParams = (fov deg,
+ * aperture, focal length) (index.js:421-423). */
+int rt0_set_camera(rt0_ctx *ctx, const float pos[3], const float lookat[3], const float params[3]);
+
+/* Replaces n_passes consecutive GlslViewport.render() calls (index.js:986-1105)
+ * with u_frame = first_frame .. first_frame+n_passes-1: each pass adds one
+ * sample per pixel to the accumulator (raytracer.glsl:2168) and, with ReSTIR,
+ * rotates the reservoir swap chain (index.js:795-820).  Synchronous. */
+int rt0_render(rt0_ctx *ctx, uint32_t first_frame, int n_passes, float time_ms);
+/* Asynchronous variant on the context's stream; rt0_sync() waits. */
+int rt0_render_async(rt0_ctx *ctx, uint32_t first_frame, int n_passes, float time_ms);
+int rt0_sync(rt0_ctx *ctx);
+
+/* Host copy of the accumulator (W*H*4 floats). */
+int rt0_read_accum(rt0_ctx *ctx, float *rgba_out);
+/* Host copy into / out of the accumulator (resume from a checkpoint). */
+int rt0_write_accum(rt0_ctx *ctx, const float *rgba_in);
+/* Replaces clear() (index.js:822-880): zero accumulator + all reservoirs. */
+int rt0_clear(rt0_ctx *ctx);
+/* Replaces resize() (index.js:471-493); contents are cleared. */
+int rt0_resize(rt0_ctx *ctx, int width, int height);
+int rt0_get_size(const rt0_ctx *ctx, int *width, int *height);
+
+/* Display epilogue, tonemapper.glsl:28-33: rgba8 = 255*pow(acc*cont, 1/2.2),
+ * alpha 255, cont = 1/passes (index.js:1089). */
+int rt0_tonemap(rt0_ctx *ctx, float contribution, uint8_t *rgba8_out);
+
+/* ReSTIR reservoir MRTs (raytracer.glsl:2171-2179).  which: 0 = current output
+ * (restir_buffer/aux of the last pass), 1 = history1, 2 = history2.  main/aux:
+ * W*H*4 floats each. */
+int rt0_read_restir(rt0_ctx *ctx, int which, float *main_out, float *aux_out);
+/* Set the six ReSTIR inputs the NEXT pass reads (spatial = restir_buffer_back,
+ * history1, history2; main+aux each); any pointer may be NULL = zeros. */
+int rt0_write_restir_inputs(rt0_ctx *ctx, const float *spatial_main, const float *spatial_aux,
+                            const float *h1_main, const float *h1_aux, const float *h2_main,
+                            const float *h2_aux);
+
+/* Pixel sharding for multi-GPU: this context renders only rows
+ * r with (r / band) % n_shards == shard.  Its accumulator stays full-size;
+ * rows it does not own are left untouched. */
+int rt0_set_shard(rt0_ctx *ctx, int shard, int n_shards, int band_rows);
+
+/* Device pointer of the accumulator (W*H*4 f32, hipMalloc'd, owned by ctx) and
+ * the HIP stream used for kernels, for zero-copy collectives by the caller. */
+int rt0_device_accum(rt0_ctx *ctx, void **dptr, void **stream);
+/* Use a caller-owned device buffer (W*H*4 f32 on the ctx's device, e.g. a
+ * torch tensor that RCCL gathers) as the accumulator; NULL restores the
+ * context's own buffer.  Contents are not cleared. */
+int rt0_set_accum_buffer(rt0_ctx *ctx, void *dptr);
+
+/* Event counters of the last rt0_render call when enabled: [0] intersection()
+ * calls, [1] radiance-loop iterations, [2] light-sampling (NEE) calls,
+ * [3] map() evaluations, [4] samples.  Counting uses a separate kernel
+ * instance; it never runs in a timed render unless enabled. */
+int rt0_set_counting(rt0_ctx *ctx, int enable);
+int rt0_read_counters(rt0_ctx *ctx, uint64_t out[5]);
+
+/* Wall time of the kernels of the last rt0_render (HIP events on the
+ * context's stream), milliseconds, and the number of kernel launches. */
+int rt0_last_kernel_ms(const rt0_ctx *ctx, float *ms, int *launches);
+
+/* Library version string. */
+const char *rt0_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT0_H */

@@ -31,7 +31,7 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 GOLD = os.path.join(REPO, "tests", "golden")
 GEN = os.path.join(REPO, "oracle", "_gen")
 REFBIN = os.path.join(REPO, "oracle", "_ref")
-W = H = 64
+W = H = 64  # default fixture size; configs may set "fixture_size"
 
 
 def sh(cmd, **kw):
@@ -72,6 +72,7 @@ def run_config(glrun, cfgs, cfg):
     st = sh(["node", os.path.join(HERE, "make_shader.js"), os.path.join(GOLD, "configs.json"), name, frag])
     defs, consts = parse_host_state(json.loads(st.stdout))
     frames = int(cfg["frames"])
+    W, H = cfg.get("fixture_size", [64, 64])
     restir = bool(defs.get("USE_RESTIR"))
     prefix = os.path.join(GEN, name)
     cmd = [glrun, "--frag", frag, "--w", str(W), "--h", str(H), "--frames", str(frames),
@@ -128,7 +129,10 @@ def main():
         if only and cfg["name"] not in only:
             continue
         info = run_config(glrun, cfgs, cfg)
-        manifest["configs"][cfg["name"]] = info
+        # re-read so that concurrent generator runs (one per slow config) merge
+        manifest = json.load(open(man_path)) if os.path.exists(man_path) else manifest
+        manifest.setdefault("configs", {})[cfg["name"]] = info
+        json.dump(manifest, open(man_path, "w"), indent=1, sort_keys=True)
         print(cfg["name"], info["nan_pixels"], info["mean_rgb"], flush=True)
     json.dump(manifest, open(man_path, "w"), indent=1, sort_keys=True)
 

@@ -172,6 +172,24 @@ function main() {
   const n1 = src.split('const Mesh meshes[').length - 1;
   if (n1 !== 1) throw new Error('expected exactly one `const Mesh meshes[`, found ' + n1);
   src = src.replace('const Mesh meshes[', 'Mesh meshes[');
+  // 3. iBox / iSDF leave their `out` normal (and iSDF its `out` index) unassigned
+  //    on a miss (raytracer.glsl:836-859, 974-993).  GLSL makes such values
+  //    undefined; SwiftShader copies out a stale register, which after the first
+  //    SDF hit turns every later SDF miss into hit.index = NUM_MESHES (black
+  //    images for every scene mixing quadrics and SDFs).  Declaring them `inout`
+  //    pins the undefined value to "caller's value unchanged" -- the behaviour
+  //    intersection() relies on (it pre-sets hit = HIT_MISS, 998) and the one the
+  //    Cornell fixtures already exhibit.
+  const patches = [
+    ['bool iBox(const Mesh box, in Ray r, in float tmin, out float t, out vec3 n){',
+     'bool iBox(const Mesh box, in Ray r, in float tmin, out float t, inout vec3 n){'],
+    ['bool iSDF(in Ray r, in float tmin, out float t, out vec3 n, out int index){',
+     'bool iSDF(in Ray r, in float tmin, out float t, inout vec3 n, inout int index){'],
+  ];
+  for (const [from, to] of patches) {
+    if (src.split(from).length !== 2) throw new Error('patch target not found: ' + from);
+    src = src.replace(from, to);
+  }
   if (nanfix) {
     const needle = 'return max(0.0, (f * f) / denom);';
     if (src.split(needle).length !== 2) throw new Error('powerHeuristic pattern not found');

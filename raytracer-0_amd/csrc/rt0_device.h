@@ -1,0 +1,80 @@
+// rt0_device.h -- data layout shared by the host library and the gfx950 kernels.
+//
+// HBM layout (one context):
+//   SceneDev  (one struct, ~9 KiB): geometry records, material records,
+//             light_index, sdf kinds.  Read with wave-uniform indices only, so
+//             the compiler emits scalar (s_load) fetches: the scene never
+//             occupies VGPRs or vector-memory bandwidth.
+//   accum     W*H float4 (RGBA32F), row 0 = bottom row.
+//   ReSTIR    8 W*H float4 planes: out main/aux, spatial-in main/aux,
+//             history1 main/aux, history2 main/aux (index.js:125-221 swap chain
+//             kept as pointer rotation on the host).
+#pragma once
+#include <stdint.h>
+
+#define RT0_MAX_MESH 128
+#define RT0_MAX_LIGHTS 128
+
+// Geometry half of raytracer.glsl's `Mesh` (239-244), 32 B.  Derived fields
+// are exact rewrites of the reference's per-test arithmetic:
+//   SPHERE: r2 = joker.x*joker.x (iSphere, 821)
+//   PLANE : negd = -joker.x (iPlane, 813)
+//   BOX   : half = joker.x*0.5 (a power-of-two scale: (|m|*jx)*0.5 == |m|*(jx*0.5))
+struct GeomRec {
+  float px, py, pz;
+  float j0;      // joker.x (0 => skipped, raytracer.glsl:1009)
+  int32_t type;  // 0 SPHERE 1 PLANE 2 BOX 3 SDF
+  float d0;      // r2 / negd / half
+  float j1, j2;  // joker.y, joker.z
+};
+
+// Material half, 32 B.  c/e are the raw material colours; the integrator
+// applies max(.,0.001) where the reference does (raytracer.glsl:2071, 2077).
+struct MatRec {
+  float cr, cg, cb;
+  int32_t type;  // 0 LIGHT 1 DIR_LIGHT 2 DIFF 3 SPEC 4 REFR_FRESNEL 5 REFR_SCHLICK 6 COAT
+  float er, eg, eb;
+  float nt;
+};
+
+struct SceneDev {
+  int32_t n_meshes, n_sdfs, n_lights, n_total;
+  GeomRec geom[RT0_MAX_MESH];
+  MatRec mat[RT0_MAX_MESH];
+  float j3[RT0_MAX_MESH];  // joker.w (udRoundBox radius)
+  int32_t sdf_kind[RT0_MAX_MESH];
+  int32_t light_index[RT0_MAX_LIGHTS];
+};
+
+// Feature flags resolved on the host (runtime, wave-uniform).
+enum : uint32_t {
+  F_SKY = 1u << 0,
+  F_BIASED = 1u << 1,
+  F_SAMPLE_LIGHTS = 1u << 2,
+  F_MIS = 1u << 3,
+  F_RESTIR = 1u << 4,      // use_restir constant
+  F_RESTIR_DEF = 1u << 5,  // #define USE_RESTIR
+  F_SPECTRAL = 1u << 6,
+  F_VOL = 1u << 7,
+};
+
+struct LaunchParams {
+  int32_t width, height;
+  uint32_t frame0;
+  int32_t nframes;
+  float res_x, res_y, aspect;
+  float cam_px, cam_py, cam_pz;
+  float ux, uy, uz, vx, vy, vz, wx, wy, wz;
+  float uULen, uVLen, aperture, focal;
+  uint32_t flags;
+  int32_t max_bounces, max_diff, max_spec, max_trans, max_scatter, marching_steps;
+  float fudge;
+  int32_t restir_samples;
+  int32_t shard, n_shards, band;  // row-band sharding
+  int32_t n_band_rows;            // rows covered by this launch's grid (host-computed)
+  const SceneDev *scene;
+  float4 *accum;
+  const float4 *rin[6];  // spatial main/aux, history1 main/aux, history2 main/aux
+  float4 *rout_main, *rout_aux;
+  unsigned long long *counters;  // 5 x u64 (counting instance only)
+};

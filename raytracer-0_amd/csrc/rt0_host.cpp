@@ -1,0 +1,554 @@
+// rt0_host.cpp -- the C ABI of include/rt0.h over HIP.
+//
+// Replaces GlslViewport's GL plumbing (index.js:4-1105): device buffers instead
+// of textures, kernel launches instead of gl.drawArrays, pointer rotation for
+// the ReSTIR swap chain (index.js:795-820) and the accumulator ping-pong.
+// Product code: there is no CPU fallback -- without a HIP device every render
+// entry point fails with RT0_E_HIP.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt0.h"
+#include "rt0_device.h"
+#include "rt0_internal.h"
+
+extern "C" hipError_t rt0_launch_pass(int variant, const LaunchParams *p, dim3 grid, hipStream_t stream);
+extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, float cont, hipStream_t stream);
+
+enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
+
+struct rt0_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int W = 0, H = 0;
+  rt0_config cfg{};
+  bool has_scene = false;
+  std::vector<rt0_mesh> meshes;
+  int n_meshes = 0, n_sdfs = 0;
+  std::vector<int32_t> lights;
+  SceneDev *d_scene = nullptr;
+  float cam_pos[3] = {0.f, 0.f, 2.8f}, cam_look[3] = {0.f, 0.f, -1.f}, cam_params[3] = {50.f, 0.f, 3.5f};
+  float4 *d_accum = nullptr;
+  float4 *ext_accum = nullptr;  // caller-owned accumulator (rt0_set_accum_buffer)
+  float4 *acc() const { return ext_accum ? ext_accum : d_accum; }
+  float4 *d_restir[R_COUNT] = {};
+  uchar4 *d_tonemap = nullptr;
+  unsigned long long *d_counters = nullptr;
+  bool counting = false;
+  uint64_t counters[5] = {};
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  float last_ms = 0.f;
+  int last_launches = 0;
+  int shard = 0, n_shards = 1, band = 16;
+  int max_frames_per_launch = 64;
+  std::string err;
+};
+
+static int fail(rt0_ctx *c, int code, const std::string &msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPCHK(c, expr)                                                                 \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail((c), RT0_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static void free_buffers(rt0_ctx *c) {
+  if (c->d_accum) (void)hipFree(c->d_accum);
+  for (auto &p : c->d_restir)
+    if (p) (void)hipFree(p), p = nullptr;
+  if (c->d_tonemap) (void)hipFree(c->d_tonemap);
+  c->d_accum = nullptr;
+  c->d_tonemap = nullptr;
+}
+
+static int alloc_buffers(rt0_ctx *c, int w, int h) {
+  size_t n = (size_t)w * h;
+  HIPCHK(c, hipMalloc(&c->d_accum, n * sizeof(float4)));
+  for (auto &p : c->d_restir) HIPCHK(c, hipMalloc(&p, n * sizeof(float4)));
+  HIPCHK(c, hipMalloc(&c->d_tonemap, n * sizeof(uchar4)));
+  c->W = w;
+  c->H = h;
+  return RT0_OK;
+}
+
+static int clear_buffers(rt0_ctx *c) {
+  size_t n = (size_t)c->W * c->H * sizeof(float4);
+  HIPCHK(c, hipMemsetAsync(c->acc(), 0, n, c->stream));
+  for (auto &p : c->d_restir) HIPCHK(c, hipMemsetAsync(p, 0, n, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT0_OK;
+}
+
+extern "C" {
+
+const char *rt0_version(void) { return "rt0-mi355x 0.1 (gfx950)"; }
+
+int rt0_create(int width, int height, int device, rt0_ctx **out) {
+  if (!out || width <= 0 || height <= 0) return RT0_E_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT0_E_HIP;
+  if (device < 0 || device >= ndev) return RT0_E_ARG;
+  rt0_ctx *c = new rt0_ctx();
+  c->device = device;
+  rt0h::default_config(c->cfg);
+  int rc;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipMalloc(&c->d_scene, sizeof(SceneDev)) != hipSuccess ||
+      hipMalloc(&c->d_counters, 5 * sizeof(unsigned long long)) != hipSuccess) {
+    rt0_destroy(c);
+    return RT0_E_HIP;
+  }
+  if ((rc = alloc_buffers(c, width, height)) != RT0_OK || (rc = clear_buffers(c)) != RT0_OK) {
+    rt0_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return RT0_OK;
+}
+
+void rt0_destroy(rt0_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_buffers(c);
+  if (c->d_scene) (void)hipFree(c->d_scene);
+  if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char *rt0_last_error(const rt0_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int rt0_parse_config(const char *const *defines, int nd, const char *const *constants, int nc, rt0_config *out) {
+  if (!out || nd < 0 || nc < 0) return RT0_E_ARG;
+  std::string err;
+  return rt0h::parse_config(defines, nd, constants, nc, *out, err);
+}
+
+int rt0_set_config(rt0_ctx *c, const rt0_config *cfg) {
+  if (!c || !cfg) return RT0_E_ARG;
+  if (cfg->defines & RT0_USE_CUBEMAP) return fail(c, RT0_E_UNSUPPORTED, "USE_CUBEMAP is not supported yet");
+  if (cfg->render_mode != 0) return fail(c, RT0_E_UNSUPPORTED, "RENDER_MODE 1 (animated) is not supported");
+  if (cfg->max_bounces < 0 || cfg->marching_steps < 0) return fail(c, RT0_E_ARG, "negative loop bound");
+  c->cfg = *cfg;
+  return RT0_OK;
+}
+
+int rt0_get_config(const rt0_ctx *c, rt0_config *out) {
+  if (!c || !out) return RT0_E_ARG;
+  *out = c->cfg;
+  return RT0_OK;
+}
+
+static int upload_scene(rt0_ctx *c) {
+  SceneDev s;
+  memset(&s, 0, sizeof s);
+  s.n_meshes = c->n_meshes;
+  s.n_sdfs = c->n_sdfs;
+  s.n_lights = (int)c->lights.size();
+  s.n_total = c->n_meshes + c->n_sdfs;
+  for (int i = 0; i < s.n_total; i++) {
+    const rt0_mesh &m = c->meshes[i];
+    GeomRec &g = s.geom[i];
+    g.px = m.pos[0];
+    g.py = m.pos[1];
+    g.pz = m.pos[2];
+    g.j0 = m.joker[0];
+    g.j1 = m.joker[1];
+    g.j2 = m.joker[2];
+    g.type = m.type;
+    g.d0 = m.type == 0 ? m.joker[0] * m.joker[0] : m.type == 1 ? -m.joker[0] : m.joker[0] * 0.5f;
+    s.j3[i] = m.joker[3];
+    s.sdf_kind[i] = m.sdf_kind;
+    MatRec &r = s.mat[i];
+    r.cr = m.c[0];
+    r.cg = m.c[1];
+    r.cb = m.c[2];
+    r.er = m.e[0];
+    r.eg = m.e[1];
+    r.eb = m.e[2];
+    r.nt = m.nt;
+    r.type = m.mat_type;
+  }
+  for (int i = 0; i < s.n_lights; i++) s.light_index[i] = c->lights[i];
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(c->d_scene, &s, sizeof s, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->has_scene = true;
+  return RT0_OK;
+}
+
+static int validate_and_store(rt0_ctx *c, const rt0_mesh *m, int ne, int ns, const int32_t *li, int nl) {
+  if (ne < 0 || ns < 0 || nl < 0) return fail(c, RT0_E_ARG, "negative count");
+  if (ne + ns > RT0_MAX_MESH) return fail(c, RT0_E_UNSUPPORTED, "too many meshes");
+  if (nl > RT0_MAX_LIGHTS) return fail(c, RT0_E_UNSUPPORTED, "too many lights");
+  if (ne + ns == 0) return fail(c, RT0_E_ARG, "empty scene");  // meshes[hit.index] needs meshes[0]
+  for (int i = 0; i < ne + ns; i++) {
+    if (m[i].tex_type != -1) return fail(c, RT0_E_UNSUPPORTED, "textured materials are not supported yet");
+    bool sdf = m[i].type == 3;
+    if ((i < ne) == sdf) return fail(c, RT0_E_ARG, "meshes[0..n_meshes) must be Euclidean, the rest SDF");
+    if (!sdf && (m[i].type < 0 || m[i].type > 2)) return fail(c, RT0_E_UNSUPPORTED, "unsupported mesh type");
+    if (sdf && (m[i].sdf_kind < 0 || m[i].sdf_kind > 6)) return fail(c, RT0_E_ARG, "bad sdf_kind");
+    if (m[i].mat_type < -1 || m[i].mat_type > 6) return fail(c, RT0_E_ARG, "bad material type");
+  }
+  for (int i = 0; i < nl; i++)
+    if (li[i] >= ne + ns) return fail(c, RT0_E_ARG, "light_index out of range");
+  c->meshes.assign(m, m + ne + ns);
+  c->n_meshes = ne;
+  c->n_sdfs = ns;
+  c->lights.assign(li, li + nl);
+  return upload_scene(c);
+}
+
+int rt0_set_scene(rt0_ctx *c, const rt0_mesh *meshes, int n_meshes, int n_sdfs, const int32_t *light_index,
+                  int n_lights) {
+  if (!c || (!meshes && n_meshes + n_sdfs > 0) || (!light_index && n_lights > 0)) return RT0_E_ARG;
+  return validate_and_store(c, meshes, n_meshes, n_sdfs, light_index, n_lights);
+}
+
+int rt0_set_scene_glsl(rt0_ctx *c, const char *scene_text, const char *const *sdf_meshes, int n_sdf) {
+  if (!c) return RT0_E_ARG;
+  std::vector<rt0_mesh> m;
+  std::vector<int32_t> l;
+  int ne = 0, ns = 0;
+  std::string err;
+  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, l, err);
+  if (rc != RT0_OK) return fail(c, rc, err);
+  return validate_and_store(c, m.data(), ne, ns, l.data(), (int)l.size());
+}
+
+int rt0_parse_scene_glsl(const char *scene_text, const char *const *sdf_meshes, int n_sdf, rt0_mesh *meshes,
+                         int max_meshes, int *n_meshes, int *n_sdfs, int32_t *light_index, int max_lights,
+                         int *n_lights) {
+  std::vector<rt0_mesh> m;
+  std::vector<int32_t> l;
+  int ne = 0, ns = 0;
+  std::string err;
+  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, l, err);
+  if (rc != RT0_OK) return rc;
+  if ((int)m.size() > max_meshes || (int)l.size() > max_lights) return RT0_E_ARG;
+  for (size_t i = 0; i < m.size(); i++) meshes[i] = m[i];
+  for (size_t i = 0; i < l.size(); i++) light_index[i] = l[i];
+  if (n_meshes) *n_meshes = ne;
+  if (n_sdfs) *n_sdfs = ns;
+  if (n_lights) *n_lights = (int)l.size();
+  return RT0_OK;
+}
+
+int rt0_get_scene(const rt0_ctx *c, rt0_mesh *meshes, int max_meshes, int *n_meshes, int *n_sdfs,
+                  int32_t *light_index, int max_lights, int *n_lights) {
+  if (!c) return RT0_E_ARG;
+  if (!c->has_scene) return RT0_E_STATE;
+  int n = c->n_meshes + c->n_sdfs;
+  if (n_meshes) *n_meshes = c->n_meshes;
+  if (n_sdfs) *n_sdfs = c->n_sdfs;
+  if (n_lights) *n_lights = (int)c->lights.size();
+  if (meshes)
+    for (int i = 0; i < n && i < max_meshes; i++) meshes[i] = c->meshes[i];
+  if (light_index)
+    for (int i = 0; i < (int)c->lights.size() && i < max_lights; i++) light_index[i] = c->lights[i];
+  return RT0_OK;
+}
+
+int rt0_set_camera(rt0_ctx *c, const float pos[3], const float lookat[3], const float params[3]) {
+  if (!c || !pos || !lookat || !params) return RT0_E_ARG;
+  memcpy(c->cam_pos, pos, sizeof c->cam_pos);
+  memcpy(c->cam_look, lookat, sizeof c->cam_look);
+  memcpy(c->cam_params, params, sizeof c->cam_params);
+  return RT0_OK;
+}
+
+int rt0_set_shard(rt0_ctx *c, int shard, int n_shards, int band_rows) {
+  if (!c || n_shards < 1 || shard < 0 || shard >= n_shards || band_rows < 1) return RT0_E_ARG;
+  if (band_rows % 16) return fail(c, RT0_E_ARG, "band_rows must be a multiple of 16");
+  c->shard = shard;
+  c->n_shards = n_shards;
+  c->band = band_rows;
+  return RT0_OK;
+}
+
+static void fill_params(rt0_ctx *c, LaunchParams &p) {
+  memset(&p, 0, sizeof p);
+  const rt0_config &g = c->cfg;
+  p.width = c->W;
+  p.height = c->H;
+  p.res_x = (float)c->W;
+  p.res_y = (float)c->H;
+  p.aspect = p.res_x / p.res_y;
+  p.cam_px = c->cam_pos[0];
+  p.cam_py = c->cam_pos[1];
+  p.cam_pz = c->cam_pos[2];
+  // camera basis, raytracer.glsl:2127-2133 (float, same operation order)
+  float lx = c->cam_look[0], ly = c->cam_look[1], lz = c->cam_look[2];
+  float il = 1.0f / sqrtf(lx * lx + ly * ly + lz * lz);
+  float wx = lx * il, wy = ly * il, wz = lz * il;
+  float cx = wy * 0.0f - 1.0f * wz, cy = wz * 0.0f - 0.0f * wx, cz = wx * 1.0f - 0.0f * wy;  // cross(w, (0,1,0))
+  float ic = 1.0f / sqrtf(cx * cx + cy * cy + cz * cz);
+  float ux = cx * ic, uy = cy * ic, uz = cz * ic;
+  p.ux = ux;
+  p.uy = uy;
+  p.uz = uz;
+  p.vx = uy * wz - wy * uz;
+  p.vy = uz * wx - wz * ux;
+  p.vz = ux * wy - wx * uy;
+  p.wx = wx;
+  p.wy = wy;
+  p.wz = wz;
+  float theta = c->cam_params[0] * 0.01745329f;
+  p.uVLen = tanf(theta * 0.5f);
+  p.uULen = p.aspect * p.uVLen;
+  p.aperture = c->cam_params[1];
+  p.focal = c->cam_params[2];
+  uint32_t f = 0;
+  if (g.defines & RT0_USE_PROCEDURAL_SKY) f |= F_SKY;
+  if (g.defines & RT0_USE_BIASED_SAMPLING) f |= F_BIASED;
+  if (g.sample_lights) f |= F_SAMPLE_LIGHTS;
+  if (g.use_mis) f |= F_MIS;
+  if (g.use_restir) f |= F_RESTIR;
+  if (g.defines & RT0_USE_RESTIR) f |= F_RESTIR_DEF;
+  if (g.defines & RT0_USE_SPECTRAL) f |= F_SPECTRAL;
+  if (g.defines & RT0_USE_VOLUMETRICS) f |= F_VOL;
+  p.flags = f;
+  p.max_bounces = g.max_bounces;
+  p.max_diff = g.max_diff_bounces;
+  p.max_spec = g.max_spec_bounces;
+  p.max_trans = g.max_trans_bounces;
+  p.max_scatter = g.max_scattering_events;
+  p.marching_steps = g.marching_steps;
+  p.fudge = g.fudge_factor;
+  p.restir_samples = g.restir_samples;
+  p.shard = c->shard;
+  p.n_shards = c->n_shards;
+  p.band = c->band;
+  int total_bands = (c->H + c->band - 1) / c->band;
+  int owned = total_bands / c->n_shards + (c->shard < total_bands % c->n_shards ? 1 : 0);
+  p.n_band_rows = owned * c->band;
+  p.scene = c->d_scene;
+  p.accum = c->acc();
+  p.counters = c->d_counters;
+}
+
+static int choose_variant(const rt0_ctx *c) {
+  const rt0_config &g = c->cfg;
+  if (c->counting) return 4;
+  if (g.defines & RT0_USE_RESTIR) return 3;
+  if (g.defines & (RT0_USE_VOLUMETRICS | RT0_USE_SPECTRAL)) return 2;
+  if (c->n_sdfs > 0) return 1;
+  return 0;
+}
+
+static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
+  if (!c || n < 0) return RT0_E_ARG;
+  if (!c->has_scene) return fail(c, RT0_E_STATE, "rt0_render before rt0_set_scene*");
+  if (c->cfg.defines & RT0_USE_CUBEMAP) return fail(c, RT0_E_UNSUPPORTED, "USE_CUBEMAP is not supported yet");
+  const bool restir = (c->cfg.defines & RT0_USE_RESTIR) != 0;
+  if (restir && c->n_shards > 1) return fail(c, RT0_E_UNSUPPORTED, "ReSTIR with row sharding is not supported yet");
+  HIPCHK(c, hipSetDevice(c->device));
+  LaunchParams p;
+  fill_params(c, p);
+  if (p.n_band_rows == 0 || n == 0) {
+    c->last_ms = 0.f;
+    c->last_launches = 0;
+    return RT0_OK;
+  }
+  const int variant = choose_variant(c);
+  dim3 grid((c->W + 15) / 16, (p.n_band_rows + 15) / 16);
+  if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 5 * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  int launches = 0;
+  if (restir) {
+    for (int k = 0; k < n; k++) {
+      p.frame0 = first + (uint32_t)k;
+      p.nframes = 1;
+      p.rin[0] = c->d_restir[R_BACK_MAIN];
+      p.rin[1] = c->d_restir[R_BACK_AUX];
+      p.rin[2] = c->d_restir[R_H1];
+      p.rin[3] = c->d_restir[R_H1A];
+      p.rin[4] = c->d_restir[R_H2];
+      p.rin[5] = c->d_restir[R_H2A];
+      p.rout_main = c->d_restir[R_OUT_MAIN];
+      p.rout_aux = c->d_restir[R_OUT_AUX];
+      HIPCHK(c, rt0_launch_pass(variant, &p, grid, c->stream));
+      launches++;
+      // swapReSTIRBuffers, index.js:795-820
+      float4 **R = c->d_restir;
+      float4 *o2 = R[R_H2], *o2a = R[R_H2A];
+      R[R_H2] = R[R_H1];
+      R[R_H2A] = R[R_H1A];
+      R[R_H1] = R[R_BACK_MAIN];
+      R[R_H1A] = R[R_BACK_AUX];
+      R[R_BACK_MAIN] = o2;
+      R[R_BACK_AUX] = o2a;
+      float4 *tm = R[R_OUT_MAIN], *ta = R[R_OUT_AUX];
+      R[R_OUT_MAIN] = R[R_BACK_MAIN];
+      R[R_OUT_AUX] = R[R_BACK_AUX];
+      R[R_BACK_MAIN] = tm;
+      R[R_BACK_AUX] = ta;
+    }
+  } else {
+    for (int k = 0; k < n; k += c->max_frames_per_launch) {
+      p.frame0 = first + (uint32_t)k;
+      p.nframes = (n - k) < c->max_frames_per_launch ? (n - k) : c->max_frames_per_launch;
+      HIPCHK(c, rt0_launch_pass(variant, &p, grid, c->stream));
+      launches++;
+    }
+  }
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->last_launches = launches;
+  if (sync) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+    if (c->counting) {
+      unsigned long long h[5];
+      HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+      for (int i = 0; i < 5; i++) c->counters[i] = h[i];
+    }
+  }
+  return RT0_OK;
+}
+
+int rt0_render(rt0_ctx *c, uint32_t first, int n, float time_ms) {
+  (void)time_ms;  // u_time only feeds RENDER_MODE 1 (getAnimatedPosition, raytracer.glsl:263-298)
+  return render_impl(c, first, n, true);
+}
+
+int rt0_render_async(rt0_ctx *c, uint32_t first, int n, float time_ms) {
+  (void)time_ms;
+  return render_impl(c, first, n, false);
+}
+
+int rt0_sync(rt0_ctx *c) {
+  if (!c) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->last_launches) HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  if (c->counting) {
+    unsigned long long h[5];
+    HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 5; i++) c->counters[i] = h[i];
+  }
+  return RT0_OK;
+}
+
+int rt0_read_accum(rt0_ctx *c, float *out) {
+  if (!c || !out) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, c->acc(), (size_t)c->W * c->H * sizeof(float4), hipMemcpyDeviceToHost));
+  return RT0_OK;
+}
+
+int rt0_write_accum(rt0_ctx *c, const float *in) {
+  if (!c || !in) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(c->acc(), in, (size_t)c->W * c->H * sizeof(float4), hipMemcpyHostToDevice));
+  return RT0_OK;
+}
+
+int rt0_clear(rt0_ctx *c) {
+  if (!c) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  return clear_buffers(c);
+}
+
+int rt0_resize(rt0_ctx *c, int w, int h) {
+  if (!c || w <= 0 || h <= 0) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  free_buffers(c);
+  c->ext_accum = nullptr;  // a caller buffer has the old size
+  int rc = alloc_buffers(c, w, h);
+  if (rc != RT0_OK) return rc;
+  return clear_buffers(c);
+}
+
+int rt0_get_size(const rt0_ctx *c, int *w, int *h) {
+  if (!c) return RT0_E_ARG;
+  if (w) *w = c->W;
+  if (h) *h = c->H;
+  return RT0_OK;
+}
+
+int rt0_tonemap(rt0_ctx *c, float contribution, uint8_t *out) {
+  if (!c || !out) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  int n = c->W * c->H;
+  HIPCHK(c, rt0_launch_tonemap(c->acc(), c->d_tonemap, n, contribution, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, c->d_tonemap, (size_t)n * sizeof(uchar4), hipMemcpyDeviceToHost));
+  return RT0_OK;
+}
+
+int rt0_read_restir(rt0_ctx *c, int which, float *main_out, float *aux_out) {
+  if (!c || which < 0 || which > 2) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // after the swap, the last pass's output sits in restir_buffer_back (index.js:817-819)
+  const int mi = which == 0 ? R_BACK_MAIN : which == 1 ? R_H1 : R_H2;
+  size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+  if (main_out) HIPCHK(c, hipMemcpy(main_out, c->d_restir[mi], bytes, hipMemcpyDeviceToHost));
+  if (aux_out) HIPCHK(c, hipMemcpy(aux_out, c->d_restir[mi + 1], bytes, hipMemcpyDeviceToHost));
+  return RT0_OK;
+}
+
+int rt0_write_restir_inputs(rt0_ctx *c, const float *sm, const float *sa, const float *h1m, const float *h1a,
+                            const float *h2m, const float *h2a) {
+  if (!c) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+  const float *src[6] = {sm, sa, h1m, h1a, h2m, h2a};
+  const int dst[6] = {R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A};
+  for (int i = 0; i < 6; i++) {
+    if (src[i]) HIPCHK(c, hipMemcpy(c->d_restir[dst[i]], src[i], bytes, hipMemcpyHostToDevice));
+    else HIPCHK(c, hipMemset(c->d_restir[dst[i]], 0, bytes));
+  }
+  return RT0_OK;
+}
+
+int rt0_device_accum(rt0_ctx *c, void **dptr, void **stream) {
+  if (!c) return RT0_E_ARG;
+  if (dptr) *dptr = c->acc();
+  if (stream) *stream = c->stream;
+  return RT0_OK;
+}
+
+int rt0_set_accum_buffer(rt0_ctx *c, void *dptr) {
+  if (!c) return RT0_E_ARG;
+  c->ext_accum = (float4 *)dptr;
+  return RT0_OK;
+}
+
+int rt0_set_counting(rt0_ctx *c, int enable) {
+  if (!c) return RT0_E_ARG;
+  c->counting = enable != 0;
+  return RT0_OK;
+}
+
+int rt0_read_counters(rt0_ctx *c, uint64_t out[5]) {
+  if (!c || !out) return RT0_E_ARG;
+  for (int i = 0; i < 5; i++) out[i] = c->counters[i];
+  return RT0_OK;
+}
+
+int rt0_last_kernel_ms(const rt0_ctx *c, float *ms, int *launches) {
+  if (!c) return RT0_E_ARG;
+  if (ms) *ms = c->last_ms;
+  if (launches) *launches = c->last_launches;
+  return RT0_OK;
+}
+
+}  // extern "C"

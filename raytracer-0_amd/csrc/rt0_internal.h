@@ -1,0 +1,17 @@
+// rt0_internal.h -- declarations shared by the host-side translation units.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt0.h"
+
+namespace rt0h {
+int lookup_material(const std::string &name, rt0_mesh &m);
+int parse_scene_glsl(const char *text, const char *const *sdf, int n_sdf, std::vector<rt0_mesh> &meshes,
+                     int &n_euclid, int &n_sdfs, std::vector<int32_t> &lights, std::string &err);
+void default_config(rt0_config &c);
+int parse_config(const char *const *defines, int nd, const char *const *constants, int nc, rt0_config &c,
+                 std::string &err);
+}  // namespace rt0h

@@ -1,0 +1,446 @@
+"""rt0 -- Python host for the MI355X raytracer-0 backend (ctypes over include/rt0.h).
+
+`GlslViewport` mirrors the reference host class (index.js:3-1105): the same
+public fields (defines, constants, scene, sdf_meshes, camera, passes,
+max_passes) and methods (render, clear, resize, setAnimatedMode,
+updateFrontTarget).  Scene/flag strings use the reference's own grammar, so a
+caller written against the reference can drive this backend unchanged.  The
+integrator itself runs only in the HIP kernels of librt0.so: there is no CPU
+fallback, and every entry point raises if the library or a GPU is missing.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librt0.so")
+
+RT0_OK = 0
+ERRORS = {-1: "RT0_E_ARG", -2: "RT0_E_HIP", -3: "RT0_E_UNSUPPORTED", -4: "RT0_E_STATE"}
+
+DEFINE_NAMES = ["USE_CUBEMAP", "USE_PROCEDURAL_SKY", "USE_BIASED_SAMPLING", "USE_BIDIRECTIONAL",
+                "USE_RESTIR", "USE_SPECTRAL", "USE_VOLUMETRICS"]
+
+# C symbols declared by include/rt0.h (checked by tests/test_abi.py)
+EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "rt0_set_config", "rt0_get_config",
+           "rt0_set_scene_glsl", "rt0_set_scene", "rt0_parse_scene_glsl", "rt0_get_scene", "rt0_set_camera", "rt0_render",
+           "rt0_render_async", "rt0_sync", "rt0_read_accum", "rt0_write_accum", "rt0_clear", "rt0_resize",
+           "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
+           "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_counting", "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version"]
+
+
+class Rt0Error(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (ERRORS.get(code, code), msg))
+        self.code = code
+
+
+class Config(ctypes.Structure):
+    """rt0_config, field order = constants[] of index.js:21-35."""
+    _fields_ = [("defines", ctypes.c_uint32), ("max_bounces", ctypes.c_int32), ("max_diff_bounces", ctypes.c_int32),
+                ("max_spec_bounces", ctypes.c_int32), ("max_trans_bounces", ctypes.c_int32),
+                ("max_scattering_events", ctypes.c_int32), ("marching_steps", ctypes.c_int32),
+                ("fudge_factor", ctypes.c_float), ("sample_lights", ctypes.c_int32), ("use_mis", ctypes.c_int32),
+                ("use_restir", ctypes.c_int32), ("light_path_length", ctypes.c_int32),
+                ("restir_samples", ctypes.c_int32), ("render_mode", ctypes.c_int32)]
+
+
+class Mesh(ctypes.Structure):
+    _fields_ = [("c", ctypes.c_float * 3), ("e", ctypes.c_float * 3), ("nt", ctypes.c_float),
+                ("mat_type", ctypes.c_int32), ("tex_type", ctypes.c_int32), ("type", ctypes.c_int32),
+                ("pos", ctypes.c_float * 3), ("joker", ctypes.c_float * 4), ("sdf_kind", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    """Load librt0.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("librt0.so not built (run `make -C raytracer-0_amd` or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    c_void_p, c_int, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    fp = P(ctypes.c_float)
+    sig = {
+        "rt0_create": (c_int, [c_int, c_int, c_int, P(c_void_p)]),
+        "rt0_destroy": (None, [c_void_p]),
+        "rt0_last_error": (ctypes.c_char_p, [c_void_p]),
+        "rt0_parse_config": (c_int, [P(ctypes.c_char_p), c_int, P(ctypes.c_char_p), c_int, P(Config)]),
+        "rt0_set_config": (c_int, [c_void_p, P(Config)]),
+        "rt0_get_config": (c_int, [c_void_p, P(Config)]),
+        "rt0_set_scene_glsl": (c_int, [c_void_p, ctypes.c_char_p, P(ctypes.c_char_p), c_int]),
+        "rt0_set_scene": (c_int, [c_void_p, P(Mesh), c_int, c_int, P(ctypes.c_int32), c_int]),
+        "rt0_parse_scene_glsl": (c_int, [ctypes.c_char_p, P(ctypes.c_char_p), c_int, P(Mesh), c_int, P(c_int),
+                                         P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
+        "rt0_get_scene": (c_int, [c_void_p, P(Mesh), c_int, P(c_int), P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
+        "rt0_set_camera": (c_int, [c_void_p, fp, fp, fp]),
+        "rt0_render": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
+        "rt0_render_async": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
+        "rt0_sync": (c_int, [c_void_p]),
+        "rt0_read_accum": (c_int, [c_void_p, fp]),
+        "rt0_write_accum": (c_int, [c_void_p, fp]),
+        "rt0_clear": (c_int, [c_void_p]),
+        "rt0_resize": (c_int, [c_void_p, c_int, c_int]),
+        "rt0_get_size": (c_int, [c_void_p, P(c_int), P(c_int)]),
+        "rt0_tonemap": (c_int, [c_void_p, c_float, P(ctypes.c_uint8)]),
+        "rt0_read_restir": (c_int, [c_void_p, c_int, fp, fp]),
+        "rt0_write_restir_inputs": (c_int, [c_void_p, fp, fp, fp, fp, fp, fp]),
+        "rt0_set_shard": (c_int, [c_void_p, c_int, c_int, c_int]),
+        "rt0_device_accum": (c_int, [c_void_p, P(c_void_p), P(c_void_p)]),
+        "rt0_set_accum_buffer": (c_int, [c_void_p, c_void_p]),
+        "rt0_set_counting": (c_int, [c_void_p, c_int]),
+        "rt0_read_counters": (c_int, [c_void_p, P(ctypes.c_uint64)]),
+        "rt0_last_kernel_ms": (c_int, [c_void_p, P(c_float), P(c_int)]),
+        "rt0_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _fp(a):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _strarr(items):
+    arr = (ctypes.c_char_p * max(1, len(items)))()
+    for i, s in enumerate(items):
+        arr[i] = s.encode()
+    return arr
+
+
+def parse_config(defines, constants):
+    """GlslViewport.defines/.constants string arrays -> Config (index.js:11-35)."""
+    cfg = Config()
+    rc = lib().rt0_parse_config(_strarr(defines), len(defines), _strarr(constants), len(constants),
+                                ctypes.byref(cfg))
+    if rc != RT0_OK:
+        raise Rt0Error(rc, "cannot parse defines/constants")
+    return cfg
+
+
+# ----------------------------------------------------------------- scene text
+def parse_scene(scene_text, sdf_meshes=()):
+    """Pure parse of GlslViewport.scene + .sdf_meshes -> (meshes, n_meshes, n_sdfs, light_index)."""
+    meshes = (Mesh * 128)()
+    lights = (ctypes.c_int32 * 128)()
+    ne, ns, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    sdf = list(sdf_meshes)
+    rc = lib().rt0_parse_scene_glsl(scene_text.encode(), _strarr(sdf), len(sdf), meshes, 128, ctypes.byref(ne),
+                                    ctypes.byref(ns), lights, 128, ctypes.byref(nl))
+    if rc != RT0_OK:
+        raise Rt0Error(rc, "cannot parse scene")
+    return list(meshes[:ne.value + ns.value]), ne.value, ns.value, list(lights[:nl.value])
+
+
+def scene_from_lines(lines):
+    """The scene textarea -> GLSL `#scene` text, as index.html:610-676 builds it.
+
+    Returns (scene_text, n_sdfs)."""
+    n_meshes = n_sdfs = n_models = 0
+    u_sphere = u_plane = u_box = False
+    lights, text = [], []
+    for i, line in enumerate(lines):
+        fields = line.split(",")
+        mat, typ = fields[0].strip(), fields[1].strip()
+        if mat.rfind("MAT_LIGHT") >= 0:
+            lights.append(i)
+        text.append("Mesh(" + line + ")" + ("," if i != len(lines) - 1 else ""))
+        if typ in ("SDF", "GRID_SDF"):
+            n_sdfs += 1
+        elif typ in ("PLANE", "SPHERE", "BOX"):
+            u_sphere |= typ == "SPHERE"
+            u_plane |= typ == "PLANE"
+            u_box |= typ == "BOX"
+            n_meshes += 1
+        elif typ == "TRIANGLE":
+            n_models += 1
+        else:
+            raise ValueError("There's no such thing as " + typ)
+    if not lights:
+        lights.append(-1)
+    b = lambda v: "true" if v else "false"  # noqa: E731
+    scene = ("const bool U_EUCLIDEAN = %s;\nconst bool U_SPHERE = %s;\nconst bool U_PLANE = %s;\n"
+             "const bool U_BOX = %s;\nconst bool U_SDF = %s;\n\nconst lowp int NUM_MESHES = %d;\n"
+             "const lowp int NUM_SDFS   = %d;\nconst lowp int NUM_MODELS = %d;\n\n"
+             "const Mesh meshes[NUM_MESHES + NUM_SDFS + NUM_MODELS] = Mesh[](\n%s\n);\n\n"
+             "const lowp int light_index[%d] = int[](\n%s\n);"
+             % (b(n_meshes > 0), b(u_sphere), b(u_plane), b(u_box), b(n_sdfs > 0), n_meshes, n_sdfs, n_models,
+                "\n".join(text), len(lights), ", ".join(str(x) for x in lights)))
+    return scene, n_sdfs
+
+
+SDF_PRIMS = ["sdBox", "udRoundBox", "sdSphere", "sdTriPrism", "sdCone", "MengerSponge", "Mandelbulb"]
+
+
+def sdf_statement(i, kind):
+    """index.html:702-717: SDF selector value -> the `#sdf_meshes` statement."""
+    m = "meshes[NUM_MESHES + %d]" % i
+    args = {0: "p-%s.pos, %s.joker.xyz" % (m, m), 1: "p-%s.pos, %s.joker.xyz, %s.joker.w" % (m, m, m),
+            2: "p-%s.pos, %s.joker.x" % (m, m), 3: "p-%s.pos, %s.joker.xy" % (m, m),
+            4: "p-%s.pos, %s.joker.xyz" % (m, m), 5: "p-%s.pos, %s.joker.xyz" % (m, m), 6: "p-%s.pos" % m}[kind]
+    return "sdf_meshes[%d] = vec2(%s(%s), %.4f);" % (i, SDF_PRIMS[kind], args, i)
+
+
+# ------------------------------------------------------------------ renderer
+class Renderer:
+    """Thin owner of one rt0 context (one GPU, one canvas)."""
+
+    def __init__(self, width, height, device=0):
+        h = ctypes.c_void_p()
+        rc = lib().rt0_create(width, height, device, ctypes.byref(h))
+        if rc != RT0_OK:
+            raise Rt0Error(rc, "rt0_create(%d, %d, device=%d) failed (no HIP device?)" % (width, height, device))
+        self.h = h
+        self.width, self.height = width, height
+
+    def _chk(self, rc):
+        if rc != RT0_OK:
+            raise Rt0Error(rc, lib().rt0_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rt0_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_config(self, cfg):
+        self._chk(lib().rt0_set_config(self.h, ctypes.byref(cfg)))
+
+    def get_config(self):
+        cfg = Config()
+        self._chk(lib().rt0_get_config(self.h, ctypes.byref(cfg)))
+        return cfg
+
+    def set_scene_glsl(self, scene_text, sdf_meshes=()):
+        sdf = list(sdf_meshes)
+        self._chk(lib().rt0_set_scene_glsl(self.h, scene_text.encode(), _strarr(sdf), len(sdf)))
+
+    def get_scene(self):
+        meshes = (Mesh * 128)()
+        lights = (ctypes.c_int32 * 128)()
+        ne, ns, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._chk(lib().rt0_get_scene(self.h, meshes, 128, ctypes.byref(ne), ctypes.byref(ns), lights, 128,
+                                      ctypes.byref(nl)))
+        return list(meshes[:ne.value + ns.value]), ne.value, ns.value, list(lights[:nl.value])
+
+    def set_camera(self, pos, lookat, params):
+        a = [np.asarray(v, np.float32) for v in (pos, lookat, params)]
+        self._chk(lib().rt0_set_camera(self.h, *[_fp(x) for x in a]))
+
+    def render(self, first_frame, n_passes, time_ms=0.0):
+        self._chk(lib().rt0_render(self.h, first_frame, n_passes, time_ms))
+
+    def render_async(self, first_frame, n_passes, time_ms=0.0):
+        self._chk(lib().rt0_render_async(self.h, first_frame, n_passes, time_ms))
+
+    def sync(self):
+        self._chk(lib().rt0_sync(self.h))
+
+    def read_accum(self):
+        out = np.empty((self.height, self.width, 4), np.float32)
+        self._chk(lib().rt0_read_accum(self.h, _fp(out)))
+        return out
+
+    def write_accum(self, a):
+        a = np.ascontiguousarray(a, np.float32)
+        self._chk(lib().rt0_write_accum(self.h, _fp(a)))
+
+    def clear(self):
+        self._chk(lib().rt0_clear(self.h))
+
+    def resize(self, w, h):
+        self._chk(lib().rt0_resize(self.h, w, h))
+        self.width, self.height = w, h
+
+    def tonemap(self, contribution):
+        out = np.empty((self.height, self.width, 4), np.uint8)
+        self._chk(lib().rt0_tonemap(self.h, contribution, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out
+
+    def read_restir(self, which=0):
+        m = np.empty((self.height, self.width, 4), np.float32)
+        a = np.empty_like(m)
+        self._chk(lib().rt0_read_restir(self.h, which, _fp(m), _fp(a)))
+        return m, a
+
+    def write_restir_inputs(self, spatial_main=None, spatial_aux=None, h1_main=None, h1_aux=None, h2_main=None,
+                            h2_aux=None):
+        arrs = [None if x is None else np.ascontiguousarray(x, np.float32)
+                for x in (spatial_main, spatial_aux, h1_main, h1_aux, h2_main, h2_aux)]
+        self._chk(lib().rt0_write_restir_inputs(self.h, *[_fp(x) for x in arrs]))
+
+    def set_shard(self, shard, n_shards, band_rows=16):
+        self._chk(lib().rt0_set_shard(self.h, shard, n_shards, band_rows))
+
+    def device_accum(self):
+        d, s = ctypes.c_void_p(), ctypes.c_void_p()
+        self._chk(lib().rt0_device_accum(self.h, ctypes.byref(d), ctypes.byref(s)))
+        return d.value, s.value
+
+    def set_accum_buffer(self, dptr):
+        """Use a caller-owned device buffer (e.g. torch tensor .data_ptr()) as accumulator."""
+        self._chk(lib().rt0_set_accum_buffer(self.h, ctypes.c_void_p(dptr) if dptr else None))
+
+    def set_counting(self, on):
+        self._chk(lib().rt0_set_counting(self.h, int(bool(on))))
+
+    def counters(self):
+        out = (ctypes.c_uint64 * 5)()
+        self._chk(lib().rt0_read_counters(self.h, out))
+        return dict(zip(("isect", "iter", "nee", "map", "samples"), list(out)))
+
+    def last_kernel_ms(self):
+        ms, n = ctypes.c_float(), ctypes.c_int()
+        self._chk(lib().rt0_last_kernel_ms(self.h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+class Vector3:
+    """vector.js:2-95 (the camera only needs x/y/z)."""
+
+    def __init__(self, x=0.0, y=0.0, z=0.0):
+        self.x, self.y, self.z = x, y, z
+
+    def tolist(self):
+        return [self.x, self.y, self.z]
+
+
+class GlslViewport:
+    """Drop-in for the reference's GlslViewport (index.js:3-1105) on the rt0 backend.
+
+    Fields and defaults follow index.js:4-103; `render()` is one pass
+    (u_frame = ++passes) exactly like index.js:986-1105, `render(n)` batches n
+    passes into one kernel launch sequence.  Changing defines/constants/scene/
+    sdf_meshes takes effect at the next render() (the reference needs an
+    explicit recompile, index.html:1167)."""
+
+    def __init__(self, canvas=None, opts=None, device=0):
+        opts = opts or {}
+        self.width = opts.get("width", 600)
+        self.height = opts.get("height", 600)
+        self.tile_rendering = opts.get("tile_rendering", False)
+        self.defines = ["//#define USE_CUBEMAP", "#define USE_PROCEDURAL_SKY", "#define USE_BIASED_SAMPLING",
+                        "//#define USE_BIDIRECTIONAL", "//#define USE_RESTIR", "//#define USE_SPECTRAL",
+                        "//#define USE_VOLUMETRICS"]
+        self.constants = list(STATIC_CONSTANTS)
+        self.animatedConstants = list(ANIMATED_CONSTANTS)
+        self.scene, _ = scene_from_lines(CORNELL_LINES)
+        self.sdf_meshes = []
+        self.camera = {"origin": Vector3(0.0, 0.0, 2.8), "lookat": Vector3(0.0, 0.0, -1.0), "fov": 50.0,
+                       "aperture": 0.0, "focalLength": 3.5}
+        self.passes = 0
+        self.max_passes = opts.get("max_passes", float("inf"))
+        self.animatedScene = False
+        self.temporalFrames = 5
+        self.renderer = Renderer(self.width, self.height, device)
+        self._compiled = None
+
+    # index.js:384-440 -- uploads camera; here also (re)applies scene + flags
+    def updateFrontTarget(self):
+        key = (tuple(self.defines), tuple(self.constants), self.scene, tuple(self.sdf_meshes))
+        if key != self._compiled:
+            self.renderer.set_config(parse_config(self.defines, self.constants))
+            self.renderer.set_scene_glsl(self.scene, self.sdf_meshes)
+            self._compiled = key
+        c = self.camera
+        self.renderer.set_camera(c["origin"].tolist(), c["lookat"].tolist(),
+                                 [c["fov"], c["aperture"], c["focalLength"]])
+
+    def render(self, n_passes=1):
+        """index.js:986-1105: u_frame = ++passes per pass; accumulate."""
+        self.updateFrontTarget()
+        first = self.passes + 1
+        self.renderer.render(first, n_passes, 0.0)
+        self.passes += n_passes
+
+    def clear(self):
+        """index.js:822-880."""
+        self.renderer.clear()
+
+    def resize(self, v):
+        """index.js:471-493: v selects 256..8192 square canvases."""
+        size = {0: 256, 1: 512, 2: 1024, 3: 2048, 4: 4096, 5: 8192}.get(v, v)
+        self.width = self.height = size
+        self.renderer.resize(size, size)
+        self.passes = 0
+
+    def setAnimatedMode(self, is_animated):
+        """index.js:940-983 (animated mode itself is RENDER_MODE 1: unsupported)."""
+        self.animatedScene = bool(is_animated)
+        if is_animated:
+            self.constants = list(self.animatedConstants)
+            self.defines[4] = "#define USE_RESTIR"
+        else:
+            self.constants = list(STATIC_CONSTANTS)
+            self.defines[4] = "//#define USE_RESTIR"
+        self.clear()
+
+    def accumulator(self):
+        return self.renderer.read_accum()
+
+    def image(self):
+        """Display pass, tonemapper.glsl:28-33 with u_cont = 1/passes (index.js:1089)."""
+        return self.renderer.tonemap(1.0 / max(1, self.passes))
+
+
+STATIC_CONSTANTS = ["const lowp int MAX_BOUNCES = 12;", "const lowp int MAX_DIFF_BOUNCES = 4;",
+                    "const lowp int MAX_SPEC_BOUNCES = 4;", "const lowp int MAX_TRANS_BOUNCES = 12;",
+                    "const lowp int MAX_SCATTERING_EVENTS = 12;", "const mediump int MARCHING_STEPS = 128;",
+                    "const lowp float FUDGE_FACTOR = 0.9;", "const bool sample_lights = true;",
+                    "const bool use_mis = false;", "const bool use_restir = false;",
+                    "const lowp int LIGHT_PATH_LENGTH = 2;", "const lowp int RESTIR_SAMPLES = 16;",
+                    "const lowp int RENDER_MODE = 0;"]
+ANIMATED_CONSTANTS = ["const lowp int MAX_BOUNCES = 6;", "const lowp int MAX_DIFF_BOUNCES = 2;",
+                      "const lowp int MAX_SPEC_BOUNCES = 2;", "const lowp int MAX_TRANS_BOUNCES = 4;",
+                      "const lowp int MAX_SCATTERING_EVENTS = 4;", "const mediump int MARCHING_STEPS = 64;",
+                      "const lowp float FUDGE_FACTOR = 0.9;", "const bool sample_lights = true;",
+                      "const bool use_mis = false;", "const bool use_restir = true;",
+                      "const lowp int LIGHT_PATH_LENGTH = 1;", "const lowp int RESTIR_SAMPLES = 8;",
+                      "const lowp int RENDER_MODE = 1;"]
+# index.js:54-85 default scene (Cornell box) in the textarea grammar
+CORNELL_LINES = ["MAT_CORNELL_WHITE, PLANE,  vec3( 0.0, 1.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)",
+                 "MAT_CORNELL_WHITE, PLANE,  vec3( 0.0,-1.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)",
+                 "MAT_CORNELL_WHITE, PLANE,  vec3( 0.0, 0.0, 1.0), vec4(2.5, 0.0, 0.0, 0.0)",
+                 "MAT_CORNELL_RED,   PLANE,  vec3( 1.0, 0.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)",
+                 "MAT_CORNELL_GREEN, PLANE,  vec3(-1.0, 0.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)",
+                 "MAT_LIGHT_4,       SPHERE, vec3( 0.0, 1.4,-1.2), vec4(0.3, 0.0, 0.0, 0.0)",
+                 "MAT_CORNELL_WHITE, BOX,    vec3( 0.5,-1.0,-1.8), vec4(1.0, 0.0, 0.0, 0.0)",
+                 "MAT_CORNELL_WHITE, BOX,    vec3(-0.45,-1.15,-1.3), vec4(0.7, 0.0, 0.0, 0.0)"]
+
+
+def configure(renderer, cfg, cfgs):
+    """Apply one tests/golden/configs.json entry (scene lines, overrides, camera) to a Renderer."""
+    d = ["//#define USE_CUBEMAP", "#define USE_PROCEDURAL_SKY", "#define USE_BIASED_SAMPLING",
+         "//#define USE_BIDIRECTIONAL", "//#define USE_RESTIR", "//#define USE_SPECTRAL", "//#define USE_VOLUMETRICS"]
+    for k, v in cfg.get("defines", {}).items():
+        d[DEFINE_NAMES.index(k)] = ("" if v else "//") + "#define " + k
+    consts = list(STATIC_CONSTANTS)
+    for k, v in cfg.get("constants", {}).items():
+        for i, s in enumerate(consts):
+            if (" %s " % k) in s:
+                val = ("true" if v else "false") if isinstance(v, bool) else str(v)
+                consts[i] = s.split("=")[0] + "= " + val + ";"
+                break
+        else:
+            raise KeyError(k)
+    renderer.set_config(parse_config(d, consts))
+    lines = cfg["scene_lines"] or cfgs["cornell_lines"]
+    scene, ns = scene_from_lines(lines)
+    kinds = cfg.get("sdf_kinds") or []
+    renderer.set_scene_glsl(scene, [sdf_statement(i, kinds[i] if i < len(kinds) else 0) for i in range(ns)])
+    cam = cfg.get("camera") or cfgs["default_camera"]
+    renderer.set_camera(cam["origin"], cam["lookat"], [cam["fov"], cam["aperture"], cam["focalLength"]])

@@ -1,0 +1,151 @@
+"""Parity of the HIP path (librt0.so through the C ABI) with the reference.
+
+* against the golden fixtures (the reference shader run by SwiftShader):
+  every config, single-sample passes 1..F, same tolerance as the oracle;
+* ReSTIR: conditional parity -- the reference's own reservoir buffers of passes
+  k-1..k-3 are uploaded through rt0_write_restir_inputs, pass k's radiance
+  must match;
+* against the CPU restatement at sizes the fixtures do not cover (128^2 bench
+  scene, 12-bounce volumetric C4 scene).
+All calls go through include/rt0.h; nothing here can fall back to the CPU.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import rt0
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REL_TOL = 1e-3
+# fraction of pixels allowed to differ (discrete flips from ulp-level
+# differences between gfx950 transcendentals and the reference executor's)
+BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol": 0.03, "menger_coat": 0.02,
+            "mis_demo_sdfbox": 0.02, "restir_mis_demo": 0.02, "c3_outdoor_restir": 0.01}
+
+
+def cfg_by_name(cfgs, name):
+    return [c for c in cfgs["configs"] if c["name"] == name][0]
+
+
+def pixel_match(got, ref):
+    nan = np.isnan(ref).any(-1)
+    d = np.abs(got - ref)
+    ok = (d <= REL_TOL * np.maximum(1.0, np.abs(ref))).all(-1) | nan
+    return ok, nan
+
+
+def make(cfgs, name, w, h):
+    r = rt0.Renderer(w, h)
+    rt0.configure(r, cfg_by_name(cfgs, name), cfgs)
+    return r
+
+
+def single(r, k):
+    r.clear()
+    r.render(k, 1)
+    return r.read_accum()
+
+
+def have(name):
+    return os.path.exists(os.path.join(GOLD, name + ".npz"))
+
+
+NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
+              "mis_demo_sdfbox", "menger_coat", "thinlens_glass", "c4_mandelbulb_vol", "spectral_vol"]
+
+
+@pytest.mark.parametrize("name", NON_RESTIR)
+def test_gpu_matches_reference_fixture(name, cfgs, gpu_required):
+    if not have(name):
+        pytest.skip("fixture not generated")
+    gold = np.load(os.path.join(GOLD, name + ".npz"))["samples"]
+    F, H, W = gold.shape[:3]
+    r = make(cfgs, name, W, H)
+    got = np.stack([single(r, k) for k in range(1, F + 1)])
+    ok, nan = pixel_match(got[..., :3], gold[..., :3])
+    bad = 1.0 - ok.mean()
+    assert bad <= BAD_FRAC.get(name, BAD_FRAC["default"]), "%s: %.4f of pixels differ" % (name, bad)
+    assert not np.isnan(got).any()
+    m = ~nan
+    g, s = gold[..., :3][m], got[..., :3][m]
+    assert abs(s.mean() - g.mean()) <= 5e-3 * max(1.0, abs(g.mean()))
+
+
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo"])
+def test_gpu_restir_conditional_parity(name, cfgs, gpu_required):
+    if not have(name):
+        pytest.skip("fixture not generated")
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    F, H, W = G["samples"].shape[:3]
+    r = make(cfgs, name, W, H)
+
+    def out(k, key):
+        return G[key][k - 1] if k >= 1 else None
+
+    for k in range(1, F + 1):
+        r.clear()
+        r.write_restir_inputs(out(k - 1, "restir_main"), out(k - 1, "restir_aux"), out(k - 2, "restir_main"),
+                              out(k - 2, "restir_aux"), out(k - 3, "restir_main"), out(k - 3, "restir_aux"))
+        r.render(k, 1)
+        ok, _ = pixel_match(r.read_accum()[..., :3], G["samples"][k - 1][..., :3])
+        assert 1.0 - ok.mean() <= BAD_FRAC.get(name, BAD_FRAC["default"]), (name, k, 1.0 - ok.mean())
+
+
+def test_gpu_restir_chain_matches_oracle_chain(cfgs, gpu_required):
+    """Unconditional multi-pass ReSTIR (the product's own swap chain) vs the
+    restatement's swap chain (GLSL semantics, no executor artefacts)."""
+    name = "c3_outdoor_restir"
+    cfg = cfg_by_name(cfgs, name)
+    o = O.Oracle(cfg, cfgs, width=64, height=64)
+    s_ref, m_ref, a_ref = o.frames_restir(4)
+    r = make(cfgs, name, 64, 64)
+    prev = np.zeros((64, 64, 4), np.float32)
+    for k in range(1, 5):
+        r.render(k, 1)
+        acc = r.read_accum()
+        sample = acc - prev
+        prev = acc
+        ok, _ = pixel_match(sample[..., :3], s_ref[k - 1][..., :3])
+        assert 1.0 - ok.mean() <= 0.03, (k, 1.0 - ok.mean())
+        m, a = r.read_restir(0)
+        okm, _ = pixel_match(m, m_ref[k - 1])
+        assert okm.mean() >= 0.95, (k, okm.mean())
+
+
+@pytest.mark.parametrize("name,size,frames", [("c2_cornell_mis_8", 128, 2), ("cornell_nee_plain", 96, 1),
+                                              ("c4_mandelbulb_vol", 48, 1)])
+def test_gpu_matches_oracle_beyond_fixtures(name, size, frames, cfgs, gpu_required):
+    cfg = cfg_by_name(cfgs, name)
+    over = {"MAX_BOUNCES": 12} if name == "c4_mandelbulb_vol" else {}
+    o = O.Oracle(cfg, cfgs, width=size, height=size, overrides=over)
+    r = rt0.Renderer(size, size)
+    cfg2 = dict(cfg)
+    cfg2["constants"] = dict(cfg["constants"], **over)
+    rt0.configure(r, cfg2, cfgs)
+    for k in range(1, frames + 1):
+        ref = o.frame(k)[0]
+        got = single(r, k)
+        ok, _ = pixel_match(got[..., :3], ref[..., :3])
+        assert 1.0 - ok.mean() <= 0.02, (name, k, 1.0 - ok.mean())
+
+
+def test_gpu_accumulation_is_sequential_sum(cfgs, gpu_required):
+    """In-kernel multi-pass accumulation == the reference's per-pass
+    `prev + sample` chain (raytracer.glsl:2168), bit for bit."""
+    r = make(cfgs, "c2_cornell_mis_8", 64, 64)
+    samples = [single(r, k) for k in range(1, 6)]
+    ref = np.zeros_like(samples[0])
+    for s in samples:
+        ref[..., :3] = ref[..., :3] + s[..., :3]
+    r.clear()
+    r.render(1, 5)
+    acc = r.read_accum()
+    assert np.array_equal(acc[..., :3], ref[..., :3])
+    # resumable: passes 1..2 then 3..5 == 1..5
+    r.clear()
+    r.render(1, 2)
+    r.render(3, 3)
+    assert np.array_equal(r.read_accum(), acc)

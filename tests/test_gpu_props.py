@@ -1,0 +1,103 @@
+"""Size-independent properties of the HIP path at BASELINE sizes (1024^2),
+where the CPU oracle would take minutes: determinism, shard/whole identity,
+accumulation chaining, finiteness, tonemap epilogue, API state errors."""
+import numpy as np
+import pytest
+
+import rt0
+
+pytestmark = pytest.mark.gpu
+
+
+def cfg_by_name(cfgs, name):
+    return [c for c in cfgs["configs"] if c["name"] == name][0]
+
+
+def test_determinism_and_sharding_bitwise(cfgs, gpu_required):
+    cfg = cfg_by_name(cfgs, "c2_cornell_mis_8")
+    r = rt0.Renderer(1024, 1024)
+    rt0.configure(r, cfg, cfgs)
+    r.render(1, 2)
+    a = r.read_accum()
+    r.clear()
+    r.render(1, 2)
+    assert np.array_equal(a, r.read_accum())
+    assert np.isfinite(a).all() and a[..., :3].mean() > 0.01
+    # 4 shards of 16-row bands, each rendering only its bands, summed == whole
+    parts = np.zeros_like(a)
+    for s in range(4):
+        rs = rt0.Renderer(1024, 1024)
+        rt0.configure(rs, cfg, cfgs)
+        rs.set_shard(s, 4, 16)
+        rs.render(1, 2)
+        p = rs.read_accum()
+        rows = np.array([(y // 16) % 4 == s for y in range(1024)])
+        assert not p[~rows].any()
+        parts[rows] = p[rows]
+        rs.close()
+    assert np.array_equal(parts, a)
+
+
+def test_odd_sizes_and_edges(cfgs, gpu_required):
+    cfg = cfg_by_name(cfgs, "c1_cornell_cos")
+    for w, h in ((1, 1), (17, 5), (130, 67)):
+        r = rt0.Renderer(w, h)
+        rt0.configure(r, cfg, cfgs)
+        r.render(1, 3)
+        a = r.read_accum()
+        assert a.shape == (h, w, 4) and np.isfinite(a).all()
+    r.render(1, 0)  # zero passes is a no-op
+    assert np.array_equal(r.read_accum(), a)
+
+
+def test_tonemap_epilogue(cfgs, gpu_required):
+    r = rt0.Renderer(32, 32)
+    rt0.configure(r, cfg_by_name(cfgs, "c2_cornell_mis_8"), cfgs)
+    r.render(1, 4)
+    acc = r.read_accum()
+    img = r.tonemap(0.25)
+    ref = np.clip(np.power(np.maximum(acc[..., :3] * 0.25, 0), 1 / 2.2), 0, 1) * 255
+    assert img.dtype == np.uint8 and (img[..., 3] == 255).all()
+    assert np.abs(img[..., :3].astype(np.float32) - ref).max() <= 1.0
+
+
+def test_state_errors(cfgs, gpu_required):
+    r = rt0.Renderer(16, 16)
+    with pytest.raises(rt0.Rt0Error) as e:
+        r.render(1, 1)
+    assert e.value.code == -4
+    cfg = rt0.parse_config(["#define USE_CUBEMAP"], [])
+    with pytest.raises(rt0.Rt0Error) as e:
+        r.set_config(cfg)
+    assert e.value.code == -3
+
+
+def test_glslviewport_drives_backend(cfgs, gpu_required):
+    vp = rt0.GlslViewport(None, {"width": 64, "height": 64})
+    vp.constants[0] = "const lowp int MAX_BOUNCES = 8;"
+    vp.constants[8] = "const bool use_mis = true;"
+    for _ in range(3):
+        vp.render()
+    assert vp.passes == 3
+    a = vp.accumulator()
+    r = rt0.Renderer(64, 64)
+    rt0.configure(r, cfg_by_name(cfgs, "c2_cornell_mis_refcaps"), cfgs)
+    r.render(1, 3)
+    assert np.array_equal(a, r.read_accum())
+    vp.resize(0)
+    assert vp.width == 256 and vp.passes == 0
+
+
+def test_counters_feed_flop_model(cfgs, gpu_required):
+    r = rt0.Renderer(64, 64)
+    rt0.configure(r, cfg_by_name(cfgs, "c2_cornell_mis_8"), cfgs)
+    r.set_counting(True)
+    r.render(1, 2)
+    c = r.counters()
+    assert c["samples"] == 64 * 64 * 2
+    assert 5 < c["isect"] / c["samples"] < 30 and 2 < c["iter"] / c["samples"] <= 8
+    counted = r.read_accum()
+    r.set_counting(False)
+    r.clear()
+    r.render(1, 2)
+    assert np.array_equal(counted, r.read_accum())

@@ -1,0 +1,122 @@
+"""Host-side logic on CPU: the C-ABI library loads and exports include/rt0.h,
+the defines/constants/scene parsers reproduce the reference's grammar, and the
+Python GlslViewport surface mirrors index.js.  No compute calls (no GPU here).
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import rt0
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    text = open(os.path.join(REPO, "include", "rt0.h")).read()
+    return sorted(set(re.findall(r"\b(rt0_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    L = rt0.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(rt0.EXPORTS) == syms
+    assert b"gfx950" in L.rt0_version()
+
+
+def test_create_fails_loudly_without_gpu_or_bad_args():
+    h = ctypes.c_void_p()
+    assert rt0.lib().rt0_create(0, 64, 0, ctypes.byref(h)) == -1
+    if not os.path.exists("/dev/kfd"):
+        with pytest.raises(rt0.Rt0Error):
+            rt0.Renderer(64, 64)
+
+
+def test_parse_config_reference_defaults():
+    vp_defines = ["//#define USE_CUBEMAP", "#define USE_PROCEDURAL_SKY", "#define USE_BIASED_SAMPLING",
+                  "//#define USE_BIDIRECTIONAL", "//#define USE_RESTIR", "//#define USE_SPECTRAL",
+                  "//#define USE_VOLUMETRICS"]
+    cfg = rt0.parse_config(vp_defines, rt0.STATIC_CONSTANTS)
+    assert cfg.defines == (1 << 1) | (1 << 2)
+    assert (cfg.max_bounces, cfg.max_diff_bounces, cfg.max_spec_bounces, cfg.max_trans_bounces) == (12, 4, 4, 12)
+    assert (cfg.max_scattering_events, cfg.marching_steps) == (12, 128)
+    assert abs(cfg.fudge_factor - 0.9) < 1e-7
+    assert (cfg.sample_lights, cfg.use_mis, cfg.use_restir, cfg.restir_samples, cfg.render_mode) == (1, 0, 0, 16, 0)
+    anim = rt0.parse_config(vp_defines, rt0.ANIMATED_CONSTANTS)
+    assert (anim.max_bounces, anim.use_restir, anim.render_mode, anim.marching_steps) == (6, 1, 1, 64)
+
+
+def test_parse_config_rejects_garbage():
+    with pytest.raises(rt0.Rt0Error):
+        rt0.parse_config(["#define USE_NOTHING"], [])
+    with pytest.raises(rt0.Rt0Error):
+        rt0.parse_config([], ["const lowp int NOT_A_CONSTANT = 3;"])
+
+
+def test_scene_parser_cornell(cfgs):
+    scene, ns = rt0.scene_from_lines(cfgs["cornell_lines"])
+    meshes, ne, nsdf, lights = rt0.parse_scene(scene, [])
+    assert (ne, nsdf, lights) == (8, 0, [5])
+    types = [m.type for m in meshes]
+    assert types == [1, 1, 1, 1, 1, 0, 2, 2]
+    assert list(meshes[5].e) == [4.0, 4.0, 4.0] and meshes[5].mat_type == 0
+    assert np.allclose(list(meshes[3].c), [0.7, 0.12, 0.05])
+    assert np.allclose(list(meshes[7].pos), [-0.45, -1.15, -1.3]) and meshes[7].joker[0] == np.float32(0.7)
+
+
+def test_scene_parser_handles_reference_comments_and_broadcast():
+    text = """// header comment
+const bool U_EUCLIDEAN = true;
+const Mesh meshes[NUM_MESHES + NUM_SDFS + NUM_MODELS] = Mesh[](
+    // Floor  (y = -1.5, normal up)
+    Mesh(MAT_CORNELL_WHITE, PLANE,  vec3( 0.0, 1.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)),
+    /* a light */ Mesh(MAT_LIGHT_4, SPHERE, vec3(0.0), vec4(0.3))
+);
+const lowp int light_index[1] = int[](1);"""
+    meshes, ne, ns, lights = rt0.parse_scene(text)
+    assert (ne, ns, lights) == (2, 0, [1])
+    assert list(meshes[1].pos) == [0.0, 0.0, 0.0] and list(meshes[1].joker) == [np.float32(0.3)] * 4
+
+
+def test_scene_parser_sdf_statements(cfgs):
+    cfg = [c for c in cfgs["configs"] if c["name"] == "c4_mandelbulb_vol"][0]
+    scene, ns = rt0.scene_from_lines(cfg["scene_lines"])
+    stm = [rt0.sdf_statement(i, cfg["sdf_kinds"][i]) for i in range(ns)]
+    assert stm[0] == "sdf_meshes[0] = vec2(Mandelbulb(p-meshes[NUM_MESHES + 0].pos), 0.0000);"
+    meshes, ne, nsdf, lights = rt0.parse_scene(scene, stm)
+    assert (ne, nsdf, lights) == (7, 1, [6])
+    assert meshes[7].type == 3 and meshes[7].sdf_kind == 6
+    for kind in range(7):
+        m, _, _, _ = rt0.parse_scene(scene, [rt0.sdf_statement(0, kind)])
+        assert m[7].sdf_kind == kind
+
+
+def test_scene_parser_errors():
+    with pytest.raises(rt0.Rt0Error):
+        rt0.parse_scene("Mesh(MAT_NOPE, PLANE, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);")
+    with pytest.raises(rt0.Rt0Error) as e:
+        rt0.parse_scene("Mesh(MAT_WHITE, TRIANGLE, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);")
+    assert e.value.code == -3
+    # SDF mesh without a #sdf_meshes statement
+    with pytest.raises(rt0.Rt0Error):
+        rt0.parse_scene("Mesh(MAT_WHITE, SDF, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);", [])
+
+
+def test_no_lights_gives_minus_one(cfgs):
+    cfg = [c for c in cfgs["configs"] if c["name"] == "menger_coat"][0]
+    scene, ns = rt0.scene_from_lines(cfg["scene_lines"])
+    assert "int[](\n-1\n)" in scene
+    _, ne, nsdf, lights = rt0.parse_scene(scene, [rt0.sdf_statement(0, 5)])
+    assert (ne, nsdf, lights) == (0, 1, [-1])
+
+
+def test_glslviewport_surface_matches_reference_fields():
+    # the fields index.html reads/writes on `sandbox` (index.html:498-1196)
+    for name in ("render", "clear", "resize", "setAnimatedMode", "updateFrontTarget"):
+        assert callable(getattr(rt0.GlslViewport, name))
+    assert len(rt0.STATIC_CONSTANTS) == 13 and len(rt0.ANIMATED_CONSTANTS) == 13

@@ -1,0 +1,128 @@
+"""Pin the CPU restatement (oracle/rt0_oracle.c) to the reference.
+
+The golden fixtures (tests/golden/*.npz) are the reference's own fragment
+shader run by SwiftShader (oracle/gen/make_golden.py).  This file checks:
+  * the RNG stream -- per-pixel seed (raytracer.glsl:2120), hash (302-306),
+    hash2 (308-312) and the bounce/NEE seed schedule -- BIT-EXACTLY;
+  * single-sample radiance of every config within the tolerance below;
+  * ReSTIR: with the reference's own reservoir buffers of passes k-1..k-3 as
+    input, pass k's radiance matches per pixel ("conditional parity"; the
+    reservoir MRTs themselves carry a SwiftShader masked-execution artefact
+    that the restatement models only under SWIFTSHADER_GHOST).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# Tolerance (frozen after measuring restatement vs oracle):
+# a pixel matches when every channel satisfies |d| <= 1e-3 * max(1, |ref|);
+# transcendental ulp drift (glibc vs SwiftShader) may flip rare discrete
+# decisions (shadow ray at an edge, hash < Re, SDF h < EPSILON), so at most
+# BAD_FRAC of pixels may differ.  Pixels where the reference is NaN are
+# excluded and counted.
+REL_TOL = 1e-3
+# Menger sponge: every path grazes many SDF edges where mod()/floor() ulp drift
+# flips the march (1.2% measured, all flips: median error 0).
+BAD_FRAC = {"default": 0.005, "c4_mandelbulb_vol": 0.02, "spectral_vol": 0.02, "menger_coat": 0.02,
+            "restir_mis_demo": 0.01}
+
+
+def pixel_match(got, ref):
+    nan = np.isnan(ref).any(-1)
+    d = np.abs(got - ref)
+    ok = (d <= REL_TOL * np.maximum(1.0, np.abs(ref))).all(-1) | nan
+    return ok, nan
+
+
+def have(name):
+    return os.path.exists(os.path.join(GOLD, name + ".npz"))
+
+
+def test_rng_seed_bitexact():
+    kat = np.load(os.path.join(GOLD, "rng_kat.npz"))
+    c = kat["kat_c"]
+    for f in range(c.shape[0]):
+        for y in range(0, 64, 7):
+            for x in range(64):
+                s = np.float32(O.pixel_seed(np.float32(x + 0.5), np.float32(y + 0.5), f + 1))
+                assert s == c[f, y, x, 0], (f, y, x)
+
+
+def test_rng_hash_schedule_bitexact():
+    kat = np.load(os.path.join(GOLD, "rng_kat.npz"))
+    c, r, a = kat["kat_c"], kat["kat_r"], kat["kat_a"]
+    f32 = np.float32
+    for f in range(c.shape[0]):
+        fr = f32(f + 1)
+        for y in range(0, 64, 5):
+            for x in range(0, 64, 3):
+                s = c[f, y, x, 0]
+                assert f32(O.hash_(f32(s + f32(13.271)))) == c[f, y, x, 1]
+                assert f32(O.hash_(f32(s + f32(63.216)))) == c[f, y, x, 2]
+                assert f32(O.hash_(f32(s + f32(496.4562)))) == c[f, y, x, 3]
+                assert f32(O.hash_(f32(s + f32(249.1686)))) == a[f, y, x, 2]
+                # bounce seed, raytracer.glsl:1810: ((seed + 7.1*f) + 5681.123) + depth*92.13
+                b0 = f32(f32(f32(s + f32(f32(7.1) * fr)) + f32(5681.123)) + f32(f32(0.0) * f32(92.13)))
+                b3 = f32(f32(f32(s + f32(f32(7.1) * fr)) + f32(5681.123)) + f32(f32(3.0) * f32(92.13)))
+                assert (O.hash2(b0, b0) == r[f, y, x, :2]).all()
+                assert (O.hash2(b3, b3) == r[f, y, x, 2:]).all()
+                # plain-NEE seed + sphere-light offset, raytracer.glsl:1972 / 1190
+                n1 = f32(f32(f32(f32(s + f32(f32(8652.1) * fr)) + f32(5681.123)) + f32(f32(1.0) * f32(7895.13)))
+                         + f32(23.1656))
+                assert (O.hash2(n1, n1) == a[f, y, x, :2]).all()
+
+
+NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
+              "c4_mandelbulb_vol", "spectral_vol", "mis_demo_sdfbox", "menger_coat", "thinlens_glass"]
+
+
+@pytest.mark.parametrize("name", NON_RESTIR)
+def test_oracle_radiance_matches_reference(name, cfgs):
+    if not have(name):
+        pytest.skip("fixture %s not generated" % name)
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    gold = np.load(os.path.join(GOLD, name + ".npz"))["samples"][..., :3]
+    o = O.Oracle(cfg, cfgs, width=gold.shape[2], height=gold.shape[1], overrides={"SWIFTSHADER_GHOST": 1})
+    got = np.stack([o.frame(k)[0] for k in range(1, gold.shape[0] + 1)])[..., :3]
+    ok, nan = pixel_match(got, gold)
+    bad = 1.0 - ok.mean()
+    assert bad <= BAD_FRAC.get(name, BAD_FRAC["default"]), "%s: %.4f of pixels differ" % (name, bad)
+    assert nan.mean() < 0.001
+    # mean radiance agrees tightly (a systematic error would shift it)
+    m = ~nan
+    assert abs(got[m].mean() - gold[m].mean()) <= 2e-3 * max(1.0, abs(gold[m].mean()))
+
+
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo"])
+def test_oracle_restir_conditional_parity(name, cfgs):
+    if not have(name):
+        pytest.skip("fixture %s not generated" % name)
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    o = O.Oracle(cfg, cfgs, width=G["samples"].shape[2], height=G["samples"].shape[1])
+    z = np.zeros_like(G["restir_main"][0])
+
+    def out(k, key):
+        return G[key][k - 1] if k >= 1 else z
+
+    for k in range(1, G["samples"].shape[0] + 1):
+        ins = [out(k - 1, "restir_main"), out(k - 1, "restir_aux"), out(k - 2, "restir_main"),
+               out(k - 2, "restir_aux"), out(k - 3, "restir_main"), out(k - 3, "restir_aux")]
+        s, _, _ = o.frame(k, ins)
+        ok, _ = pixel_match(s[..., :3], G["samples"][k - 1][..., :3])
+        assert 1.0 - ok.mean() <= BAD_FRAC.get(name, BAD_FRAC["default"]), (name, k, 1.0 - ok.mean())
+
+
+def test_oracle_accumulation_is_sequential_sum(cfgs):
+    cfg = cfgs["configs"][0]
+    o = O.Oracle(cfg, cfgs, width=16, height=16)
+    acc = o.accumulate(1, 3)
+    ref = np.zeros_like(acc)
+    for k in range(1, 4):
+        ref[..., :3] += o.frame(k)[0][..., :3]
+    assert np.array_equal(acc[..., :3], ref[..., :3])
