@@ -96,11 +96,8 @@ def main():
     acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
     r.set_accum_buffer(acc.data_ptr())
     if world > 1:
+        import rt0.shard as shard
         r.set_shard(rank, world, band)
-        own_idx = torch.tensor(owned, device=acc.device)
-        max_owned = (nb + world - 1) // world
-        gather_bufs = [torch.zeros((max_owned, band, W, 4), device=acc.device) for _ in range(world)] \
-            if rank == 0 else None
         image = torch.zeros((H, W, 4), device=acc.device) if rank == 0 else None
 
     def step(frame0):
@@ -108,13 +105,7 @@ def main():
         torch.cuda.synchronize()
         r.render(frame0, SPP)  # synchronous: returns after the kernels finished
         if world > 1:
-            send = torch.zeros((max_owned, band, W, 4), device=acc.device)
-            send[:len(owned)] = acc.view(nb, band, W, 4).index_select(0, own_idx)
-            dist.gather(send, gather_bufs, dst=0)
-            if rank == 0:
-                for src in range(world):
-                    ob = [b for b in range(nb) if b % world == src]
-                    image.view(nb, band, W, 4)[ob] = gather_bufs[src][:len(ob)]
+            shard.gather_image(acc, rank, world, band, image=image)  # RCCL gather of the HDR bands
 
     for i in range(args.warmup):
         step(1)

@@ -398,6 +398,10 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
       R[R_BACK_AUX] = ta;
     }
   } else {
+    // the counting instance also carries the ReSTIR plumbing: give it valid planes
+    for (int i = 0; i < 6; i++) p.rin[i] = c->d_restir[R_BACK_MAIN + i];
+    p.rout_main = c->d_restir[R_OUT_MAIN];
+    p.rout_aux = c->d_restir[R_OUT_AUX];
     for (int k = 0; k < n; k += c->max_frames_per_launch) {
       p.frame0 = first + (uint32_t)k;
       p.nframes = (n - k) < c->max_frames_per_launch ? (n - k) : c->max_frames_per_launch;

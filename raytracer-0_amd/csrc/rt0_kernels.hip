@@ -995,6 +995,7 @@ __global__ __launch_bounds__(256) void rt0_pass_kernel(const LaunchParams P) {
   }
   P.accum[pix] = a;
   if constexpr (RESTIR) {
+    if (P.rout_main == nullptr || P.rout_aux == nullptr) return;
     if (P.flags & F_RESTIR_DEF) {
       const Res &q = it.fin;
       float na = fminf(fmaxf(q.age / 30.0f, 0.0f), 1.0f);

@@ -1,0 +1,173 @@
+'use strict';
+/*
+ * glsl_viewport.js -- GlslViewport on the MI355X rt0 backend.
+ *
+ * Same constructor, fields and methods the reference's page script uses on its
+ * `sandbox` object (index.js:3-1105, index.html:259-1387): defines, constants,
+ * animatedConstants, scene, sdf_meshes, camera, passes, max_passes, render(),
+ * clear(), resize(v), setAnimatedMode(b), updateFrontTarget().  The shader
+ * pipeline is replaced by the rt0 C ABI (include/rt0.h) through the N-API
+ * addon rt0.node: a change of defines/constants/scene is picked up at the next
+ * render() (the reference needs recompile(), index.html:1167-1196).
+ * There is no CPU fallback: without a HIP device the constructor throws.
+ */
+const path = require('path');
+
+const addon = require(path.join(__dirname, 'rt0.node'));
+
+// vector.js:2-95, the part the camera uses
+class Vector3 {
+  constructor(x, y, z) {
+    this.x = x === undefined ? 0.0 : x;
+    this.y = y === undefined ? 0.0 : y;
+    this.z = z === undefined ? 0.0 : z;
+  }
+  toArray() { return [this.x, this.y, this.z]; }
+}
+
+// index.html:610-676: scene textarea lines -> the GLSL text spliced at #scene
+function sceneFromLines(lines) {
+  let nMeshes = 0, nSdfs = 0, nModels = 0;
+  let uSphere = false, uPlane = false, uBox = false;
+  const lights = [], text = [];
+  lines.forEach((line, i) => {
+    const fields = line.split(',');
+    const mat = fields[0].trim(), type = fields[1].trim();
+    if (mat.lastIndexOf('MAT_LIGHT') >= 0) lights.push(i);
+    text.push('Mesh(' + line + ')' + (i !== lines.length - 1 ? ',' : ''));
+    if (type === 'SDF' || type === 'GRID_SDF') nSdfs++;
+    else if (type === 'PLANE' || type === 'SPHERE' || type === 'BOX') {
+      uSphere = uSphere || type === 'SPHERE';
+      uPlane = uPlane || type === 'PLANE';
+      uBox = uBox || type === 'BOX';
+      nMeshes++;
+    } else if (type === 'TRIANGLE') nModels++;
+    else throw new Error("There's no such thing as " + type);
+  });
+  if (lights.length === 0) lights.push(-1);
+  return {
+    nSdfs,
+    scene: 'const bool U_EUCLIDEAN = ' + (nMeshes > 0) + ';\nconst bool U_SPHERE = ' + uSphere +
+      ';\nconst bool U_PLANE = ' + uPlane + ';\nconst bool U_BOX = ' + uBox + ';\nconst bool U_SDF = ' +
+      (nSdfs > 0) + ';\n\nconst lowp int NUM_MESHES = ' + nMeshes + ';\nconst lowp int NUM_SDFS   = ' + nSdfs +
+      ';\nconst lowp int NUM_MODELS = ' + nModels + ';\n\nconst Mesh meshes[NUM_MESHES + NUM_SDFS + NUM_MODELS] = ' +
+      'Mesh[](\n' + text.join('\n') + '\n);\n\nconst lowp int light_index[' + lights.length + '] = int[](\n' +
+      lights.join(', ') + '\n);',
+  };
+}
+
+// index.html:702-717: SDF selector value -> #sdf_meshes statement
+const SDF_PRIMS = ['sdBox', 'udRoundBox', 'sdSphere', 'sdTriPrism', 'sdCone', 'MengerSponge', 'Mandelbulb'];
+function sdfStatement(i, kind) {
+  const m = 'meshes[NUM_MESHES + ' + i + ']';
+  const args = [
+    `p-${m}.pos, ${m}.joker.xyz`, `p-${m}.pos, ${m}.joker.xyz, ${m}.joker.w`, `p-${m}.pos, ${m}.joker.x`,
+    `p-${m}.pos, ${m}.joker.xy`, `p-${m}.pos, ${m}.joker.xyz`, `p-${m}.pos, ${m}.joker.xyz`, `p-${m}.pos`,
+  ][kind];
+  return `sdf_meshes[${i}] = vec2(${SDF_PRIMS[kind]}(${args}), ${i.toFixed(4)});`;
+}
+
+const STATIC_CONSTANTS = [
+  'const lowp int MAX_BOUNCES = 12;', 'const lowp int MAX_DIFF_BOUNCES = 4;', 'const lowp int MAX_SPEC_BOUNCES = 4;',
+  'const lowp int MAX_TRANS_BOUNCES = 12;', 'const lowp int MAX_SCATTERING_EVENTS = 12;',
+  'const mediump int MARCHING_STEPS = 128;', 'const lowp float FUDGE_FACTOR = 0.9;', 'const bool sample_lights = true;',
+  'const bool use_mis = false;', 'const bool use_restir = false;', 'const lowp int LIGHT_PATH_LENGTH = 2;',
+  'const lowp int RESTIR_SAMPLES = 16;', 'const lowp int RENDER_MODE = 0;',
+];
+const ANIMATED_CONSTANTS = [
+  'const lowp int MAX_BOUNCES = 6;', 'const lowp int MAX_DIFF_BOUNCES = 2;', 'const lowp int MAX_SPEC_BOUNCES = 2;',
+  'const lowp int MAX_TRANS_BOUNCES = 4;', 'const lowp int MAX_SCATTERING_EVENTS = 4;',
+  'const mediump int MARCHING_STEPS = 64;', 'const lowp float FUDGE_FACTOR = 0.9;', 'const bool sample_lights = true;',
+  'const bool use_mis = false;', 'const bool use_restir = true;', 'const lowp int LIGHT_PATH_LENGTH = 1;',
+  'const lowp int RESTIR_SAMPLES = 8;', 'const lowp int RENDER_MODE = 1;',
+];
+// index.js:54-85 default scene (Cornell box), textarea grammar
+const CORNELL_LINES = [
+  'MAT_CORNELL_WHITE, PLANE,  vec3( 0.0, 1.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)',
+  'MAT_CORNELL_WHITE, PLANE,  vec3( 0.0,-1.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)',
+  'MAT_CORNELL_WHITE, PLANE,  vec3( 0.0, 0.0, 1.0), vec4(2.5, 0.0, 0.0, 0.0)',
+  'MAT_CORNELL_RED,   PLANE,  vec3( 1.0, 0.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)',
+  'MAT_CORNELL_GREEN, PLANE,  vec3(-1.0, 0.0, 0.0), vec4(1.5, 0.0, 0.0, 0.0)',
+  'MAT_LIGHT_4,       SPHERE, vec3( 0.0, 1.4,-1.2), vec4(0.3, 0.0, 0.0, 0.0)',
+  'MAT_CORNELL_WHITE, BOX,    vec3( 0.5,-1.0,-1.8), vec4(1.0, 0.0, 0.0, 0.0)',
+  'MAT_CORNELL_WHITE, BOX,    vec3(-0.45,-1.15,-1.3), vec4(0.7, 0.0, 0.0, 0.0)',
+];
+
+class GlslViewport {
+  constructor(canvas, opts) {
+    opts = opts || {};
+    this.canvas = canvas || {};
+    this.canvas.width = opts.width || 600;
+    this.canvas.height = opts.height || 600;
+    this.tile_rendering = opts.tile_rendering || false;
+    this.device = opts.device || 0;
+    this.defines = ['//#define USE_CUBEMAP', '#define USE_PROCEDURAL_SKY', '#define USE_BIASED_SAMPLING',
+      '//#define USE_BIDIRECTIONAL', '//#define USE_RESTIR', '//#define USE_SPECTRAL', '//#define USE_VOLUMETRICS'];
+    this.constants = STATIC_CONSTANTS.slice();
+    this.animatedConstants = ANIMATED_CONSTANTS.slice();
+    this.scene = sceneFromLines(CORNELL_LINES).scene;
+    this.sdf_meshes = [];
+    this.camera = {
+      origin: new Vector3(0.0, 0.0, 2.8), lookat: new Vector3(0.0, 0.0, -1.0), fov: 50.0, aperture: 0.0,
+      focalLength: 3.5,
+    };
+    this.passes = 0;
+    this.max_passes = opts.max_passes || Infinity;
+    this.paused = opts.paused || false;
+    this.animatedScene = false;
+    this.temporalFrames = 5;
+    this.loadTime = Date.now();
+    this._h = addon.create(this.canvas.width, this.canvas.height, this.device);
+    this._compiled = null;
+  }
+
+  // index.js:384-440 (uniform upload); here also the "recompile" of scene/flags
+  updateFrontTarget() {
+    const key = JSON.stringify([this.defines, this.constants, this.scene, this.sdf_meshes]);
+    if (key !== this._compiled) {
+      addon.setConfig(this._h, this.defines, this.constants);
+      addon.setScene(this._h, this.scene, this.sdf_meshes);
+      this._compiled = key;
+    }
+    const c = this.camera;
+    addon.setCamera(this._h, [c.origin.x, c.origin.y, c.origin.z], [c.lookat.x, c.lookat.y, c.lookat.z],
+      [c.fov, c.aperture, c.focalLength]);
+  }
+
+  // index.js:986-1105: one pass, u_frame = ++passes (n > 1 batches passes)
+  render(n) {
+    n = n || 1;
+    this.updateFrontTarget();
+    addon.render(this._h, this.passes + 1, n, Date.now() - this.loadTime);
+    this.passes += n;
+  }
+
+  // index.js:822-880
+  clear() { addon.clear(this._h); }
+
+  // index.js:471-493
+  resize(v) {
+    const size = { 0: 256, 1: 512, 2: 1024, 3: 2048, 4: 4096, 5: 8192 }[v] || v;
+    this.canvas.width = this.canvas.height = size;
+    addon.resize(this._h, size, size);
+    this.passes = 0;
+  }
+
+  // index.js:940-983
+  setAnimatedMode(isAnimated) {
+    this.animatedScene = !!isAnimated;
+    this.constants = isAnimated ? this.animatedConstants.slice() : STATIC_CONSTANTS.slice();
+    this.defines[4] = isAnimated ? '#define USE_RESTIR' : '//#define USE_RESTIR';
+    this.clear();
+  }
+
+  accumulator() { return addon.readAccum(this._h); }
+
+  // display pass (tonemapper.glsl:28-33) with u_cont = 1/passes (index.js:1089)
+  image() { return addon.tonemap(this._h, 1.0 / Math.max(1, this.passes)); }
+
+  lastKernelMs() { return addon.lastKernelMs(this._h); }
+}
+
+module.exports = { GlslViewport, Vector3, sceneFromLines, sdfStatement, STATIC_CONSTANTS, ANIMATED_CONSTANTS,
+  CORNELL_LINES, addon };

@@ -1,0 +1,76 @@
+"""The reference's own host language: the N-API addon + JS GlslViewport.
+
+CPU: node loads rt0.node, the pure parsers answer like the C ABI, and the
+constructor throws (no GPU, no fallback).  GPU: a node script drives the same
+render as the Python host and the accumulators agree bit for bit.
+"""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import rt0
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VIEWPORT = os.path.join(REPO, "raytracer-0_amd", "js", "glsl_viewport.js")
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None or not os.path.exists(os.path.join(REPO, "raytracer-0_amd", "js",
+                                                                                "rt0.node")),
+                                reason="node or the rt0.node addon is missing")
+
+
+def run_node(src, timeout=300):
+    out = subprocess.run([NODE, "-e", src], capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    assert out.returncode == 0, out.stderr
+    return out.stdout
+
+
+def test_addon_parsers_match_c_abi(cfgs):
+    src = """
+const v = require(%r);
+const c = v.addon.parseConfig(['#define USE_PROCEDURAL_SKY', '#define USE_RESTIR'], v.STATIC_CONSTANTS);
+const s = v.sceneFromLines(%s);
+const p = v.addon.parseScene(s.scene, []);
+console.log(JSON.stringify({cfg: c, scene: s.scene, n: p.nMeshes, lights: p.lightIndex, types: p.meshes.map(m => m.type)}));
+""" % (VIEWPORT, json.dumps(cfgs["cornell_lines"]))
+    r = json.loads(run_node(src))
+    assert r["cfg"]["defines"] == (1 << 1) | (1 << 4) and r["cfg"]["MAX_BOUNCES"] == 12
+    # the JS and the Python restatements of index.html's scene generator agree
+    assert r["scene"] == rt0.scene_from_lines(cfgs["cornell_lines"])[0]
+    assert r["n"] == 8 and r["lights"] == [5] and r["types"] == [1, 1, 1, 1, 1, 0, 2, 2]
+
+
+def test_js_sdf_statements_match_python():
+    src = "const v = require(%r); console.log(JSON.stringify([0,1,2,3,4,5,6].map(k => v.sdfStatement(1, k))));" % VIEWPORT
+    assert json.loads(run_node(src)) == [rt0.sdf_statement(1, k) for k in range(7)]
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU present")
+def test_js_constructor_throws_without_gpu():
+    out = run_node("const v = require(%r); try { new v.GlslViewport(null, {width: 8, height: 8}); "
+                   "console.log('no-throw'); } catch (e) { console.log('threw ' + e.message); }" % VIEWPORT)
+    assert out.startswith("threw rt0 error -2")
+
+
+@pytest.mark.gpu
+def test_js_glslviewport_renders_like_python(cfgs, gpu_required, tmp_path):
+    out = tmp_path / "acc.bin"
+    src = """
+const fs = require('fs');
+const v = require(%r);
+const vp = new v.GlslViewport(null, {width: 64, height: 64});
+vp.constants[0] = 'const lowp int MAX_BOUNCES = 8;';
+vp.constants[8] = 'const bool use_mis = true;';
+vp.render(); vp.render(); vp.render(2);
+fs.writeFileSync(%r, Buffer.from(vp.accumulator().buffer));
+console.log(vp.passes);
+""" % (VIEWPORT, str(out))
+    assert run_node(src).strip() == "4"
+    a = np.fromfile(str(out), np.float32).reshape(64, 64, 4)
+    r = rt0.Renderer(64, 64)
+    rt0.configure(r, [c for c in cfgs["configs"] if c["name"] == "c2_cornell_mis_refcaps"][0], cfgs)
+    r.render(1, 4)
+    assert np.array_equal(a, r.read_accum())
