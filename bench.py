@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--config", default="c2_cornell_mis_8")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--secondary", action="store_true", help="also time the MAX_DIFF_BOUNCES=4 variant")
+    ap.add_argument("--jit", type=int, default=1, help="1: scene-specialised kernels (default), 0: ahead-of-time")
     args = ap.parse_args()
 
     import torch
@@ -89,6 +90,7 @@ def main():
     cfg = [c for c in cfgs["configs"] if c["name"] == args.config][0]
 
     r = rt0.Renderer(W, H, device=local)
+    r.set_jit(bool(args.jit))
     rt0.configure(r, cfg, cfgs)
     band = 16
     nb = H // band
@@ -160,7 +162,8 @@ def main():
         "config": {"workload": "%s: 1024x1024 Cornell, MIS power heuristic, MAX_BOUNCES=8, MAX_DIFF_BOUNCES=%d, "
                                "64 spp per step (u_frame 1..64)" % (args.config, cfg["constants"].get(
                                    "MAX_DIFF_BOUNCES", 4)),
-                   "width": W, "height": H, "spp": SPP, "parallelism": "row-band x%d (16-row bands)" % world},
+                   "width": W, "height": H, "spp": SPP, "parallelism": "row-band x%d (16-row bands)" % world,
+                   "kernel": "scene-specialised (hipRTC JIT)" if args.jit else "ahead-of-time"},
         "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": None,
                      "flop_per_sample": round(fps, 1),

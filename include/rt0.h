@@ -157,6 +157,18 @@ int rt0_device_accum(rt0_ctx *ctx, void **dptr, void **stream);
  * context's own buffer.  Contents are not cleared. */
 int rt0_set_accum_buffer(rt0_ctx *ctx, void *dptr);
 
+/* Scene-specialised kernels (default on; env RT0_JIT=0 turns the default off):
+ * like the reference recompiling its shader per scene (index.html:1167), the
+ * integrator is compiled by hipRTC with the scene and the constants baked in,
+ * once per (scene, config), cached per process.  0 = ahead-of-time kernels
+ * that read the scene from HBM. */
+int rt0_set_jit(rt0_ctx *ctx, int enable);
+/* Compile the scene-specialised kernel for (scene, config) without a device
+ * (hipRTC only): checks the generated code builds; *code_size receives the
+ * code-object size.  err (may be NULL) receives the compiler log. */
+int rt0_jit_compile(const char *scene_text, const char *const *sdf_meshes, int n_sdf, const rt0_config *cfg,
+                    size_t *code_size, char *err, size_t err_len);
+
 /* Event counters of the last rt0_render call when enabled: [0] intersection()
  * calls, [1] radiance-loop iterations, [2] light-sampling (NEE) calls,
  * [3] map() evaluations, [4] samples.  Counting uses a separate kernel

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -16,6 +17,7 @@
 #include "../../include/rt0.h"
 #include "rt0_device.h"
 #include "rt0_internal.h"
+#include "rt0_jit.h"
 
 extern "C" hipError_t rt0_launch_pass(int variant, const LaunchParams *p, dim3 grid, hipStream_t stream);
 extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, float cont, hipStream_t stream);
@@ -46,6 +48,9 @@ struct rt0_ctx {
   int last_launches = 0;
   int shard = 0, n_shards = 1, band = 16;
   int max_frames_per_launch = 64;
+  SceneDev host_scene;   // what d_scene holds (also the JIT's scene data)
+  bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
+  std::string jit_err;
   std::string err;
 };
 
@@ -99,6 +104,7 @@ int rt0_create(int width, int height, int device, rt0_ctx **out) {
   if (device < 0 || device >= ndev) return RT0_E_ARG;
   rt0_ctx *c = new rt0_ctx();
   c->device = device;
+  if (const char *e = getenv("RT0_JIT")) c->use_jit = atoi(e) != 0;
   rt0h::default_config(c->cfg);
   int rc;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -184,6 +190,7 @@ static int upload_scene(rt0_ctx *c) {
   }
   for (int i = 0; i < s.n_lights; i++) s.light_index[i] = c->lights[i];
   HIPCHK(c, hipSetDevice(c->device));
+  c->host_scene = s;
   HIPCHK(c, hipMemcpyAsync(c->d_scene, &s, sizeof s, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->has_scene = true;
@@ -365,6 +372,17 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
   }
   const int variant = choose_variant(c);
   dim3 grid((c->W + 15) / 16, (p.n_band_rows + 15) / 16);
+  // scene-specialised kernel (compiled once per scene/config, cached); the
+  // counting instance is always the ahead-of-time one
+  void *jit_fn = nullptr;
+  if (c->use_jit && !c->counting) {
+    int rc = rt0h::jit_get(c->host_scene, rt0h::make_jit_key(c->cfg, c->n_sdfs), c->device, &jit_fn, c->jit_err);
+    if (rc != RT0_OK) return fail(c, rc, c->jit_err);
+  }
+  auto launch = [&](const LaunchParams &lp) -> hipError_t {
+    if (jit_fn) return rt0h::jit_launch(jit_fn, &lp, grid.x, grid.y, c->stream) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
+    return rt0_launch_pass(variant, &lp, grid, c->stream);
+  };
   if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 5 * sizeof(unsigned long long), c->stream));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   int launches = 0;
@@ -380,7 +398,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
       p.rin[5] = c->d_restir[R_H2A];
       p.rout_main = c->d_restir[R_OUT_MAIN];
       p.rout_aux = c->d_restir[R_OUT_AUX];
-      HIPCHK(c, rt0_launch_pass(variant, &p, grid, c->stream));
+      HIPCHK(c, launch(p));
       launches++;
       // swapReSTIRBuffers, index.js:795-820
       float4 **R = c->d_restir;
@@ -405,7 +423,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
     for (int k = 0; k < n; k += c->max_frames_per_launch) {
       p.frame0 = first + (uint32_t)k;
       p.nframes = (n - k) < c->max_frames_per_launch ? (n - k) : c->max_frames_per_launch;
-      HIPCHK(c, rt0_launch_pass(variant, &p, grid, c->stream));
+      HIPCHK(c, launch(p));
       launches++;
     }
   }
@@ -527,6 +545,12 @@ int rt0_device_accum(rt0_ctx *c, void **dptr, void **stream) {
   if (!c) return RT0_E_ARG;
   if (dptr) *dptr = c->acc();
   if (stream) *stream = c->stream;
+  return RT0_OK;
+}
+
+int rt0_set_jit(rt0_ctx *c, int enable) {
+  if (!c) return RT0_E_ARG;
+  c->use_jit = enable != 0;
   return RT0_OK;
 }
 

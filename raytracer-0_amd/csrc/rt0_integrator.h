@@ -1,0 +1,1134 @@
+// rt0_integrator.h -- raytracer-0's per-pixel integrator for gfx950 (device code).
+//
+// Included by rt0_kernels.hip (ahead-of-time instances over a scene in HBM) and
+// embedded verbatim into librt0.so for the scene-specialising JIT (rt0_jit.cpp):
+// like the reference, which recompiles its shader whenever the scene or the
+// flags change (index.html:1167-1196), the JIT bakes the scene and the
+// constants in as compile-time data so that the mesh loop unrolls and every
+// type dispatch / flag test folds away.
+//
+// Semantics follow shaders/pathtracing/raytracer.glsl line by line (cited per
+// function).  Geometry and shading may be FMA-contracted (ulp-level); every
+// expression that feeds the RNG or the ReSTIR packing is evaluated in the
+// reference's operation order with contraction off (NC(...) helpers), so the
+// RNG stream is bit-identical to the reference; u2f() reproduces the reference
+// executor's uint->float.  Deviation: powerHeuristic's max(0, 0/0)
+// is 0 (IEEE maxNum), not NaN.
+#pragma once
+#ifndef RT0_JIT
+#include <hip/hip_runtime.h>
+#include "rt0_device.h"
+#endif
+
+#define DEV __device__ __forceinline__
+
+namespace rt0 {
+
+constexpr float EPSILON = 0.001f;
+constexpr float INF_T = 1e4f;
+constexpr float PI_F = 3.14159265f;
+constexpr float ONE_OVER_PI = 0.31830989f;
+constexpr float TWO_PI = 6.28318531f;
+constexpr float FOUR_PI = 12.5663706f;
+constexpr float VOL_SIGMA_T = 0.15f;
+constexpr float VOL_SIGMA_S = 0.13f;
+constexpr float VOL_G = 0.5f;
+
+enum { T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_SDF = 3 };
+enum { M_LIGHT = 0, M_DIR_LIGHT = 1, M_DIFF = 2, M_SPEC = 3, M_REFR_FRESNEL = 4, M_REFR_SCHLICK = 5, M_COAT = 6 };
+
+// ------------------------------------------------------------------ math
+struct v3 {
+  float x, y, z;
+};
+DEV v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+DEV v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+DEV v3 operator-(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+DEV v3 operator*(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+DEV v3 operator*(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+DEV float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+DEV float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+DEV float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+DEV float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+DEV float fdiv(float a, float b) { return a * frcp(b); }
+DEV float sgn(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+DEV float step_(float e, float x) { return x < e ? 0.0f : 1.0f; }
+DEV float mixf(float x, float y, float a) { return a * (y - x) + x; }
+DEV v3 normalize(v3 a) { return a * frsq(dot(a, a)); }
+DEV float length(v3 a) { return fsqrt(dot(a, a)); }
+DEV v3 vmaxs(v3 a, float s) { return mk(fmaxf(a.x, s), fmaxf(a.y, s), fmaxf(a.z, s)); }
+DEV float vmaxc(v3 a) { return fmaxf(a.x, fmaxf(a.y, a.z)); }
+DEV v3 vabs(v3 a) { return mk(fabsf(a.x), fabsf(a.y), fabsf(a.z)); }
+DEV v3 reflect(v3 i, v3 n) { return i - n * (2.0f * dot(n, i)); }
+DEV v3 refract(v3 i, v3 n, float eta) {
+  float d = dot(n, i);
+  float k = 1.0f - eta * eta * (1.0f - d * d);
+  if (k < 0.0f) return mk(0.f, 0.f, 0.f);
+  return i * eta - n * (eta * d + fsqrt(k));
+}
+DEV float fsin(float x) { return __sinf(x); }
+DEV float fcos(float x) { return __cosf(x); }
+DEV float fexp(float x) { return __expf(x); }
+DEV float flog(float x) { return __logf(x); }
+
+// ----------------------------------------------- non-contracted arithmetic
+// Every helper below is evaluated exactly as the reference writes it (no FMA).
+DEV float nc_fract(float x) {
+#pragma clang fp contract(off)
+  return x - floorf(x);
+}
+// a + b*c, unfused
+DEV float nc_addmul(float a, float b, float c) {
+#pragma clang fp contract(off)
+  return a + b * c;
+}
+// ((s + a*f) + b) + c*d  (raytracer.glsl:1810, 1956, 1972, 2003, 2024, 2046)
+DEV float nc_seed4(float s, float a, float f, float b, float c, float d) {
+#pragma clang fp contract(off)
+  return ((s + a * f) + b) + c * d;
+}
+// (s + a*f) + c*d  (raytracer.glsl:1909/1943)
+DEV float nc_seed3(float s, float a, float f, float c, float d) {
+#pragma clang fp contract(off)
+  return (s + a * f) + c * d;
+}
+
+// ------------------------------------------------------------------- RNG
+// uint -> float with the reference executor's double rounding above 2^31
+// (the conversion the golden fixtures were produced with).
+DEV float u2f(uint32_t m) {
+#pragma clang fp contract(off)
+  if (m < 0x80000000u) return (float)(int32_t)m;
+  return (float)(int32_t)(m - 0x80000000u) + 2147483648.0f;
+}
+// raytracer.glsl:302-306
+DEV float hash(float seed) {
+#pragma clang fp contract(off)
+  uint32_t n = __float_as_uint(seed) * 747796405u + 2891336453u;
+  n = ((n >> ((n >> 28u) + 4u)) ^ n) * 277803737u;
+  return u2f((n >> 22u) ^ n) * 2.3283064365386963e-10f;
+}
+// raytracer.glsl:308-312
+DEV void hash2(float sx, float sy, float &ox, float &oy) {
+#pragma clang fp contract(off)
+  float x = sx * 0.1031f, y = sy * 0.1030f;
+  x = x - floorf(x);
+  y = y - floorf(y);
+  float d = x * (y + 19.19f) + y * (x + 19.19f);
+  x += d;
+  y += d;
+  float a = (x + y) * x, b = (x + y) * y;
+  ox = a - floorf(a);
+  oy = b - floorf(b);
+}
+
+// ------------------------------------------------------- scene policies
+// DynScene: the scene lives in HBM (SceneDev) and is read with wave-uniform
+// indices (scalar loads).  A JIT scene (generated by rt0_jit.cpp) provides the
+// same interface as compile-time constants with kStatic = true.
+struct DynScene {
+  static constexpr bool kStatic = false;
+  static constexpr int kMeshes = 0, kSdfs = 0, kLights = 0;
+  const SceneDev *__restrict__ S;
+  DEV int n_meshes() const { return S->n_meshes; }
+  DEV int n_sdfs() const { return S->n_sdfs; }
+  DEV int n_lights() const { return S->n_lights; }
+  DEV GeomRec geom(int i) const { return S->geom[i]; }
+  DEV MatRec mat(int i) const { return S->mat[i]; }
+  DEV float j3(int i) const { return S->j3[i]; }
+  DEV int sdf_kind(int i) const { return S->sdf_kind[i]; }
+  DEV int light(int i) const { return S->light_index[i]; }
+};
+
+// DynCfg: defines/constants as wave-uniform kernel arguments.  A JIT config
+// provides the same accessors as constexpr.
+struct DynCfg {
+  uint32_t fl;
+  int mb, md, ms, mt, msc, mst, rs;
+  float fud;
+  DEV explicit DynCfg(const LaunchParams &P)
+      : fl(P.flags), mb(P.max_bounces), md(P.max_diff), ms(P.max_spec), mt(P.max_trans), msc(P.max_scatter),
+        mst(P.marching_steps), rs(P.restir_samples), fud(P.fudge) {}
+  DEV uint32_t flags() const { return fl; }
+  DEV int max_bounces() const { return mb; }
+  DEV int max_diff() const { return md; }
+  DEV int max_spec() const { return ms; }
+  DEV int max_trans() const { return mt; }
+  DEV int max_scatter() const { return msc; }
+  DEV int marching_steps() const { return mst; }
+  DEV int restir_samples() const { return rs; }
+  DEV float fudge() const { return fud; }
+};
+
+template <int I, int N, class F>
+DEV void static_for(F &&f) {
+  if constexpr (I < N) {
+    f(I);
+    static_for<I + 1, N>(f);
+  }
+}
+// loop over meshes [0, n_meshes): fully unrolled with constant indices for a
+// static (JIT) scene, a uniform runtime loop otherwise
+template <class Scene, class F>
+DEV void for_meshes(const Scene &sc, F &&f) {
+  if constexpr (Scene::kStatic) static_for<0, Scene::kMeshes>(f);
+  else
+    for (int i = 0; i < sc.n_meshes(); ++i) f(i);
+}
+template <class Scene, class F>
+DEV void for_lights(const Scene &sc, F &&f) {
+  if constexpr (Scene::kStatic) static_for<0, Scene::kLights>(f);
+  else
+    for (int i = 0; i < sc.n_lights(); ++i) f(i);
+}
+template <class Scene, class F>
+DEV void for_sdfs(const Scene &sc, F &&f) {
+  if constexpr (Scene::kStatic) static_for<0, Scene::kSdfs>(f);
+  else
+    for (int i = 0; i < sc.n_sdfs(); ++i) f(i);
+}
+
+// --------------------------------------------------------------- geometry
+struct Hit {
+  v3 n, pos;
+  int index;
+};
+
+// SDF primitives, raytracer.glsl:496-528, 642-698
+DEV float sdBox(v3 p, v3 b) {
+  v3 d = vabs(p) - b;
+  v3 m = mk(fmaxf(d.x, 0.f), fmaxf(d.y, 0.f), fmaxf(d.z, 0.f));
+  return length(m) + fminf(fmaxf(d.x, fmaxf(d.y, d.z)), 0.0f);
+}
+DEV float sdCone(v3 p, v3 c) {
+  float qx = fsqrt(p.x * p.x + p.z * p.z), qy = p.y;
+  float d1 = -qy - c.z;
+  float d2 = fmaxf(qx * c.x + qy * c.y, qy);
+  float a = fmaxf(d1, 0.f), b = fmaxf(d2, 0.f);
+  return fsqrt(a * a + b * b) + fminf(fmaxf(d1, d2), 0.f);
+}
+DEV float gmod(float x, float y) { return x - y * floorf(x * frcp(y)); }
+DEV float menger(v3 p, v3 scale) {
+  float d = sdBox(p, scale);
+  float s = 1.0f;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    v3 ps = p * s;
+    v3 a = mk(gmod(ps.x, 2.0f) - 1.0f, gmod(ps.y, 2.0f) - 1.0f, gmod(ps.z, 2.0f) - 1.0f);
+    s *= 3.0f;
+    v3 r = mk(fabsf(1.0f - 3.0f * fabsf(a.x)), fabsf(1.0f - 3.0f * fabsf(a.y)), fabsf(1.0f - 3.0f * fabsf(a.z)));
+    float da = fmaxf(r.x, r.y), db = fmaxf(r.y, r.z), dc = fmaxf(r.z, r.x);
+    float c = (fminf(da, fminf(db, dc)) - 1.0f) / s;
+    d = fmaxf(c, d);
+  }
+  return d;
+}
+DEV float mandelbulb(v3 p) {
+  v3 w = p;
+  float m = dot(w, w);
+  float dz = 1.0f;
+  for (int i = 0; i < 3; ++i) {
+    float m2 = m * m, m4 = m2 * m2;
+    dz = 8.0f * fsqrt(m4 * m2 * m) * dz + 1.0f;
+    float x = w.x, x2 = x * x, x4 = x2 * x2;
+    float y = w.y, y2 = y * y, y4 = y2 * y2;
+    float z = w.z, z2 = z * z, z4 = z2 * z2;
+    float k3 = x2 + z2;
+    float k2 = frsq(k3 * k3 * k3 * k3 * k3 * k3 * k3);
+    float k1 = x4 + y4 + z4 - 6.0f * y2 * z2 - 6.0f * x2 * y2 + 2.0f * z2 * x2;
+    float k4 = x2 - y2 + z2;
+    w.x = p.x + 64.0f * x * y * z * (x2 - z2) * k4 * (x4 - 6.0f * x2 * z2 + z4) * k1 * k2;
+    w.y = p.y + -16.0f * y2 * k3 * k4 * k4 + k1 * k1;
+    w.z = p.z + -8.0f * y * k4 * (x4 * x4 - 28.0f * x4 * x2 * z2 + 70.0f * x4 * z4 - 28.0f * x2 * z2 * z4 + z4 * z4) * k1 * k2;
+    m = dot(w, w);
+    if (m > 4.0f) break;
+  }
+  return fdiv(0.25f * flog(m) * fsqrt(m), dz);
+}
+
+template <class Scene>
+struct Geometry {
+  // map(), raytracer.glsl:700-712 + the #sdf_meshes statements of index.html:702-717
+  static DEV float map(const Scene &sc, v3 p, float &id, unsigned long long &nmap) {
+    ++nmap;
+    float rx = 0.f, ry = 0.f;
+    const int ne = sc.n_meshes();
+    for_sdfs(sc, [&](int i) {
+      const GeomRec g = sc.geom(ne + i);
+      v3 q = p - mk(g.px, g.py, g.pz);
+      v3 j = mk(g.j0, g.j1, g.j2);
+      float d;
+      switch (sc.sdf_kind(ne + i)) {
+        case 0: d = sdBox(q, j); break;
+        case 1: {
+          v3 dd = vabs(q) - j;
+          d = length(mk(fmaxf(dd.x, 0.f), fmaxf(dd.y, 0.f), fmaxf(dd.z, 0.f))) - sc.j3(ne + i);
+          break;
+        }
+        case 2: d = length(q) - g.j0; break;
+        case 3: {
+          v3 qa = vabs(q);
+          d = fmaxf(qa.z - g.j1, fmaxf(qa.x * 0.866025f + q.y * 0.5f, -q.y) - g.j0 * 0.5f);
+          break;
+        }
+        case 4: d = sdCone(q, j); break;
+        case 5: d = menger(q, j); break;
+        default: d = mandelbulb(q); break;
+      }
+      if (i == 0) {
+        rx = d;
+        ry = 0.f;
+      } else {
+        float a = (rx < d) ? 1.0f : 0.0f;
+        rx = mixf(d, rx, a);
+        ry = mixf((float)i, ry, a);
+      }
+    });
+    id = ry;
+    return rx;
+  }
+  // raytracer.glsl:714-722
+  static DEV v3 calcNormal(const Scene &sc, v3 pos, unsigned long long &nmap) {
+    float id;
+    v3 a = mk(1.f, -1.f, -1.f) * map(sc, pos + mk(EPSILON, -EPSILON, -EPSILON), id, nmap);
+    v3 b = mk(-1.f, -1.f, 1.f) * map(sc, pos + mk(-EPSILON, -EPSILON, EPSILON), id, nmap);
+    v3 c = mk(-1.f, 1.f, -1.f) * map(sc, pos + mk(-EPSILON, EPSILON, -EPSILON), id, nmap);
+    v3 d = mk(1.f, 1.f, 1.f) * map(sc, pos + mk(EPSILON, EPSILON, EPSILON), id, nmap);
+    return normalize(((a + b) + c) + d);
+  }
+
+  // intersection(), raytracer.glsl:997-1082.  Returns tmin (INF_T = miss,
+  // hit.index = 0 as HIT_MISS).  uv/texel parsing is omitted: only NULL_TEX
+  // materials are accepted, so they never reach an output.
+  template <bool SDF, class Cfg>
+  static DEV float intersect(const Scene &sc, const Cfg &C, v3 o, v3 d, Hit &hit, unsigned long long &nmap) {
+    hit.n = mk(0.f, 0.f, 0.f);
+    hit.index = 0;
+    int type = -1;
+    float tmin = INF_T;
+    const v3 m = mk(frcp(d.x), frcp(d.y), frcp(d.z));  // iBox's 1/r.d, hoisted (837)
+    // Each candidate test is branch-free (v_cndmask selects): a lane never
+    // waits on another lane's taken branch inside the mesh loop.  The box
+    // normal of iBox (853-856) depends only on the winning box and its t, so
+    // it is evaluated once after the loop for the winner.
+    for_meshes(sc, [&](int i) {
+      const GeomRec g = sc.geom(i);
+      if (g.j0 == 0.0f) return;  // raytracer.glsl:1009
+      const v3 gp = mk(g.px, g.py, g.pz);
+      if (g.type == T_SPHERE) {  // iSphere, 818-833
+        v3 oc = o - gp;
+        float b = dot(oc, d);
+        float c = dot(oc, oc) - g.d0;
+        float disc = b * b - c;
+        float sd = fsqrt(fmaxf(disc, 0.0f));
+        float t0 = -b - sd, t1 = -b + sd;
+        bool ok0 = (t0 > EPSILON && t0 < tmin);
+        bool ok1 = (t1 > EPSILON && t1 < tmin);
+        float t = ok0 ? t0 : t1;
+        bool ok = disc >= 0.0f && (ok0 || ok1);
+        tmin = ok ? t : tmin;
+        type = ok ? (int)T_SPHERE : type;
+        hit.index = ok ? i : hit.index;
+      } else if (g.type == T_PLANE) {  // iPlane, 812-815
+        float t = fdiv(g.d0 - dot(gp, o), dot(gp, d));
+        bool ok = (t > EPSILON && t < tmin);
+        tmin = ok ? t : tmin;
+        type = ok ? (int)T_PLANE : type;
+        hit.index = ok ? i : hit.index;
+      } else if (g.type == T_BOX) {  // iBox, 836-851
+        v3 nv = m * (gp - o);
+        v3 k = vabs(m) * g.d0;
+        v3 t1 = nv - k, t2 = nv + k;
+        float tN = fmaxf(fmaxf(t1.x, t1.y), t1.z);
+        float tF = fminf(fminf(t2.x, t2.y), t2.z);
+        float t = (tN > 0.0f) ? tN : tF;
+        bool ok = !(tN > tF || tF < 0.0f) && !(t < EPSILON || t >= tmin);
+        tmin = ok ? t : tmin;
+        type = ok ? (int)T_BOX : type;
+        hit.index = ok ? i : hit.index;
+      }
+    });
+    if (type == T_BOX) {  // iBox's normal for the winning box, 853-856
+      const GeomRec g = sc.geom(hit.index);
+      v3 hp = (o + d * tmin) - mk(g.px, g.py, g.pz);
+      v3 dd = vabs(hp) - mk(g.d0, g.d0, g.d0);
+      v3 s = mk(sgn(hp.x), sgn(hp.y), sgn(hp.z));
+      v3 st = mk(step_(dd.y, dd.x) * step_(dd.z, dd.x), step_(dd.z, dd.y) * step_(dd.x, dd.y),
+                 step_(dd.x, dd.z) * step_(dd.y, dd.z));
+      hit.n = normalize(s * st);
+    }
+    if constexpr (SDF) {
+      if (sc.n_sdfs() > 0) {  // iSDF, 974-993
+        float t = EPSILON * 4.0f;
+        float id = 0.f;
+        for (int i = 0; i < C.marching_steps(); ++i) {
+          float dist = map(sc, o + d * t, id, nmap);
+          float h = fabsf(dist);
+          if (h < EPSILON || t > tmin) break;
+          t += h * C.fudge();
+        }
+        if (!(t > tmin)) {
+          hit.n = calcNormal(sc, o + d * t, nmap);
+          hit.index = sc.n_meshes() + (int)id;
+          tmin = t;
+          type = T_SDF;
+        }
+      }
+    }
+    if (type >= 0) {
+      hit.pos = d * tmin + o;
+      if (type == T_SPHERE) {
+        const GeomRec g = sc.geom(hit.index);
+        hit.n = normalize(hit.pos - mk(g.px, g.py, g.pz));
+      } else if (type == T_PLANE) {
+        const GeomRec g = sc.geom(hit.index);
+        hit.n = normalize(mk(g.px, g.py, g.pz));
+      }
+    } else {
+      hit.pos = mk(0.f, 0.f, 0.f);
+    }
+    return tmin;
+  }
+};
+
+// ------------------------------------------------------------ sampling
+// raytracer.glsl:1092-1107
+DEV void calc_binormals(v3 n, v3 &ox, v3 &oz) {
+  float sig = n.z < 0.0f ? -1.0f : 1.0f;
+  if (fabsf(n.z) > 0.99999f) {
+    ox = mk(1.f, 0.f, 0.f);
+    oz = mk(0.f, sig, 0.f);
+    return;
+  }
+  float a = frcp(sig - n.z);
+  float b = n.x * n.y * a;
+  ox = mk(1.0f + sig * n.x * n.x * a, sig * b, -sig * n.x);
+  oz = mk(b, sig + n.y * n.y * a, -n.y);
+}
+DEV v3 frame_dir(v3 w, v3 u, v3 v, float rx, float ry) {
+  float om = fsqrt(1.0f - ry * ry);
+  return normalize((u * (fcos(rx) * om) + v * (fsin(rx) * om)) + w * ry);
+}
+// getSampleBiased(w, 1.0, seed), 1109-1120: pow(r.y, 1/2) == sqrt(r.y)
+DEV v3 sample_cosine(v3 w, float seed) {
+  v3 u, v;
+  calc_binormals(w, u, v);
+  float rx, ry;
+  hash2(seed, seed, rx, ry);
+  return frame_dir(w, u, v, rx * TWO_PI, fsqrt(ry));
+}
+// getConeSample, 1122-1133
+DEV v3 sample_cone(v3 w, float extent, float seed) {
+  v3 u, v;
+  calc_binormals(w, u, v);
+  float rx, ry;
+  hash2(seed, seed, rx, ry);
+  return frame_dir(w, u, v, rx * TWO_PI, 1.0f - ry * extent);
+}
+// randomSphereDirection, 1143-1147
+DEV v3 random_sphere_dir(float seed) {
+  float rx, ry;
+  hash2(seed, seed, rx, ry);
+  rx *= TWO_PI;
+  ry *= TWO_PI;
+  float sy = fsin(ry), cy = fcos(ry);
+  return mk(fsin(rx) * sy, fsin(rx) * cy, fcos(rx));
+}
+// sampleHG, 1157-1171
+DEV v3 sample_hg(v3 w, float seed) {
+  float ux, uy;
+  hash2(seed, seed + 1.789f, ux, uy);
+  constexpr float g = VOL_G;
+  float sqr = (1.0f - g * g) / (1.0f - g + 2.0f * g * ux);
+  float cos_theta = (1.0f + g * g - sqr * sqr) / (2.0f * g);
+  float sin_theta = fsqrt(fmaxf(0.0f, 1.0f - cos_theta * cos_theta));
+  float phi = TWO_PI * uy;
+  v3 t, b;
+  calc_binormals(w, t, b);
+  return normalize((t * (fcos(phi) * sin_theta) + b * (fsin(phi) * sin_theta)) + w * cos_theta);
+}
+
+// powerHeuristic / cosineHemispherePdf / lightSamplingPdf, 1233-1262
+DEV float power_heuristic(float f, float g) {
+  float denom = f * f + g * g;
+  return fmaxf(0.0f, fdiv(f * f, denom));  // maxNum: 0/0 -> 0 (documented deviation)
+}
+DEV float cos_pdf(v3 wi, v3 n) { return fmaxf(0.0f, dot(wi, n)) * ONE_OVER_PI; }
+DEV float light_pdf(const GeomRec &g, const MatRec &mt, v3 x) {
+  if (mt.type != M_LIGHT) return 0.0f;
+  if (g.type == T_SPHERE) {
+    v3 d = mk(g.px, g.py, g.pz) - x;
+    float d2 = dot(d, d);
+    float r2 = g.d0;
+    if (d2 <= r2) return 0.0f;
+    float ctm = fsqrt(fmaxf(0.0f, 1.0f - fdiv(r2, d2)));
+    float denom = 1.0f - ctm;
+    if (denom < 1e-6f) return 0.0f;
+    return frcp(TWO_PI * denom);
+  }
+  return 1.0f / FOUR_PI;
+}
+
+DEV float spectral_ior(float lambda, float A) {
+  float lu = lambda * 0.001f;
+  return A + fdiv(0.04f, lu * lu);
+}
+DEV float pow5(float x) {
+  float a = fabsf(x), a2 = a * a;
+  return a2 * a2 * a;
+}
+DEV float schlick(v3 rd, v3 n, float nc, float nt) {
+  float q = fdiv(nc - nt, nc + nt);
+  float R0 = q * q;
+  return R0 + (1.0f - R0) * pow5(1.0f + dot(n, rd));
+}
+DEV float fresnel(v3 rd, v3 n, float nc, float nt, v3 refr) {
+  float cosI = dot(rd, n), cosT = dot(n, refr);
+  float rs = fdiv(nc * cosI - nt * cosT, nc * cosI + nt * cosT);
+  float rp = fdiv(nc * cosT - nt * cosI, nc * cosT + nt * cosI);
+  return (rs * rs + rp * rp) * 0.5f;
+}
+
+// CIE fit, raytracer.glsl:324-353
+DEV v3 wavelength_to_rgb(float l) {
+  float t1 = (l - 442.0f) * (l < 442.0f ? 0.0624f : 0.0374f);
+  float t2 = (l - 599.8f) * (l < 599.8f ? 0.0264f : 0.0323f);
+  float t3 = (l - 501.1f) * (l < 501.1f ? 0.0490f : 0.0382f);
+  float X = 0.362f * fexp(-0.5f * t1 * t1) + 1.056f * fexp(-0.5f * t2 * t2) - 0.065f * fexp(-0.5f * t3 * t3);
+  float y1 = (l - 568.8f) * (l < 568.8f ? 0.0213f : 0.0247f);
+  float y2 = (l - 530.9f) * (l < 530.9f ? 0.0613f : 0.0322f);
+  float Y = 0.821f * fexp(-0.5f * y1 * y1) + 0.286f * fexp(-0.5f * y2 * y2);
+  float z1 = (l - 437.0f) * (l < 437.0f ? 0.0845f : 0.0278f);
+  float z2 = (l - 459.0f) * (l < 459.0f ? 0.0385f : 0.0725f);
+  float Z = 1.217f * fexp(-0.5f * z1 * z1) + 0.681f * fexp(-0.5f * z2 * z2);
+  v3 rgb = mk(3.2404542f * X - 1.5371385f * Y - 0.4985314f * Z, -0.9692660f * X + 1.8760108f * Y + 0.0415560f * Z,
+              0.0556434f * X - 0.2040259f * Y + 1.0572252f * Z);
+  return mk(fmaxf(0.0f, rgb.x) / 0.378f, fmaxf(0.0f, rgb.y) / 0.298f, fmaxf(0.0f, rgb.z) / 0.285f);
+}
+
+// ---------------------------------------------------------------- ReSTIR
+// raytracer.glsl:1264-1802.
+struct Res {
+  v3 pos, col;
+  float ws, M, W, age;
+  int idx;
+};
+DEV Res empty_res() { return Res{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, 0.f, 0.f, 0.f, -1}; }
+DEV bool finite_(float x) { return __builtin_isfinite(x); }
+// packReservoirAux alpha, 1425-1430 (unfused, as the next pass decodes it with fract)
+DEV float pack_alpha(float age, float M, int idx, int nlights) {
+#pragma clang fp contract(off)
+  float na = fminf(fmaxf(age / 30.0f, 0.0f), 1.0f);
+  float nM = fminf(fmaxf(M / 100.0f, 0.0f), 1.0f);
+  float nli = (float)(idx + 1) / (float)(nlights > 1 ? nlights : 1);
+  return na * 0.33f + nM * 0.33f + nli * 0.34f;
+}
+// unpackReservoirEnhanced alpha decode, 1448-1457 (unfused)
+DEV void unpack_alpha(float pa, int nlights, float &age, float &M, int &idx) {
+#pragma clang fp contract(off)
+  float nli = pa * 2.94f;
+  nli = nli - floorf(nli);
+  float temp = pa - nli * 0.34f;
+  float nM = temp * 3.03f;
+  nM = nM - floorf(nM);
+  float nage = (temp - nM * 0.33f) * 3.03f;
+  age = nage * 30.0f;
+  M = nM * 100.0f;
+  int len1 = nlights > 1 ? nlights : 1;
+  idx = (int)(nli * (float)len1) - 1;
+}
+
+// ----------------------------------------------------------- integrator
+template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
+struct Integrator {
+  using G = Geometry<Scene>;
+  const LaunchParams &P;
+  Scene sc;
+  Cfg C;
+  float fcx, fcy;  // gl_FragCoord
+  uint32_t frame;
+  float hero;
+  int diff_b, spec_b, scat_ev;
+  unsigned long long n_isect, n_iter, n_nee, n_map;
+  Res fin;  // g_final_reservoir (raytracer.glsl:1616)
+
+  DEV Integrator(const LaunchParams &p, Scene s, Cfg c)
+      : P(p), sc(s), C(c), n_isect(0), n_iter(0), n_nee(0), n_map(0) {}
+
+  DEV bool flag(uint32_t f) const { return (C.flags() & f) != 0; }
+
+  DEV float isect(v3 o, v3 d, Hit &h) {
+    if (COUNT) ++n_isect;
+    return G::template intersect<SDF>(sc, C, o, d, h, n_map);
+  }
+
+  // calcDirectLighting, raytracer.glsl:1174-1230
+  DEV v3 direct_light(int li, v3 x, v3 nl, float seed) {
+    if (COUNT) ++n_nee;
+    const GeomRec g = sc.geom(li);
+    const MatRec lm = sc.mat(li);
+    Hit hit;
+    v3 dl = mk(0.f, 0.f, 0.f);
+    if (lm.type == M_LIGHT) {
+      if (g.type == T_SPHERE) {
+        v3 sw = mk(g.px, g.py, g.pz) - x;
+        float d2 = dot(sw, sw);
+        float cos_a_max = fsqrt(1.0f - fminf(fmaxf(fdiv(g.d0, d2), 0.0f), 1.0f));
+        v3 sr = sample_cone(normalize(sw), 1.0f - cos_a_max, seed + 23.1656f);
+        float t = isect(x + nl * EPSILON, sr, hit);
+        const MatRec mh = sc.mat(hit.index);
+        if (mh.type == M_LIGHT) {
+          float weight = 2.0f * (1.0f - cos_a_max);
+          float T_fog = 1.0f;
+          if (VOL && flag(F_VOL)) T_fog = fexp(-VOL_SIGMA_T * t);
+          v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
+          dl = (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
+        }
+      } else if (SDF && g.type == T_SDF) {
+        v3 ld = mk(g.px, g.py, g.pz) + random_sphere_dir(seed + 78.2358f) * mk(g.j0, g.j1, g.j2);
+        v3 sr = normalize(ld - x);
+        isect(x + nl * EPSILON, sr, hit);
+        const MatRec mh = sc.mat(hit.index);
+        if (mh.type == M_LIGHT) {
+          v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
+          dl = (c * mk(mh.er, mh.eg, mh.eb)) * fmaxf(0.001f, dot(sr, nl));
+        }
+      }
+    } else if (lm.type == M_DIR_LIGHT) {
+      v3 ld = mk(g.px, g.py, g.pz);
+      float t = isect(x + nl * EPSILON, ld, hit);
+      if (t == INF_T) dl = (mk(lm.cr, lm.cg, lm.cb) * mk(lm.er, lm.eg, lm.eb)) * fmaxf(0.001f, dot(ld, nl));
+    }
+    return dl;
+  }
+
+  // --------------------------------------------------------- ReSTIR parts
+  DEV bool valid_res(const Res &r) {
+    if (!finite_(r.M) || !finite_(r.ws) || !finite_(r.W) || !finite_(r.age)) return false;
+    if (r.M <= 0.0f || r.M > 200.0f) return false;
+    if (r.ws <= 0.0f || r.ws > 1000.0f) return false;
+    if (r.W < 0.0f || r.W > 20.0f) return false;
+    if (r.age < 0.0f || r.age > 35.0f) return false;
+    float lc = dot(r.col, r.col);
+    if (lc < 0.000001f || lc > 10000.0f) return false;
+    if (r.idx >= sc.n_lights() && r.idx != -1) return false;
+    if (dot(r.pos, r.pos) < EPSILON * EPSILON && r.idx >= 0) return false;
+    return true;
+  }
+  DEV float target_fn(v3 lp, v3 lc, v3 hp, v3 hn, const MatRec &mat) {
+    v3 lv = lp - hp;
+    float dist_sq = dot(lv, lv);
+    if (dist_sq < EPSILON * EPSILON) return 0.0f;
+    v3 ld = normalize(lv);
+    float ct = fmaxf(0.0f, dot(hn, ld));
+    if (ct <= 0.0f) return 0.0f;
+    const v3 lum = mk(0.2126f, 0.7152f, 0.0722f);
+    float llum = dot(lc, lum);
+    if (llum <= 0.0f) return 0.0f;
+    float slum = dot(mk(mat.cr, mat.cg, mat.cb), lum);
+    float nnt = fdiv(mat.nt - 1.0f, mat.nt + 1.0f);
+    float R0 = nnt * nnt;
+    float is_refr = (mat.type == M_REFR_FRESNEL || mat.type == M_REFR_SCHLICK) ? 1.0f : 0.0f;
+    float is_coat = (mat.type == M_COAT) ? 1.0f : 0.0f;
+    float base = mixf(slum, R0, is_refr);
+    float bw = mixf(base, (1.0f - R0) * slum, is_coat) * ONE_OVER_PI;
+    float safe = fmaxf(dist_sq, 1e-4f);
+    return fdiv(llum * bw * ct, safe);
+  }
+  DEV bool visible(v3 from, v3 to) {
+    v3 sd = to - from;
+    float dist = length(sd);
+    if (dist < EPSILON * 10.0f) return true;
+    sd = normalize(sd);
+    Hit h;
+    float t = isect(from + (sd * EPSILON) * 2.0f, sd, h);
+    if (t < dist - EPSILON * 2.0f) {
+      if (h.index >= 0 && h.index < sc.n_meshes() + sc.n_sdfs()) return sc.mat(h.index).type == M_LIGHT;
+      return false;
+    }
+    return true;
+  }
+  // GL LINEAR + CLAMP_TO_EDGE fetch of an RGBA32F plane (index.js:660-664)
+  DEV float4 tex2d(const float4 *__restrict__ t, float u, float v) {
+#pragma clang fp contract(off)
+    float x = u * P.res_x - 0.5f, y = v * P.res_y - 0.5f;
+    float fx0 = floorf(x), fy0 = floorf(y);
+    float a = x - fx0, b = y - fy0;
+    int x0 = (int)fx0, y0 = (int)fy0;
+    int x1 = min(max(x0 + 1, 0), P.width - 1), y1 = min(max(y0 + 1, 0), P.height - 1);
+    x0 = min(max(x0, 0), P.width - 1);
+    y0 = min(max(y0, 0), P.height - 1);
+    float4 t00 = t[(size_t)y0 * P.width + x0], t10 = t[(size_t)y0 * P.width + x1];
+    float4 t01 = t[(size_t)y1 * P.width + x0], t11 = t[(size_t)y1 * P.width + x1];
+    float4 r;
+    float top, bot;
+    top = t00.x + a * (t10.x - t00.x); bot = t01.x + a * (t11.x - t01.x); r.x = top + b * (bot - top);
+    top = t00.y + a * (t10.y - t00.y); bot = t01.y + a * (t11.y - t01.y); r.y = top + b * (bot - top);
+    top = t00.z + a * (t10.z - t00.z); bot = t01.z + a * (t11.z - t01.z); r.z = top + b * (bot - top);
+    top = t00.w + a * (t10.w - t00.w); bot = t01.w + a * (t11.w - t01.w); r.w = top + b * (bot - top);
+    return r;
+  }
+  DEV Res unpack(float4 m, float4 a) {
+    Res r = empty_res();
+    if (m.w > 0.0f) {
+      r.pos = mk(m.x, m.y, m.z);
+      r.W = m.w;
+      r.col = mk(a.x, a.y, a.z);
+      unpack_alpha(a.w, sc.n_lights(), r.age, r.M, r.idx);
+      r.idx = min(max(r.idx, -1), sc.n_lights() - 1);
+      r.M = fmaxf(1.0f, r.M);
+      r.ws = r.W * r.M;
+    }
+    return r;
+  }
+  DEV void combine(Res &t, const Res &s, v3 hp, v3 hn, const MatRec &mat, float rnd) {
+    if (!valid_res(s)) return;
+    float tw = target_fn(s.pos, s.col, hp, hn, mat);
+    if (tw <= 0.0f) return;
+    float sc_ = fminf(fmaxf(tw * fmaxf(s.W, 0.0f) * fmaxf(s.M, 1.0f), 0.0f), 200.0f);
+    t.ws += sc_;
+    t.M += s.M;
+    if (t.M > 40.0f) {
+      float inv = fdiv(40.0f, t.M);
+      t.ws *= inv;
+      t.M = 40.0f;
+    }
+    if (t.ws > 0.0f) {
+      float p = fdiv(sc_, t.ws);
+      if (rnd < p) {
+        t.pos = s.pos;
+        t.col = s.col;
+        t.idx = s.idx;
+        t.age = fminf(s.age + 0.25f, 30.0f);
+      }
+    }
+  }
+  // sampleLightsReSTIR, raytracer.glsl:1619-1801
+  DEV v3 restir(v3 hp, v3 hn, const MatRec &mat, float sx, float sy) {
+    if (!flag(F_RESTIR)) return mk(0.f, 0.f, 0.f);
+    const int nl = sc.n_lights();
+    if (nl == 0 || sc.light(0) < 0) return mk(0.f, 0.f, 0.f);
+    const float scx = fcx / P.res_x, scy = fcy / P.res_y;
+    Res init = empty_res();
+    int eff = min(C.restir_samples(), max(4, nl));
+    for (int i = 0; i < eff; i++) {
+      float rvx, rvy;
+      hash2(nc_addmul(sx, (float)i, 0.1f), nc_addmul(sy, (float)i, 0.2f), rvx, rvy);
+      int ai = min(max((int)(rvx * (float)nl), 0), nl - 1);
+      int li = sc.light(ai);
+      if (li < 0 || li >= sc.n_meshes() + sc.n_sdfs()) continue;
+      const GeomRec lg = sc.geom(li);
+      const MatRec lmt = sc.mat(li);
+      v3 lp = mk(lg.px, lg.py, lg.pz);
+      v3 lc = mk(lmt.cr, lmt.cg, lmt.cb) * mk(lmt.er, lmt.eg, lmt.eb);
+      float tv = target_fn(lp, lc, hp, hn, mat);
+      if (tv > 0.0f) {  // updateReservoir, 1305-1326
+        init.ws += tv;
+        init.M += 1.0f;
+        if (init.M > 60.0f) {
+          init.ws *= 0.95f;
+          init.M *= 0.95f;
+        }
+        if (init.ws > 0.0f) {
+          if (rvy < fdiv(tv, init.ws)) {
+            init.pos = lp;
+            init.col = lc;
+            init.idx = li;
+          }
+        }
+      }
+    }
+    Res tr = init;
+    if (frame > 2u) {
+      for (int lvl = 0; lvl < 2; lvl++) {
+        Res h = empty_res();
+        {  // sampleTemporalHistory, 1485-1523
+          v3 m3 = hp - mk(P.cam_px, P.cam_py, P.cam_pz);
+          float ms = 0.001f * (float)(lvl + 1);
+          float hjx, hjy;
+          hash2(nc_addmul(scx, (float)((uint32_t)lvl + frame), 0.1f), nc_addmul(scy, (float)((uint32_t)lvl + frame), 0.1f),
+                hjx, hjy);
+          float px = (scx + m3.x * ms) + (hjx - 0.5f) * 0.002f;
+          float py = (scy + m3.y * ms) + (hjy - 0.5f) * 0.002f;
+          if (!(px < 0.01f || px > 0.99f || py < 0.01f || py > 0.99f)) {
+            float4 md = tex2d(P.rin[lvl == 0 ? 2 : 4], px, py);
+            float4 ad = tex2d(P.rin[lvl == 0 ? 3 : 5], px, py);
+            h = unpack(md, ad);
+            if (valid_res(h)) h.age += (float)(lvl + 1);
+          }
+        }
+        if (valid_res(h) && h.M > 0.0f && h.age < 30.0f) {
+          h.age += (float)(lvl + 1);
+          float ta = lvl == 1 ? 0.95f * 0.80f : 0.95f;
+          h.M *= ta;
+          h.ws *= ta;
+          float trand = hash(nc_addmul(sx + 789.123f, (float)lvl, 456.789f));
+          combine(tr, h, hp, hn, mat, trand);
+        }
+      }
+      if (tr.M > 100.0f) {
+        tr.M = fminf(tr.M, 80.0f);
+        tr.ws *= 0.9f;
+      }
+    }
+    Res fr = tr;
+    int ns = nl > 10 ? 4 : 8;
+    if (frame < 10u) ns = max(2, ns / 2);
+    const float PX[8] = {-0.4706f, 0.8090f, -0.2628f, 0.6882f, -0.9511f, 0.1625f, 0.5000f, -0.6882f};
+    const float PY[8] = {0.4706f, 0.2628f, -0.8090f, -0.5000f, -0.1625f, 0.9511f, -0.6882f, 0.5000f};
+    for (int i = 0; i < ns; i++) {
+      float srx, sry;
+      hash2(nc_addmul(sx, (float)i, 0.3f), nc_addmul(sy, (float)i, 0.4f), srx, sry);
+      float nx = scx + (PX[i] * 16.0f) / P.res_x, ny = scy + (PY[i] * 16.0f) / P.res_y;
+      Res nb = empty_res();
+      if (!(nx < 0.0f || nx > 1.0f || ny < 0.0f || ny > 1.0f)) nb = unpack(tex2d(P.rin[0], nx, ny), tex2d(P.rin[1], nx, ny));
+      if (nb.M > 0.0f) {
+        if (nb.idx >= 0) {
+          v3 ldf = nb.pos - hp;
+          if (dot(ldf, ldf) > 225.0f) continue;
+        }
+        if (nb.age > 30.0f * 0.8f || srx < 0.03f) continue;
+        combine(fr, nb, hp, hn, mat, sry);
+      }
+    }
+    // finalizeReservoir, 1525-1576
+    if (fr.ws <= 0.0f || fr.M <= 0.0f) {
+      fr.W = 0.0f;
+    } else {
+      float tp = target_fn(fr.pos, fr.col, hp, hn, mat);
+      if (tp <= 0.0f || !visible(hp, fr.pos)) {
+        fr.W = 0.0f;
+      } else {
+        float cM = fminf(fmaxf(fr.M, 1.0f), 40.0f);
+        float raw = fr.ws / (tp * cM);
+        float bc = 1.0f;
+        if (fr.age > 0.0f) {
+          float na = fminf(fmaxf(fr.age / 30.0f, 0.0f), 1.0f);
+          bc *= mixf(0.85f, 1.0f, 1.0f - na * 0.3f);
+        }
+        if (cM > 16.0f) bc *= fsqrt(16.0f / cM);
+        fr.W = fminf(fmaxf(bc * raw, 0.0f), 12.0f);
+        if (!finite_(fr.W)) fr.W = 0.0f;
+      }
+    }
+    fr.age = fminf(fr.age, 30.0f);
+    fin = fr;
+    if (fr.W > 0.0f && fr.idx >= 0 && fr.idx < nl) {
+      int act = sc.light(fr.idx);
+      if (act >= 0 && act < sc.n_meshes() + sc.n_sdfs()) {
+        v3 lc = direct_light(act, hp, hn, sx + 456.789f);
+        float ew = fminf(fmaxf(fr.W, 0.0f), 8.0f);
+        if (fr.M > 30.0f) ew *= fsqrt(30.0f / fr.M);
+        v3 fc = lc * ew;
+        if (!finite_(fc.x) || !finite_(fc.y) || !finite_(fc.z)) return mk(0.f, 0.f, 0.f);
+        return fc;
+      }
+    }
+    return mk(0.f, 0.f, 0.f);
+  }
+
+  // Non-specular light sampling dispatch, raytracer.glsl:1899-1976
+  DEV v3 sample_lights(v3 x, v3 nl, const MatRec &mat, float seed, float bounce) {
+    const float fr = (float)frame;
+    v3 acc = mk(0.f, 0.f, 0.f);
+    const int nlights = sc.n_lights();
+    if (flag(F_RESTIR) && flag(F_MIS)) {
+      if (RESTIR && flag(F_RESTIR_DEF)) {
+        if (nlights > 8) {
+          acc = restir(x, nl, mat, nc_seed3(seed, 8652.1f, fr, bounce, 7895.13f),
+                       nc_seed3(seed, 1234.567f, fr, bounce, 9876.54f));
+        } else {
+          const float base = nc_seed4(seed, 8652.1f, fr, 5681.123f, bounce, 7895.13f);
+          for_lights(sc, [&](int i) {
+            int idx = sc.light(i);
+            if (idx < 0) return;
+            const GeomRec lg = sc.geom(idx);
+            const MatRec lmt = sc.mat(idx);
+            if (lmt.type != M_LIGHT) return;
+            v3 lv = mk(lg.px, lg.py, lg.pz) - x;
+            v3 ld = normalize(lv);
+            float dsq = dot(lv, lv);
+            float ct = fmaxf(0.0f, dot(nl, ld));
+            float imp = ct * dot(mk(lmt.er, lmt.eg, lmt.eb), mk(0.2126f, 0.7152f, 0.0722f)) * frsq(dsq + 1.0f);
+            if (imp < 0.001f) return;
+            v3 ls = direct_light(idx, x, nl, nc_addmul(base, (float)i, 123.456f));
+            if (dot(ls, ls) < 0.001f * 0.001f) return;
+            acc = acc + ls * power_heuristic(light_pdf(lg, lmt, x), cos_pdf(ld, nl));
+          });
+        }
+      }
+    } else if (flag(F_RESTIR)) {
+      if (RESTIR && flag(F_RESTIR_DEF))
+        acc = restir(x, nl, mat, nc_seed3(seed, 8652.1f, fr, bounce, 7895.13f),
+                     nc_seed3(seed, 1234.567f, fr, bounce, 9876.54f));
+    } else if (flag(F_MIS) && nlights > 0) {
+      const float base = nc_seed4(seed, 8652.1f, fr, 5681.123f, bounce, 7895.13f);
+      for_lights(sc, [&](int i) {
+        int idx = sc.light(i);
+        if (idx < 0) return;
+        const GeomRec lg = sc.geom(idx);
+        const MatRec lmt = sc.mat(idx);
+        if (lmt.type != M_LIGHT) return;
+        v3 ls = direct_light(idx, x, nl, nc_addmul(base, (float)i, 123.456f));
+        if (dot(ls, ls) > 0.000001f) {
+          v3 ld = normalize(mk(lg.px, lg.py, lg.pz) - x);
+          acc = acc + ls * power_heuristic(light_pdf(lg, lmt, x), cos_pdf(ld, nl));
+        }
+      });
+    } else {
+      const float s = nc_seed4(seed, 8652.1f, fr, 5681.123f, bounce, 7895.13f);
+      for_lights(sc, [&](int i) {
+        int idx = sc.light(i);
+        if (idx >= 0) acc = acc + direct_light(idx, x, nl, s);
+      });
+    }
+    return acc;
+  }
+
+  // radiance() + brdf(), raytracer.glsl:1986-2105 and 1804-1980
+  DEV v3 radiance(v3 ro, v3 rd, float seed) {
+    v3 acc = mk(0.f, 0.f, 0.f), mask = mk(1.f, 1.f, 1.f);
+    bool spec = true;
+    v3 prev_nl = mk(0.f, 1.f, 0.f);
+    const float fr = (float)frame;
+    for (int depth = 0; depth < C.max_bounces(); ++depth) {
+      if (COUNT) ++n_iter;
+      Hit hit;
+      float t = isect(ro, rd, hit);
+      if constexpr (VOL) {
+        if (flag(F_VOL)) {
+          float sd = -flog(fmaxf(hash(nc_addmul(seed + 4729.3f, (float)depth, 991.1f)), 1e-6f)) / VOL_SIGMA_T;
+          if (sd < fminf(INF_T, t)) {
+            v3 sp = ro + rd * sd;
+            mask = mask * (VOL_SIGMA_S / VOL_SIGMA_T);
+            if (flag(F_SAMPLE_LIGHTS)) {
+              for_lights(sc, [&](int li) {
+                int lidx = sc.light(li);
+                if (lidx < 0) return;
+                const GeomRec lg = sc.geom(lidx);
+                const MatRec lmt = sc.mat(lidx);
+                if (lmt.type != M_LIGHT || lg.type != T_SPHERE) return;
+                v3 dlc = mk(lg.px, lg.py, lg.pz) - sp;
+                float dc = length(dlc);
+                float cam = fsqrt(1.0f - fminf(fmaxf(fdiv(lg.d0, dc * dc), 0.0f), 1.0f));
+                float idc = frcp(dc);
+                v3 dir = sample_cone(mk(dlc.x * idc, dlc.y * idc, dlc.z * idc), 1.0f - cam,
+                                     nc_addmul(nc_addmul(seed + 2341.7f, (float)li, 917.3f), (float)depth, 199.1f));
+                if (COUNT) ++n_nee;
+                Hit sh;
+                float ts = isect(sp + dir * (EPSILON * 20.0f), dir, sh);
+                if (sh.index != lidx) return;
+                float omega = 2.0f * (1.0f - cam);
+                float ct = dot(rd, dir);
+                constexpr float g2 = VOL_G * VOL_G;
+                float den = 1.0f + g2 - 2.0f * VOL_G * ct;
+                float phase = fdiv(1.0f - g2, FOUR_PI * den * fsqrt(den));
+                float Tf = fexp(-VOL_SIGMA_T * ts);
+                acc = acc + ((((mask * mk(lmt.cr, lmt.cg, lmt.cb)) * mk(lmt.er, lmt.eg, lmt.eb)) * phase) * Tf) *
+                                (PI_F * omega);
+              });
+            }
+            rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
+            ro = sp;
+            spec = false;
+            ++scat_ev;
+            if (scat_ev >= C.max_scatter() || vmaxc(mask) < 0.01f) break;
+            continue;
+          }
+        }
+      }
+      if (t == INF_T) {
+        if (!spec && flag(F_SAMPLE_LIGHTS)) break;
+        if (flag(F_SKY)) {
+          float k = fminf(fmaxf(rd.y * 0.6f + 0.5f, 0.3f), 1.0f);
+          v3 sky = mk(0.5f + 0.5f * fcos(TWO_PI * (0.525f + 0.9f * k)), 0.5f + 0.5f * fcos(TWO_PI * (0.408f + 0.97f * k)),
+                      0.5f + 0.5f * fcos(TWO_PI * (0.409f + 0.8f * k)));
+          acc = acc + mask * sky;
+        }
+        break;
+      }
+      const GeomRec g = sc.geom(hit.index);
+      const MatRec mt = sc.mat(hit.index);
+      v3 c = vmaxs(mk(mt.cr, mt.cg, mt.cb), 0.001f);
+      float inside = -sgn(dot(rd, hit.n));
+      v3 e = vmaxs(mk(mt.er, mt.eg, mt.eb), 0.001f);
+      if (mt.type == M_LIGHT) {
+        mask = mask * c;
+        float w = 1.0f;
+        if (flag(F_MIS) && !spec && flag(F_SAMPLE_LIGHTS) && depth > 0) {
+          v3 ld = normalize(hit.pos - ro);
+          w = power_heuristic(cos_pdf(ld, prev_nl), light_pdf(g, mt, ro));
+        }
+        acc = acc + (mask * e) * w;
+        break;
+      }
+      prev_nl = hit.n * inside;
+
+      // ---- brdf(), 1804-1980
+      const v3 x = hit.pos;
+      const v3 nl = hit.n * inside;
+      const float bounce = (float)depth;
+      v3 rdir;
+      {
+        float s = nc_seed4(seed, 7.1f, fr, 5681.123f, bounce, 92.13f);
+        rdir = flag(F_BIASED) ? sample_cosine(nl, s) : sample_cone(nl, 1.0f, s);
+      }
+      const float ncr = 1.00029f;
+      float nt_eff = fabsf(mt.nt);
+      if constexpr (SPECTRAL) {
+        if (flag(F_SPECTRAL) && mt.nt < 0.0f) nt_eff = spectral_ior(hero, fabsf(mt.nt));
+      }
+      const int mtype = mt.type;
+      if (mtype == M_DIFF) {
+        ro = x + nl * EPSILON;
+        rd = rdir;
+        mask = mask * c;
+        ++diff_b;
+        spec = false;
+      } else if (mtype == M_SPEC) {
+        ro = x + nl * EPSILON;
+        rd = normalize(e * rdir + reflect(rd, nl));
+        mask = mask * c;
+        ++spec_b;
+        spec = true;
+      } else if (mtype == M_REFR_FRESNEL || mtype == M_REFR_SCHLICK) {
+        float nnt = inside < 0.0f ? fdiv(nt_eff, ncr) : fdiv(ncr, nt_eff);
+        v3 tdir = refract(rd, nl, nnt);
+        if (length(tdir) == 0.0f) {  // total internal reflection
+          ro = x + nl * EPSILON;
+          rd = normalize(e * rdir + reflect(rd, nl));
+          ++spec_b;
+          spec = true;
+        } else {
+          tdir = normalize(e * rdir + tdir);
+          float Re = mtype == M_REFR_FRESNEL ? fresnel(rd, nl, ncr, nt_eff, tdir) : schlick(rd, nl, ncr, nt_eff);
+          if (hash(seed) < Re) {
+            ro = x + nl * EPSILON;
+            rd = normalize(e * rdir + reflect(rd, nl));
+            ++spec_b;
+          } else {
+            ro = x - nl * EPSILON;
+            mask = mask * c;
+            rd = tdir;
+            ++scat_ev;
+          }
+          spec = true;
+        }
+      } else if (mtype == M_COAT) {
+        ro = x + nl * EPSILON;
+        if (hash(seed) < schlick(rd, nl, ncr, nt_eff)) {
+          rd = normalize(e * rdir + reflect(rd, nl));
+          ++spec_b;
+          spec = true;
+        } else {
+          rd = rdir;
+          mask = mask * c;
+          ++diff_b;
+          spec = false;
+        }
+      }
+      if (!spec && flag(F_SAMPLE_LIGHTS)) acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;
+      // ---- end brdf
+
+      if (vmaxc(mask) < 0.01f) break;
+      if (diff_b >= C.max_diff() || spec_b >= C.max_spec() || 0 >= C.max_trans() || scat_ev >= C.max_scatter()) break;
+    }
+    return acc;
+  }
+
+  // main(), raytracer.glsl:2111-2180: one sample of pixel (px, py) at `frame`
+  DEV v3 sample(int px, int py) {
+    fcx = (float)px + 0.5f;
+    fcy = (float)py + 0.5f;
+    diff_b = spec_b = scat_ev = 0;
+    const float stx = 2.0f * fcx / P.res_x - 1.0f, sty = 2.0f * fcy / P.res_y - 1.0f;
+    float seed;
+    {
+#pragma clang fp contract(off)
+      seed = hash((fcx * 12.9898f + fcy * 78.233f) + 1113.1f * (float)frame);
+    }
+    hero = 550.0f;
+    if constexpr (SPECTRAL) {
+      if (flag(F_SPECTRAL)) hero = nc_addmul(380.0f, hash(seed + 4821.73f), 340.0f);
+    }
+    const v3 u = mk(P.ux, P.uy, P.uz), v = mk(P.vx, P.vy, P.vz), w = mk(P.wx, P.wy, P.wz);
+    const float ax = hash(seed + 13.271f), ay = hash(seed + 63.216f);
+    const float flx = step_(0.5f, ax), fly = step_(0.5f, ay);
+    const float hx = mixf(ax, 1.0f - ax, flx), hy = mixf(ay, 1.0f - ay, fly);
+    const float sx = fsqrt(2.0f * hx), sy = fsqrt(2.0f * hy);
+    const float dx = mixf(sx - 1.0f, 1.0f - sx, flx) / (P.res_x * 0.5f) + stx;
+    const float dy = mixf(sy - 1.0f, 1.0f - sy, fly) / (P.res_y * 0.5f) + sty;
+    const v3 fp = normalize(((u * dx) * P.uULen + (v * dy) * P.uVLen) + w) * P.focal;
+    v3 ro = mk(P.cam_px, P.cam_py, P.cam_pz), rd;
+    if (P.aperture != 0.0f) {
+      const float ang = hash(seed + 496.4562f) * TWO_PI;
+      const float rad = hash(seed + 249.1686f) * P.aperture;
+      const v3 ap = (u * fcos(ang) + v * fsin(ang)) * rad;
+      ro = ro + ap;
+      rd = normalize(fp - ap);
+    } else {
+      rd = normalize(fp);  // aperture 0: randomAperturePos == 0 exactly
+    }
+    if (RESTIR) fin = empty_res();
+    v3 col = radiance(ro, rd, seed);
+    if constexpr (SPECTRAL) {
+      if (flag(F_SPECTRAL)) col = col * wavelength_to_rgb(hero);
+    }
+    return col;
+  }
+};
+
+// Row-band sharding: launch row `r` of the band-compressed grid maps to image
+// row (r/band * n_shards + shard) * band + r % band.
+DEV int image_row(const LaunchParams &P, int r) {
+  const int b = r / P.band;
+  return (b * P.n_shards + P.shard) * P.band + (r - b * P.band);
+}
+
+// The pass kernel body: 16x16 pixel tile per 256-thread workgroup (four 8x8
+// wave tiles); each lane accumulates its pixel's passes in registers.
+template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
+DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lx = (lane & 7) + ((wave & 1) << 3);
+  const int ly = (lane >> 3) + ((wave >> 1) << 3);
+  const int px = blockIdx.x * 16 + lx;
+  const int r = blockIdx.y * 16 + ly;
+  if (px >= P.width || r >= P.n_band_rows) return;
+  const int py = image_row(P, r);
+  if (py >= P.height) return;
+  Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT> it(P, sc, cfg);
+  const size_t pix = (size_t)py * P.width + px;
+  float4 a = P.accum[pix];
+  for (int f = 0; f < P.nframes; ++f) {
+    it.frame = P.frame0 + (uint32_t)f;
+    v3 s = it.sample(px, py);
+    {
+#pragma clang fp contract(off)
+      a.x += s.x;
+      a.y += s.y;
+      a.z += s.z;
+    }
+  }
+  P.accum[pix] = a;
+  if constexpr (RESTIR) {
+    if (P.rout_main == nullptr || P.rout_aux == nullptr) return;
+    if (it.flag(F_RESTIR_DEF)) {
+      const Res &q = it.fin;
+      P.rout_main[pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
+      P.rout_aux[pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+    } else {
+      P.rout_main[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+      P.rout_aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if constexpr (COUNT) {
+    atomicAdd(&P.counters[0], it.n_isect);
+    atomicAdd(&P.counters[1], it.n_iter);
+    atomicAdd(&P.counters[2], it.n_nee);
+    atomicAdd(&P.counters[3], it.n_map);
+    atomicAdd(&P.counters[4], (unsigned long long)P.nframes);
+  }
+}
+
+}  // namespace rt0

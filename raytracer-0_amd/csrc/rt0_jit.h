@@ -1,0 +1,34 @@
+// rt0_jit.h -- scene-specialising run-time compilation (see rt0_jit.cpp).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt0.h"
+
+#include "rt0_device.h"
+
+namespace rt0h {
+
+// Everything the generated kernel bakes in besides the scene itself.
+struct JitKey {
+  uint32_t flags;
+  int max_bounces, max_diff, max_spec, max_trans, max_scatter, marching_steps, restir_samples;
+  float fudge;
+  bool restir, vol, sdf, spectral;
+};
+
+std::string jit_source(const SceneDev &s, const JitKey &k);
+int jit_compile(const std::string &src, std::vector<char> &code, std::string &err);
+// runtime feature flags (F_*) of a config, and the JIT key of (config, scene)
+uint32_t flags_from_config(const rt0_config &c);
+JitKey make_jit_key(const rt0_config &c, int n_sdfs);
+// flatten validated mesh records into the device scene layout
+SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, const int32_t *li, int nl);
+// Compile (or fetch from the process cache) the kernel for this scene/config on
+// `device`; *fn receives a hipFunction_t.
+int jit_get(const SceneDev &s, const JitKey &k, int device, void **fn, std::string &err);
+int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, void *stream);
+
+}  // namespace rt0h

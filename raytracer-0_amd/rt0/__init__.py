@@ -27,7 +27,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_set_scene_glsl", "rt0_set_scene", "rt0_parse_scene_glsl", "rt0_get_scene", "rt0_set_camera", "rt0_render",
            "rt0_render_async", "rt0_sync", "rt0_read_accum", "rt0_write_accum", "rt0_clear", "rt0_resize",
            "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
-           "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_counting", "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version"]
+           "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting", "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version"]
 
 
 class Rt0Error(RuntimeError):
@@ -93,6 +93,9 @@ def lib():
         "rt0_set_shard": (c_int, [c_void_p, c_int, c_int, c_int]),
         "rt0_device_accum": (c_int, [c_void_p, P(c_void_p), P(c_void_p)]),
         "rt0_set_accum_buffer": (c_int, [c_void_p, c_void_p]),
+        "rt0_set_jit": (c_int, [c_void_p, c_int]),
+        "rt0_jit_compile": (c_int, [ctypes.c_char_p, P(ctypes.c_char_p), c_int, P(Config), P(ctypes.c_size_t),
+                                    ctypes.c_char_p, ctypes.c_size_t]),
         "rt0_set_counting": (c_int, [c_void_p, c_int]),
         "rt0_read_counters": (c_int, [c_void_p, P(ctypes.c_uint64)]),
         "rt0_last_kernel_ms": (c_int, [c_void_p, P(c_float), P(c_int)]),
@@ -139,6 +142,18 @@ def parse_scene(scene_text, sdf_meshes=()):
     if rc != RT0_OK:
         raise Rt0Error(rc, "cannot parse scene")
     return list(meshes[:ne.value + ns.value]), ne.value, ns.value, list(lights[:nl.value])
+
+
+def jit_compile(scene_text, sdf_meshes, cfg):
+    """Build the scene-specialised kernel offline (hipRTC, no device); returns the code-object size."""
+    sdf = list(sdf_meshes)
+    size = ctypes.c_size_t()
+    err = ctypes.create_string_buffer(4096)
+    rc = lib().rt0_jit_compile(scene_text.encode(), _strarr(sdf), len(sdf), ctypes.byref(cfg), ctypes.byref(size),
+                               err, 4096)
+    if rc != RT0_OK:
+        raise Rt0Error(rc, err.value.decode(errors="replace"))
+    return size.value
 
 
 def scene_from_lines(lines):
@@ -295,6 +310,10 @@ class Renderer:
         """Use a caller-owned device buffer (e.g. torch tensor .data_ptr()) as accumulator."""
         self._chk(lib().rt0_set_accum_buffer(self.h, ctypes.c_void_p(dptr) if dptr else None))
 
+    def set_jit(self, on):
+        """Scene-specialised (hipRTC) kernels on/off (default on)."""
+        self._chk(lib().rt0_set_jit(self.h, int(bool(on))))
+
     def set_counting(self, on):
         self._chk(lib().rt0_set_counting(self.h, int(bool(on))))
 
@@ -422,8 +441,8 @@ CORNELL_LINES = ["MAT_CORNELL_WHITE, PLANE,  vec3( 0.0, 1.0, 0.0), vec4(1.5, 0.0
                  "MAT_CORNELL_WHITE, BOX,    vec3(-0.45,-1.15,-1.3), vec4(0.7, 0.0, 0.0, 0.0)"]
 
 
-def configure(renderer, cfg, cfgs):
-    """Apply one tests/golden/configs.json entry (scene lines, overrides, camera) to a Renderer."""
+def config_strings(cfg):
+    """configs.json entry -> (defines, constants) string arrays in GlslViewport's format."""
     d = ["//#define USE_CUBEMAP", "#define USE_PROCEDURAL_SKY", "#define USE_BIASED_SAMPLING",
          "//#define USE_BIDIRECTIONAL", "//#define USE_RESTIR", "//#define USE_SPECTRAL", "//#define USE_VOLUMETRICS"]
     for k, v in cfg.get("defines", {}).items():
@@ -437,10 +456,20 @@ def configure(renderer, cfg, cfgs):
                 break
         else:
             raise KeyError(k)
-    renderer.set_config(parse_config(d, consts))
+    return d, consts
+
+
+def scene_strings(cfg, cfgs):
+    """configs.json entry -> (scene text, sdf_meshes statements)."""
     lines = cfg["scene_lines"] or cfgs["cornell_lines"]
     scene, ns = scene_from_lines(lines)
     kinds = cfg.get("sdf_kinds") or []
-    renderer.set_scene_glsl(scene, [sdf_statement(i, kinds[i] if i < len(kinds) else 0) for i in range(ns)])
+    return scene, [sdf_statement(i, kinds[i] if i < len(kinds) else 0) for i in range(ns)]
+
+
+def configure(renderer, cfg, cfgs):
+    """Apply one tests/golden/configs.json entry (scene lines, overrides, camera) to a Renderer."""
+    renderer.set_config(parse_config(*config_strings(cfg)))
+    renderer.set_scene_glsl(*scene_strings(cfg, cfgs))
     cam = cfg.get("camera") or cfgs["default_camera"]
     renderer.set_camera(cam["origin"], cam["lookat"], [cam["fov"], cam["aperture"], cam["focalLength"]])

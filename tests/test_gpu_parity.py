@@ -149,3 +149,19 @@ def test_gpu_accumulation_is_sequential_sum(cfgs, gpu_required):
     r.render(1, 2)
     r.render(3, 3)
     assert np.array_equal(r.read_accum(), acc)
+
+
+@pytest.mark.parametrize("name", ["c2_cornell_mis_8", "c3_outdoor_restir", "spectral_vol", "mis_demo_sdfbox"])
+def test_jit_matches_aot(name, cfgs, gpu_required):
+    """Scene-specialised kernels == ahead-of-time kernels (same arithmetic up
+    to FMA placement, so compare with the parity tolerance)."""
+    cfg = cfg_by_name(cfgs, name)
+    out = []
+    for jit in (True, False):
+        r = rt0.Renderer(64, 64)
+        r.set_jit(jit)
+        rt0.configure(r, cfg, cfgs)
+        r.render(1, 2)
+        out.append(r.read_accum())
+    ok, _ = pixel_match(out[0][..., :3], out[1][..., :3])
+    assert ok.mean() >= 0.97, ok.mean()

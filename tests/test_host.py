@@ -120,3 +120,12 @@ def test_glslviewport_surface_matches_reference_fields():
     for name in ("render", "clear", "resize", "setAnimatedMode", "updateFrontTarget"):
         assert callable(getattr(rt0.GlslViewport, name))
     assert len(rt0.STATIC_CONSTANTS) == 13 and len(rt0.ANIMATED_CONSTANTS) == 13
+
+
+def test_jit_kernels_build_for_every_config(cfgs):
+    """The scene-specialised kernel (hipRTC, rt0_jit.cpp) builds for every
+    parity config without a device."""
+    for cfg in cfgs["configs"]:
+        scene, sdf = rt0.scene_strings(cfg, cfgs)
+        size = rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))
+        assert size > 4096, cfg["name"]
