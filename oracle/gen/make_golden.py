@@ -79,7 +79,8 @@ def run_config(glrun, cfgs, cfg):
            "--single", "--out", prefix] + cam_args(cfg, cfgs)
     if restir:
         cmd.append("--restir-out")
-    sh(cmd, timeout=1800)
+    # volumetric shaders take SwiftShader hours (mostly JIT compile): RT0_GOLDEN_TIMEOUT
+    sh(cmd, timeout=int(os.environ.get("RT0_GOLDEN_TIMEOUT", "1800")))
 
     def load(tag):
         return np.stack([np.fromfile("%s_f%d_%s.bin" % (prefix, k, tag), dtype=np.float32).reshape(H, W, 4)

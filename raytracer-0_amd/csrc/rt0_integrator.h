@@ -72,25 +72,35 @@ DEV float fexp(float x) { return __expf(x); }
 DEV float flog(float x) { return __logf(x); }
 
 // ----------------------------------------------- non-contracted arithmetic
-// Every helper below is evaluated exactly as the reference writes it (no FMA).
+// Every helper below is evaluated exactly as the reference writes it (no FMA):
+// the RNG seeds feed a bit-level hash, so one fused a*b+c changes the whole
+// random stream.  `#pragma clang fp contract(off)` alone is not enough: with
+// -ffp-contract=fast, or with the ROCm 7.0 hipRTC that PyTorch bundles (and
+// that a process importing torch binds to), the backend fuses across it.  An
+// empty asm on the product makes it opaque, so no compiler can fuse it.
+DEV float opq(float x) {
+  asm("" : "+v"(x));
+  return x;
+}
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
+  x = opq(x);
   return x - floorf(x);
 }
 // a + b*c, unfused
 DEV float nc_addmul(float a, float b, float c) {
 #pragma clang fp contract(off)
-  return a + b * c;
+  return a + opq(b * c);
 }
 // ((s + a*f) + b) + c*d  (raytracer.glsl:1810, 1956, 1972, 2003, 2024, 2046)
 DEV float nc_seed4(float s, float a, float f, float b, float c, float d) {
 #pragma clang fp contract(off)
-  return ((s + a * f) + b) + c * d;
+  return ((s + opq(a * f)) + b) + opq(c * d);
 }
 // (s + a*f) + c*d  (raytracer.glsl:1909/1943)
 DEV float nc_seed3(float s, float a, float f, float c, float d) {
 #pragma clang fp contract(off)
-  return (s + a * f) + c * d;
+  return (s + opq(a * f)) + opq(c * d);
 }
 
 // ------------------------------------------------------------------- RNG
@@ -106,18 +116,18 @@ DEV float hash(float seed) {
 #pragma clang fp contract(off)
   uint32_t n = __float_as_uint(seed) * 747796405u + 2891336453u;
   n = ((n >> ((n >> 28u) + 4u)) ^ n) * 277803737u;
-  return u2f((n >> 22u) ^ n) * 2.3283064365386963e-10f;
+  return opq(u2f((n >> 22u) ^ n) * 2.3283064365386963e-10f);
 }
 // raytracer.glsl:308-312
 DEV void hash2(float sx, float sy, float &ox, float &oy) {
 #pragma clang fp contract(off)
-  float x = sx * 0.1031f, y = sy * 0.1030f;
+  float x = opq(sx * 0.1031f), y = opq(sy * 0.1030f);
   x = x - floorf(x);
   y = y - floorf(y);
-  float d = x * (y + 19.19f) + y * (x + 19.19f);
+  float d = opq(x * (y + 19.19f)) + opq(y * (x + 19.19f));
   x += d;
   y += d;
-  float a = (x + y) * x, b = (x + y) * y;
+  float a = opq((x + y) * x), b = opq((x + y) * y);
   ox = a - floorf(a);
   oy = b - floorf(b);
 }
@@ -521,17 +531,17 @@ DEV float pack_alpha(float age, float M, int idx, int nlights) {
   float na = fminf(fmaxf(age / 30.0f, 0.0f), 1.0f);
   float nM = fminf(fmaxf(M / 100.0f, 0.0f), 1.0f);
   float nli = (float)(idx + 1) / (float)(nlights > 1 ? nlights : 1);
-  return na * 0.33f + nM * 0.33f + nli * 0.34f;
+  return (opq(na * 0.33f) + opq(nM * 0.33f)) + opq(nli * 0.34f);
 }
 // unpackReservoirEnhanced alpha decode, 1448-1457 (unfused)
 DEV void unpack_alpha(float pa, int nlights, float &age, float &M, int &idx) {
 #pragma clang fp contract(off)
-  float nli = pa * 2.94f;
+  float nli = opq(pa * 2.94f);
   nli = nli - floorf(nli);
-  float temp = pa - nli * 0.34f;
-  float nM = temp * 3.03f;
+  float temp = pa - opq(nli * 0.34f);
+  float nM = opq(temp * 3.03f);
   nM = nM - floorf(nM);
-  float nage = (temp - nM * 0.33f) * 3.03f;
+  float nage = (temp - opq(nM * 0.33f)) * 3.03f;
   age = nage * 30.0f;
   M = nM * 100.0f;
   int len1 = nlights > 1 ? nlights : 1;
@@ -651,7 +661,7 @@ struct Integrator {
   // GL LINEAR + CLAMP_TO_EDGE fetch of an RGBA32F plane (index.js:660-664)
   DEV float4 tex2d(const float4 *__restrict__ t, float u, float v) {
 #pragma clang fp contract(off)
-    float x = u * P.res_x - 0.5f, y = v * P.res_y - 0.5f;
+    float x = opq(u * P.res_x) - 0.5f, y = opq(v * P.res_y) - 0.5f;
     float fx0 = floorf(x), fy0 = floorf(y);
     float a = x - fx0, b = y - fy0;
     int x0 = (int)fx0, y0 = (int)fy0;
@@ -662,10 +672,10 @@ struct Integrator {
     float4 t01 = t[(size_t)y1 * P.width + x0], t11 = t[(size_t)y1 * P.width + x1];
     float4 r;
     float top, bot;
-    top = t00.x + a * (t10.x - t00.x); bot = t01.x + a * (t11.x - t01.x); r.x = top + b * (bot - top);
-    top = t00.y + a * (t10.y - t00.y); bot = t01.y + a * (t11.y - t01.y); r.y = top + b * (bot - top);
-    top = t00.z + a * (t10.z - t00.z); bot = t01.z + a * (t11.z - t01.z); r.z = top + b * (bot - top);
-    top = t00.w + a * (t10.w - t00.w); bot = t01.w + a * (t11.w - t01.w); r.w = top + b * (bot - top);
+    top = t00.x + opq(a * (t10.x - t00.x)); bot = t01.x + opq(a * (t11.x - t01.x)); r.x = top + opq(b * (bot - top));
+    top = t00.y + opq(a * (t10.y - t00.y)); bot = t01.y + opq(a * (t11.y - t01.y)); r.y = top + opq(b * (bot - top));
+    top = t00.z + opq(a * (t10.z - t00.z)); bot = t01.z + opq(a * (t11.z - t01.z)); r.z = top + opq(b * (bot - top));
+    top = t00.w + opq(a * (t10.w - t00.w)); bot = t01.w + opq(a * (t11.w - t01.w)); r.w = top + opq(b * (bot - top));
     return r;
   }
   DEV Res unpack(float4 m, float4 a) {
@@ -1045,7 +1055,7 @@ struct Integrator {
     float seed;
     {
 #pragma clang fp contract(off)
-      seed = hash((fcx * 12.9898f + fcy * 78.233f) + 1113.1f * (float)frame);
+      seed = hash((opq(fcx * 12.9898f) + opq(fcy * 78.233f)) + opq(1113.1f * (float)frame));
     }
     hero = 550.0f;
     if constexpr (SPECTRAL) {
@@ -1105,9 +1115,9 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     v3 s = it.sample(px, py);
     {
 #pragma clang fp contract(off)
-      a.x += s.x;
-      a.y += s.y;
-      a.z += s.z;
+      a.x += opq(s.x);
+      a.y += opq(s.y);
+      a.z += opq(s.z);
     }
   }
   P.accum[pix] = a;

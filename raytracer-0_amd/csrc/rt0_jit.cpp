@@ -24,6 +24,10 @@
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
+#include <link.h>
+#include <unistd.h>
+
 #include "../../include/rt0.h"
 #include "rt0_device.h"
 #include "rt0_jit.h"
@@ -124,28 +128,91 @@ static uint64_t fnv1a(const std::string &s) {
   return h;
 }
 
+// Debugging aid: RT0_JIT_DUMP=<prefix> keeps every generated source and code
+// object as <prefix>_<source hash>_<pid><ext>.
+static void dump_artifact(const std::string &src, const char *ext, const void *data, size_t n) {
+  const char *dump = getenv("RT0_JIT_DUMP");
+  if (!dump) return;
+  char name[512];
+  snprintf(name, sizeof name, "%s_%016llx_%d%s", dump, (unsigned long long)fnv1a(src), (int)getpid(), ext);
+  if (FILE *f = fopen(name, "wb")) {
+    fwrite(data, 1, n, f);
+    fclose(f);
+  }
+}
+
+// The compiler is pinned: hipRTC is loaded from the ROCm install librt0 was
+// built against ($ROCM_PATH or /opt/rocm; RT0_HIPRTC overrides the path) into
+// a private link namespace (dlmopen).  A process that imported PyTorch first
+// already has torch's bundled, older libhiprtc.so.7 under the same soname;
+// binding to that one would make the generated code -- and so the last bits of
+// every pixel -- depend on import order.  The private namespace keeps one
+// compiler (and one answer) for every host: Python with or without torch, node.
+struct Rtc {
+  decltype(&hiprtcCreateProgram) create = nullptr;
+  decltype(&hiprtcCompileProgram) compile = nullptr;
+  decltype(&hiprtcGetProgramLogSize) log_size = nullptr;
+  decltype(&hiprtcGetProgramLog) log = nullptr;
+  decltype(&hiprtcGetCodeSize) code_size = nullptr;
+  decltype(&hiprtcGetCode) get_code = nullptr;
+  decltype(&hiprtcDestroyProgram) destroy = nullptr;
+  std::string path, error;
+};
+
+static const Rtc &rtc() {
+  static Rtc r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    if (const char *p = getenv("RT0_HIPRTC")) r.path = p;
+    else r.path = std::string(getenv("ROCM_PATH") ? getenv("ROCM_PATH") : "/opt/rocm") + "/lib/libhiprtc.so.7";
+    void *h = dlmopen(LM_ID_NEWLM, r.path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char *e = dlerror();
+      r.error = "cannot load hipRTC from " + r.path + ": " + (e ? e : "?");
+      return;
+    }
+    r.create = (decltype(r.create))dlsym(h, "hiprtcCreateProgram");
+    r.compile = (decltype(r.compile))dlsym(h, "hiprtcCompileProgram");
+    r.log_size = (decltype(r.log_size))dlsym(h, "hiprtcGetProgramLogSize");
+    r.log = (decltype(r.log))dlsym(h, "hiprtcGetProgramLog");
+    r.code_size = (decltype(r.code_size))dlsym(h, "hiprtcGetCodeSize");
+    r.get_code = (decltype(r.get_code))dlsym(h, "hiprtcGetCode");
+    r.destroy = (decltype(r.destroy))dlsym(h, "hiprtcDestroyProgram");
+    if (!r.create || !r.compile || !r.log_size || !r.log || !r.code_size || !r.get_code || !r.destroy)
+      r.error = "hipRTC at " + r.path + " lacks an entry point";
+  });
+  return r;
+}
+
 int jit_compile(const std::string &src, std::vector<char> &code, std::string &err) {
+  const Rtc &R = rtc();
+  if (!R.error.empty()) {
+    err = R.error;
+    return RT0_E_HIP;
+  }
+  dump_artifact(src, ".hip", src.data(), src.size());
   hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "rt0_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+  if (R.create(&prog, src.c_str(), "rt0_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
     err = "hiprtcCreateProgram failed";
     return RT0_E_HIP;
   }
-  const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=fast", "-std=c++17"};
-  hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+  const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=fast-honor-pragmas", "-std=c++17"};
+  hiprtcResult r = R.compile(prog, 4, opts);
   if (r != HIPRTC_SUCCESS) {
     size_t ls = 0;
-    hiprtcGetProgramLogSize(prog, &ls);
+    R.log_size(prog, &ls);
     std::string log(ls, '\0');
-    if (ls) hiprtcGetProgramLog(prog, &log[0]);
-    hiprtcDestroyProgram(&prog);
+    if (ls) R.log(prog, &log[0]);
+    R.destroy(&prog);
     err = "JIT compile failed: " + log.substr(0, 2000);
     return RT0_E_HIP;
   }
   size_t cs = 0;
-  hiprtcGetCodeSize(prog, &cs);
+  R.code_size(prog, &cs);
   code.resize(cs);
-  hiprtcGetCode(prog, code.data());
-  hiprtcDestroyProgram(&prog);
+  R.get_code(prog, code.data());
+  R.destroy(&prog);
+  dump_artifact(src, ".co", code.data(), code.size());
   return RT0_OK;
 }
 

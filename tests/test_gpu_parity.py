@@ -21,8 +21,9 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 REL_TOL = 1e-3
 # fraction of pixels allowed to differ (discrete flips from ulp-level
-# differences between gfx950 transcendentals and the reference executor's)
-BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol": 0.03, "menger_coat": 0.02,
+# differences between gfx950 transcendentals and the reference executor's, and
+# from FMA contraction outside the RNG; ray-marched SDF scenes amplify them)
+BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol": 0.03, "menger_coat": 0.03,
             "mis_demo_sdfbox": 0.02, "restir_mis_demo": 0.02, "c3_outdoor_restir": 0.01}
 
 

@@ -73,4 +73,17 @@ console.log(vp.passes);
     r = rt0.Renderer(64, 64)
     rt0.configure(r, [c for c in cfgs["configs"] if c["name"] == "c2_cornell_mis_refcaps"][0], cfgs)
     r.render(1, 4)
-    assert np.array_equal(a, r.read_accum())
+    b = r.read_accum()
+    bad = (a != b).any(-1)
+    if bad.any():
+        r2 = rt0.Renderer(64, 64)
+        r2.set_jit(False)
+        rt0.configure(r2, [c for c in cfgs["configs"] if c["name"] == "c2_cornell_mis_refcaps"][0], cfgs)
+        r2.render(1, 4)
+        c = r2.read_accum()
+        out2 = tmp_path / "acc2.bin"
+        run_node(src.replace(str(out), str(out2)))
+        a2 = np.fromfile(str(out2), np.float32).reshape(64, 64, 4)
+        raise AssertionError("%.4f of pixels differ (max %.3g); js vs py-aot %.4f, py vs py-aot %.4f, js rerun %.4f" % (
+            bad.mean(), np.abs(a - b).max(), (a != c).any(-1).mean(), (b != c).any(-1).mean(),
+            (a2 != a).any(-1).mean()))
