@@ -256,6 +256,14 @@ DEV float mandelbulb(v3 p) {
   return fdiv(0.25f * flog(m) * fsqrt(m), dz);
 }
 
+// Index of the axis a unit plane normal lies on (n = +-e_axis), else -1.
+DEV int axis_of(v3 n) {
+  if (n.y == 0.f && n.z == 0.f && fabsf(n.x) == 1.f) return 0;
+  if (n.x == 0.f && n.z == 0.f && fabsf(n.y) == 1.f) return 1;
+  if (n.x == 0.f && n.y == 0.f && fabsf(n.z) == 1.f) return 2;
+  return -1;
+}
+
 template <class Scene>
 struct Geometry {
   // map(), raytracer.glsl:700-712 + the #sdf_meshes statements of index.html:702-717
@@ -340,7 +348,20 @@ struct Geometry {
         type = ok ? (int)T_SPHERE : type;
         hit.index = ok ? i : hit.index;
       } else if (g.type == T_PLANE) {  // iPlane, 812-815
-        float t = fdiv(g.d0 - dot(gp, o), dot(gp, d));
+        float t;
+        int ax = -1;
+        if constexpr (Scene::kStatic) ax = axis_of(gp);  // folds: the normal is compile-time data
+        if (ax >= 0) {
+          // axis-aligned normal s*e_ax: dot(n, v) == s*v[ax] exactly for finite v,
+          // and 1/(s*d[ax]) == s*m[ax] (v_rcp is sign-symmetric) -- same bits,
+          // without the zero terms and a second reciprocal
+          const float s = ax == 0 ? gp.x : (ax == 1 ? gp.y : gp.z);
+          const float oa = ax == 0 ? o.x : (ax == 1 ? o.y : o.z);
+          const float ma = ax == 0 ? m.x : (ax == 1 ? m.y : m.z);
+          t = (g.d0 - s * oa) * (s * ma);
+        } else {
+          t = fdiv(g.d0 - dot(gp, o), dot(gp, d));
+        }
         bool ok = (t > EPSILON && t < tmin);
         tmin = ok ? t : tmin;
         type = ok ? (int)T_PLANE : type;

@@ -57,6 +57,7 @@ static std::string strip_includes(const char *src) {
 
 std::string jit_source(const SceneDev &s, const JitKey &k) {
   std::ostringstream o;
+  if (const char *x = getenv("RT0_JIT_EXTRA")) o << "// options: " << x << "\n";  // part of the cache key
   o << "#define RT0_JIT 1\n"
        "using __hip_internal::int32_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
   o << strip_includes(rt0_jit_source_text);
@@ -107,7 +108,10 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     << "; }\n  __device__ static constexpr int restir_samples() { return " << k.restir_samples
     << "; }\n  __device__ static constexpr float fudge() { return " << fl(k.fudge) << "; }\n};\n";
   o << "}  // namespace rt0\n";
-  o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_pass(const LaunchParams P) {\n"
+  o << "extern \"C\" __global__ __launch_bounds__(256) ";
+  if (const char *w = getenv("RT0_JIT_WAVES_PER_EU"))  // tuning knob: occupancy target
+    o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w) << "))) ";
+  o << "void rt0_jit_pass(const LaunchParams P) {\n"
        "  rt0::pass_body<rt0::JitScene, rt0::JitCfg, "
     << (k.restir ? "true" : "false") << ", " << (k.vol ? "true" : "false") << ", " << (k.sdf ? "true" : "false")
     << ", " << (k.spectral ? "true" : "false")
@@ -196,8 +200,20 @@ int jit_compile(const std::string &src, std::vector<char> &code, std::string &er
     err = "hiprtcCreateProgram failed";
     return RT0_E_HIP;
   }
-  const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=fast-honor-pragmas", "-std=c++17"};
-  hiprtcResult r = R.compile(prog, 4, opts);
+  // -fno-slp-vectorize: SLP-packed v_pk_*_f32 pairs cost more issue cycles on
+  // gfx950 than the scalar ops they replace (measured: +19% samples/s without)
+  std::vector<std::string> ov = {"--offload-arch=gfx950", "-O3", "-ffp-contract=fast-honor-pragmas", "-fno-slp-vectorize",
+                                 "-std=c++17"};
+  if (const char *x = getenv("RT0_JIT_EXTRA")) {  // tuning knob: extra compiler options, ' ' or ',' separated
+    std::string e(x);
+    for (char &ch : e)
+      if (ch == ',') ch = ' ';
+    std::istringstream is(e);
+    for (std::string w; is >> w;) ov.push_back(w);
+  }
+  std::vector<const char *> opts;
+  for (auto &s : ov) opts.push_back(s.c_str());
+  hiprtcResult r = R.compile(prog, (int)opts.size(), opts.data());
   if (r != HIPRTC_SUCCESS) {
     size_t ls = 0;
     R.log_size(prog, &ls);
