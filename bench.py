@@ -34,6 +34,7 @@ PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
 W = H = 1024
 SPP = 64
+PROFILE_ROUND = "r01"  # profiles/<round>/ holding the PMC summary of this workload
 
 
 def flop_per_sample(c, mis=True):
@@ -146,6 +147,14 @@ def main():
     owned_samples = len(owned) * band * W * SPP
     kern_s = float(np.mean(kernel_ms)) / 1000.0
     achieved_tflops = fps * owned_samples / kern_s / 1e12
+    # HBM traffic per launch from the committed rocprofv3 PMC passes of this
+    # workload (scripts/gpu_profile.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2
+    # gfx950 correction); counters cannot be read from inside this process
+    traffic, pmc = None, None
+    pmc_path = os.path.join(HERE, "profiles", PROFILE_ROUND, "pmc_summary.json")
+    if world == 1 and os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path))
+        traffic = pmc["traffic_bytes_per_launch"]
     out = {
         "metric": "Msamples/sec (pixels x spp / s) at 1024^2 Cornell, 8 bounces",
         "value": round(value, 3),
@@ -165,7 +174,11 @@ def main():
                    "width": W, "height": H, "spp": SPP, "parallelism": "row-band x%d (16-row bands)" % world,
                    "kernel": "scene-specialised (hipRTC JIT)" if args.jit else "ahead-of-time"},
         "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_FP32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes/launch",
+                     "traffic_source": ("profiles/%s/pmc_summary.json" % PROFILE_ROUND) if pmc else None,
+                     "valu_lane_utilisation": round(pmc["valu_lane_utilisation"], 4) if pmc and "valu_lane_utilisation"
+                     in pmc else None,
                      "flop_per_sample": round(fps, 1),
                      "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3)
                                            for k in ("isect", "iter", "nee")},

@@ -606,7 +606,12 @@ struct Integrator {
         float d2 = dot(sw, sw);
         float cos_a_max = fsqrt(1.0f - fminf(fmaxf(fdiv(g.d0, d2), 0.0f), 1.0f));
         v3 sr = sample_cone(normalize(sw), 1.0f - cos_a_max, seed + 23.1656f);
+#ifdef RT0_EXP_NO_SHADOW  // profiling experiment only (breaks parity): shadow ray skipped
+        float t = 1.0f;
+        hit.index = li;
+#else
         float t = isect(x + nl * EPSILON, sr, hit);
+#endif
         const MatRec mh = sc.mat(hit.index);
         if (mh.type == M_LIGHT) {
           float weight = 2.0f * (1.0f - cos_a_max);
@@ -862,6 +867,9 @@ struct Integrator {
   DEV v3 sample_lights(v3 x, v3 nl, const MatRec &mat, float seed, float bounce) {
     const float fr = (float)frame;
     v3 acc = mk(0.f, 0.f, 0.f);
+#ifdef RT0_EXP_NO_NEE  // profiling experiment only (breaks parity): no light sampling
+    return acc;
+#endif
     const int nlights = sc.n_lights();
     if (flag(F_RESTIR) && flag(F_MIS)) {
       if (RESTIR && flag(F_RESTIR_DEF)) {
