@@ -157,6 +157,27 @@ int rt0_device_accum(rt0_ctx *ctx, void **dptr, void **stream);
  * context's own buffer.  Contents are not cleared. */
 int rt0_set_accum_buffer(rt0_ctx *ctx, void *dptr);
 
+/* Sharded ReSTIR: the reservoir textures of index.js:149-163
+ * (units 7-12) and their swap chain (swapReSTIRBuffers, index.js:795-820).
+ * A shard renders one contiguous row block (rt0_set_shard with
+ * band_rows * n_shards >= height), one pass per rt0_render call; between
+ * passes the caller copies `rows` halo rows of the newest reservoir planes
+ * from the neighbouring shards (rt0/shard.py does it over RCCL).
+ *   rt0_set_restir_buffers: 8 caller-owned W*H*4 f32 device planes (e.g.
+ *     torch tensors the collective reads/writes); NULL returns to
+ *     context-owned planes.  All planes are cleared.
+ *   rt0_device_restir: device pointers of the reservoir planes a following
+ *     pass reads: which = 0 newest output (spatial input), 1 / 2 the
+ *     temporal history levels.
+ *   rt0_set_halo: rows of exchanged halo (valid rows around the own block).
+ *   rt0_read_halo_misses: bilinear fetches that fell outside own block + halo
+ *     since the last reset (non-zero = the halo was too small: the result
+ *     differs from the unsharded render). */
+int rt0_set_restir_buffers(rt0_ctx *ctx, void *const planes[8]);
+int rt0_device_restir(rt0_ctx *ctx, int which, void **main_out, void **aux_out);
+int rt0_set_halo(rt0_ctx *ctx, int rows);
+int rt0_read_halo_misses(rt0_ctx *ctx, uint32_t *misses, int reset);
+
 /* Scene-specialised kernels (default on; env RT0_JIT=0 turns the default off):
  * like the reference recompiling its shader per scene (index.html:1167), the
  * integrator is compiled by hipRTC with the scene and the constants baked in,

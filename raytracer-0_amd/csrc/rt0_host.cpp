@@ -7,6 +7,7 @@
 // entry point fails with RT0_E_HIP.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -47,6 +48,9 @@ struct rt0_ctx {
   float last_ms = 0.f;
   int last_launches = 0;
   int shard = 0, n_shards = 1, band = 16;
+  int halo = 0;                  // rows of exchanged reservoir halo (sharded ReSTIR)
+  bool ext_restir = false;       // reservoir planes owned by the caller (rt0_set_restir_buffers)
+  uint32_t *d_halo_miss = nullptr;
   int max_frames_per_launch = 64;
   SceneDev host_scene;   // what d_scene holds (also the JIT's scene data)
   bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
@@ -67,8 +71,11 @@ static int fail(rt0_ctx *c, int code, const std::string &msg) {
 
 static void free_buffers(rt0_ctx *c) {
   if (c->d_accum) (void)hipFree(c->d_accum);
-  for (auto &p : c->d_restir)
-    if (p) (void)hipFree(p), p = nullptr;
+  for (auto &p : c->d_restir) {
+    if (p && !c->ext_restir) (void)hipFree(p);
+    p = nullptr;
+  }
+  c->ext_restir = false;
   if (c->d_tonemap) (void)hipFree(c->d_tonemap);
   c->d_accum = nullptr;
   c->d_tonemap = nullptr;
@@ -110,7 +117,9 @@ int rt0_create(int width, int height, int device, rt0_ctx **out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipMalloc(&c->d_scene, sizeof(SceneDev)) != hipSuccess ||
-      hipMalloc(&c->d_counters, 5 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&c->d_counters, 5 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&c->d_halo_miss, sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(c->d_halo_miss, 0, sizeof(uint32_t)) != hipSuccess) {
     rt0_destroy(c);
     return RT0_E_HIP;
   }
@@ -129,6 +138,7 @@ void rt0_destroy(rt0_ctx *c) {
   free_buffers(c);
   if (c->d_scene) (void)hipFree(c->d_scene);
   if (c->d_counters) (void)hipFree(c->d_counters);
+  if (c->d_halo_miss) (void)hipFree(c->d_halo_miss);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -345,6 +355,16 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.scene = c->d_scene;
   p.accum = c->acc();
   p.counters = c->d_counters;
+  if (c->n_shards > 1) {  // one contiguous block per shard (checked for ReSTIR in render_impl)
+    const int lo = c->shard * c->band, hi = std::min(c->H, lo + c->band);
+    p.valid_lo = std::max(0, lo - c->halo);
+    p.valid_hi = std::min(c->H, hi + c->halo);
+    p.halo_miss = c->d_halo_miss;
+  } else {
+    p.valid_lo = 0;
+    p.valid_hi = c->H;
+    p.halo_miss = nullptr;
+  }
 }
 
 static int choose_variant(const rt0_ctx *c) {
@@ -361,7 +381,14 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
   if (!c->has_scene) return fail(c, RT0_E_STATE, "rt0_render before rt0_set_scene*");
   if (c->cfg.defines & RT0_USE_CUBEMAP) return fail(c, RT0_E_UNSUPPORTED, "USE_CUBEMAP is not supported yet");
   const bool restir = (c->cfg.defines & RT0_USE_RESTIR) != 0;
-  if (restir && c->n_shards > 1) return fail(c, RT0_E_UNSUPPORTED, "ReSTIR with row sharding is not supported yet");
+  // ReSTIR reads neighbouring pixels of the previous passes' reservoirs: a
+  // shard must own one contiguous row block, whose halo the caller exchanges
+  // between passes (rt0_device_restir; rt0/shard.py)
+  if (restir && c->n_shards > 1 && c->band * c->n_shards < c->H)
+    return fail(c, RT0_E_UNSUPPORTED, "ReSTIR sharding needs one contiguous row block per shard "
+                                      "(band_rows * n_shards >= height)");
+  if (restir && c->n_shards > 1 && n > 1)
+    return fail(c, RT0_E_ARG, "sharded ReSTIR renders one pass per call (halo exchange between passes)");
   HIPCHK(c, hipSetDevice(c->device));
   LaunchParams p;
   fill_params(c, p);
@@ -557,6 +584,50 @@ int rt0_set_jit(rt0_ctx *c, int enable) {
 int rt0_set_accum_buffer(rt0_ctx *c, void *dptr) {
   if (!c) return RT0_E_ARG;
   c->ext_accum = (float4 *)dptr;
+  return RT0_OK;
+}
+
+int rt0_set_restir_buffers(rt0_ctx *c, void *const planes[8]) {
+  if (!c) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+  if (planes) {
+    for (int i = 0; i < R_COUNT; i++)
+      if (!planes[i]) return fail(c, RT0_E_ARG, "rt0_set_restir_buffers: null plane");
+    if (!c->ext_restir)
+      for (auto &p : c->d_restir) (void)hipFree(p);
+    for (int i = 0; i < R_COUNT; i++) c->d_restir[i] = (float4 *)planes[i];
+    c->ext_restir = true;
+  } else if (c->ext_restir) {  // back to planes owned by the context
+    for (auto &p : c->d_restir) HIPCHK(c, hipMalloc(&p, bytes));
+    c->ext_restir = false;
+  }
+  for (auto &p : c->d_restir) HIPCHK(c, hipMemsetAsync(p, 0, bytes, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT0_OK;
+}
+
+int rt0_device_restir(rt0_ctx *c, int which, void **main_out, void **aux_out) {
+  if (!c || which < 0 || which > 2) return RT0_E_ARG;
+  static const int M[3] = {R_BACK_MAIN, R_H1, R_H2}, A[3] = {R_BACK_AUX, R_H1A, R_H2A};
+  if (main_out) *main_out = c->d_restir[M[which]];
+  if (aux_out) *aux_out = c->d_restir[A[which]];
+  return RT0_OK;
+}
+
+int rt0_set_halo(rt0_ctx *c, int rows) {
+  if (!c || rows < 0) return RT0_E_ARG;
+  c->halo = rows;
+  return RT0_OK;
+}
+
+int rt0_read_halo_misses(rt0_ctx *c, uint32_t *misses, int reset) {
+  if (!c || !misses) return RT0_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(misses, c->d_halo_miss, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (reset) HIPCHK(c, hipMemset(c->d_halo_miss, 0, sizeof(uint32_t)));
   return RT0_OK;
 }
 

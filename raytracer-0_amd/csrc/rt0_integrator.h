@@ -694,6 +694,7 @@ struct Integrator {
     int x1 = min(max(x0 + 1, 0), P.width - 1), y1 = min(max(y0 + 1, 0), P.height - 1);
     x0 = min(max(x0, 0), P.width - 1);
     y0 = min(max(y0, 0), P.height - 1);
+    if (P.halo_miss && (y0 < P.valid_lo || y1 >= P.valid_hi)) atomicAdd(P.halo_miss, 1u);
     float4 t00 = t[(size_t)y0 * P.width + x0], t10 = t[(size_t)y0 * P.width + x1];
     float4 t01 = t[(size_t)y1 * P.width + x0], t11 = t[(size_t)y1 * P.width + x1];
     float4 r;

@@ -27,7 +27,8 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_set_scene_glsl", "rt0_set_scene", "rt0_parse_scene_glsl", "rt0_get_scene", "rt0_set_camera", "rt0_render",
            "rt0_render_async", "rt0_sync", "rt0_read_accum", "rt0_write_accum", "rt0_clear", "rt0_resize",
            "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
-           "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting", "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version"]
+           "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
+           "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting", "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version"]
 
 
 class Rt0Error(RuntimeError):
@@ -93,6 +94,10 @@ def lib():
         "rt0_set_shard": (c_int, [c_void_p, c_int, c_int, c_int]),
         "rt0_device_accum": (c_int, [c_void_p, P(c_void_p), P(c_void_p)]),
         "rt0_set_accum_buffer": (c_int, [c_void_p, c_void_p]),
+        "rt0_set_restir_buffers": (c_int, [c_void_p, P(c_void_p)]),
+        "rt0_device_restir": (c_int, [c_void_p, c_int, P(c_void_p), P(c_void_p)]),
+        "rt0_set_halo": (c_int, [c_void_p, c_int]),
+        "rt0_read_halo_misses": (c_int, [c_void_p, P(ctypes.c_uint32), c_int]),
         "rt0_set_jit": (c_int, [c_void_p, c_int]),
         "rt0_jit_compile": (c_int, [ctypes.c_char_p, P(ctypes.c_char_p), c_int, P(Config), P(ctypes.c_size_t),
                                     ctypes.c_char_p, ctypes.c_size_t]),
@@ -309,6 +314,32 @@ class Renderer:
     def set_accum_buffer(self, dptr):
         """Use a caller-owned device buffer (e.g. torch tensor .data_ptr()) as accumulator."""
         self._chk(lib().rt0_set_accum_buffer(self.h, ctypes.c_void_p(dptr) if dptr else None))
+
+    def set_restir_buffers(self, dptrs):
+        """Use 8 caller-owned W*H*4 f32 device planes (e.g. torch tensors) as the
+        ReSTIR reservoir textures; None returns to context-owned planes."""
+        if dptrs is None:
+            self._chk(lib().rt0_set_restir_buffers(self.h, None))
+            return
+        if len(dptrs) != 8:
+            raise ValueError("8 reservoir planes expected")
+        arr = (ctypes.c_void_p * 8)(*dptrs)
+        self._chk(lib().rt0_set_restir_buffers(self.h, arr))
+
+    def device_restir(self, which=0):
+        """Device pointers (main, aux) of the reservoir planes the next pass reads:
+        0 = newest output (spatial input), 1/2 = temporal history levels."""
+        m, a = ctypes.c_void_p(), ctypes.c_void_p()
+        self._chk(lib().rt0_device_restir(self.h, which, ctypes.byref(m), ctypes.byref(a)))
+        return m.value, a.value
+
+    def set_halo(self, rows):
+        self._chk(lib().rt0_set_halo(self.h, rows))
+
+    def halo_misses(self, reset=True):
+        n = ctypes.c_uint32()
+        self._chk(lib().rt0_read_halo_misses(self.h, ctypes.byref(n), int(bool(reset))))
+        return n.value
 
     def set_jit(self, on):
         """Scene-specialised (hipRTC) kernels on/off (default on)."""

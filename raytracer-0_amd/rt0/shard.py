@@ -46,16 +46,137 @@ def unpack(gathered, world, band, image):
 
 def gather_image(acc, rank, world, band, image=None, bufs=None):
     """Collective: every rank passes its accumulator; rank 0 returns the
-    assembled [H, W, 4] image (others return None).  H must be a multiple of band."""
+    assembled [H, W, 4] image (others return None).  A partial last band is
+    padded for the transfer."""
     import torch
     import torch.distributed as dist
-    if acc.shape[0] % band:
-        raise ValueError("image height must be a multiple of the band height")
+    H = acc.shape[0]
+    pad = (-H) % band
+    if pad:
+        acc = torch.cat([acc, acc.new_zeros((pad,) + tuple(acc.shape[1:]))])
     send = pack(acc, rank, world, band)
     if rank == 0:
         bufs = bufs if bufs is not None else [torch.empty_like(send) for _ in range(world)]
         dist.gather(send, bufs, dst=0)
-        image = image if image is not None else torch.zeros_like(acc)
-        return unpack(bufs, world, band, image)
+        full = torch.zeros_like(acc) if (image is None or pad) else image
+        full = unpack(bufs, world, band, full)
+        if pad:
+            if image is None:
+                return full[:H].clone()
+            image.copy_(full[:H])
+            return image
+        return full
     dist.gather(send, None, dst=0)
     return None
+
+
+# ------------------------------------------------------------- sharded ReSTIR
+# ReSTIR's spatial pass reads the previous pass's reservoirs up to ~16 px away
+# (raytracer.glsl:1726-1760) and the temporal pass reads the history at a
+# reprojected position (1485-1523), so a ReSTIR shard owns ONE contiguous row
+# block (band_rows = block height) and, after every pass, swaps `halo` rows of
+# the newest reservoir planes with the shards above and below: one point-to-
+# point exchange per pass, 2 x halo x W x 32 B per neighbour (SURVEY 8e).  The
+# history planes are earlier "newest" planes, so their halos are already in
+# place.  librt0 counts any fetch outside block + halo (Renderer.halo_misses):
+# zero means the sharded render equals the unsharded one bit for bit.
+
+def block_band(height, world):
+    """Rows per shard for contiguous blocks: ceil(H / world) rounded up to the
+    16-row workgroup tile."""
+    return ((height + world - 1) // world + 15) // 16 * 16
+
+
+def block_rows(rank, band, height):
+    lo = min(height, rank * band)
+    return lo, min(height, lo + band)
+
+
+def halo_plan(rank, world, band, height, halo):
+    """Point-to-point transfers of one halo exchange for `rank`:
+    [("send"|"recv", peer, row0, row1)].  Every send has the matching recv on
+    the peer with the same row count."""
+    lo, hi = block_rows(rank, band, height)
+    if lo >= hi or halo <= 0:
+        return []
+    if halo > band:
+        raise ValueError("halo (%d rows) larger than a shard's block (%d rows)" % (halo, band))
+    plan = []
+    if rank > 0:
+        plo, phi = block_rows(rank - 1, band, height)
+        plan.append(("send", rank - 1, lo, lo + min(halo, hi - lo)))
+        plan.append(("recv", rank - 1, lo - min(halo, phi - plo), lo))
+    if rank < world - 1:
+        nlo, nhi = block_rows(rank + 1, band, height)
+        if nlo < nhi:
+            plan.append(("send", rank + 1, hi - min(halo, hi - lo), hi))
+            plan.append(("recv", rank + 1, hi, hi + min(halo, nhi - nlo)))
+    return plan
+
+
+def exchange_halo(planes, rank, world, band, halo):
+    """Collective over torch.distributed (RCCL on GPUs, gloo on CPU): planes is
+    a list of [H, W, 4] tensors, fresh in this rank's block; afterwards the
+    halo rows hold the neighbours' rows."""
+    import torch.distributed as dist
+    height = planes[0].shape[0]
+    ops = []
+    for p in planes:
+        for kind, peer, r0, r1 in halo_plan(rank, world, band, height, halo):
+            fn = dist.isend if kind == "send" else dist.irecv
+            ops.append(dist.P2POp(fn, p[r0:r1], peer))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+def exchange_halo_local(planes_by_rank, band, halo):
+    """The same exchange between shards living in one process (tests, or
+    several shards on one device): planes_by_rank[rank] = list of planes."""
+    world = len(planes_by_rank)
+    height = planes_by_rank[0][0].shape[0]
+    for rank in range(world):
+        for kind, peer, r0, r1 in halo_plan(rank, world, band, height, halo):
+            if kind == "recv":
+                for dst, src in zip(planes_by_rank[rank], planes_by_rank[peer]):
+                    dst[r0:r1].copy_(src[r0:r1])
+
+
+class RestirShard:
+    """One rank's sharded ReSTIR renderer state: torch-owned reservoir planes
+    handed to librt0, so that the halo rows can be exchanged as tensors."""
+
+    def __init__(self, renderer, rank, world, height, width, device, halo=24):
+        import torch
+        self.r = renderer
+        self.rank, self.world, self.halo = rank, world, halo
+        self.band = block_band(height, world)
+        self.planes = torch.zeros((8, height, width, 4), dtype=torch.float32, device=device)
+        renderer.set_restir_buffers([self.planes[i].data_ptr() for i in range(8)])
+        self.by_ptr = {self.planes[i].data_ptr(): i for i in range(8)}
+        renderer.set_shard(rank, world, self.band)
+        renderer.set_halo(halo)
+        torch.cuda.synchronize(device)
+
+    def newest(self):
+        m, a = self.r.device_restir(0)
+        return [self.planes[self.by_ptr[m]], self.planes[self.by_ptr[a]]]
+
+    def render(self, first, n, exchange=None):
+        """Passes first..first+n-1, one launch each, halo exchange after each
+        (exchange(planes) defaults to exchange_halo over torch.distributed).
+        Raises if any fetch fell outside block + halo."""
+        import torch
+        for k in range(first, first + n):
+            self.r.render(k, 1)
+            planes = self.newest()
+            if exchange is None:
+                exchange_halo(planes, self.rank, self.world, self.band, self.halo)
+            else:
+                exchange(planes)
+            # librt0 launches on its own stream: the collective's writes must land first
+            torch.cuda.synchronize(self.planes.device)
+        miss = self.r.halo_misses()
+        if miss:
+            raise RuntimeError("sharded ReSTIR: %d reservoir fetches fell outside the %d-row halo; "
+                               "raise the halo" % (miss, self.halo))

@@ -105,3 +105,70 @@ def test_counters_feed_flop_model(cfgs, gpu_required):
     plain = r.read_accum()
     ok = (np.abs(counted - plain) <= 1e-3 * np.maximum(1.0, np.abs(plain))).all(-1)
     assert ok.mean() >= 0.99, ok.mean()
+
+
+def _restir_shards(cfgs, cfg, W, H, world, halo):
+    import torch
+    import rt0.shard as shard
+    band = shard.block_band(H, world)
+    out = []
+    for rank in range(world):
+        r = rt0.Renderer(W, H)
+        rt0.configure(r, cfg, cfgs)
+        planes = torch.zeros((8, H, W, 4), dtype=torch.float32, device="cuda:0")
+        r.set_restir_buffers([planes[i].data_ptr() for i in range(8)])
+        r.set_shard(rank, world, band)
+        r.set_halo(halo)
+        out.append((r, planes, {planes[i].data_ptr(): i for i in range(8)}))
+    torch.cuda.synchronize()
+    return out, band
+
+
+@pytest.mark.parametrize("world,halo", [(3, 24), (4, 24)])
+def test_sharded_restir_matches_whole_image(cfgs, gpu_required, world, halo):
+    """ReSTIR over contiguous row blocks + per-pass halo exchange of the newest
+    reservoir planes (the SURVEY 8e exchange step) == the unsharded render, bit
+    for bit, including the temporal passes (u_frame > 2)."""
+    import torch
+    import rt0.shard as shard
+    cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
+    W, H, F = 48, 96, 5
+    whole = rt0.Renderer(W, H)
+    rt0.configure(whole, cfg, cfgs)
+    for k in range(1, F + 1):
+        whole.render(k, 1)
+    ref = whole.read_accum()
+    ref_main, ref_aux = whole.read_restir(0)
+    shards, band = _restir_shards(cfgs, cfg, W, H, world, halo)
+
+    def newest(s):
+        r, planes, by_ptr = s
+        m, a = r.device_restir(0)
+        return [planes[by_ptr[m]], planes[by_ptr[a]]]
+
+    for k in range(1, F + 1):
+        for r, _, _ in shards:
+            r.render(k, 1)
+        shard.exchange_halo_local([newest(s) for s in shards], band, halo)
+        torch.cuda.synchronize()  # torch's copies before librt0's next launch (its own stream)
+    img = np.zeros_like(ref)
+    main = np.zeros_like(ref_main)
+    for rank, (r, _, _) in enumerate(shards):
+        lo, hi = shard.block_rows(rank, band, H)
+        img[lo:hi] = r.read_accum()[lo:hi]
+        main[lo:hi] = r.read_restir(0)[0][lo:hi]
+        assert r.halo_misses() == 0
+    assert np.array_equal(img, ref)
+    assert np.array_equal(main, ref_main)
+
+
+def test_sharded_restir_reports_a_too_small_halo(cfgs, gpu_required):
+    import rt0.shard as shard
+    cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
+    shards, band = _restir_shards(cfgs, cfg, 48, 96, 3, 2)
+    for k in range(1, 3):
+        for r, _, _ in shards:
+            r.render(k, 1)
+    assert shards[1][0].halo_misses() > 0  # the middle block reads 16 px away
+    with pytest.raises(rt0.Rt0Error):
+        shards[0][0].render(3, 2)  # sharded ReSTIR: one pass per call
