@@ -15,8 +15,10 @@ RCCL inside the timed region ("strong" scaling: total work fixed).
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
 `roofline` (VALU FP32: algorithmic FLOP/sample from SURVEY 8d x counted events,
-over the kernel's HIP-event time) and `cpu_baseline` (the C restatement
-oracle/rt0_oracle.c, OpenMP on host cores, bounded sample).
+over the kernel's HIP-event time; HBM traffic from the committed PMC passes)
+and `cpu_baseline` (the JS CPU integrator oracle/js/rt0_cpu.js on
+node worker_threads, bounded sample of the same workload), with the C
+restatement oracle/rt0_oracle.c (OpenMP) beside it as `cpu_baseline_c`.
 """
 import argparse
 import json
@@ -43,12 +45,42 @@ def flop_per_sample(c, mis=True):
     return 140.0 + 150.0 * c["isect"] / n + 130.0 * c["iter"] / n + (140.0 + 54.0 * mis) * c["nee"] / n
 
 
-def cpu_baseline(cfgs, cfg, budget_s=12.0):
+def host_threads():
+    """Host threads the baselines may use: OMP_NUM_THREADS (16 on the GPU box,
+    whose os.cpu_count() shows the whole machine), else up to 16."""
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+
+def cpu_baseline_js(cfg_name, budget_s=10.0):
+    """SURVEY 8d's CPU baseline: the JS CPU integrator (oracle/js/rt0_cpu.js,
+    fp32 restatement of the same integrator, parity-checked in
+    tests/test_cpu_js.py) on node worker_threads, timed on a bounded sample of
+    the same workload: rows 480..543 of the 1024^2 image, successive passes
+    until the time budget."""
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    if node is None:
+        return None
+    threads = host_threads()
+    r = subprocess.run([node, os.path.join(HERE, "oracle", "js", "cpu_bench.js"),
+                        os.path.join(HERE, "tests", "golden", "configs.json"), cfg_name, str(W), str(H), str(threads),
+                        "bench", "480", "544", str(budget_s)], capture_output=True, text=True, timeout=budget_s * 10 + 60)
+    if r.returncode != 0:
+        return {"error": r.stderr[-300:]}
+    d = json.loads(r.stdout)
+    return {"value": d["msamples_s"], "unit": "Msamples/s", "cores": d["threads"], "kind": "port",
+            "sample": "oracle/js/rt0_cpu.js (JS CPU integrator, node %s worker_threads x%d, %s): rows 480..543 of "
+                      "the 1024^2 bench image, successive passes, %d samples in %.1f s"
+                      % (d["node"], d["threads"], d["cpu"], d["samples"], d["seconds"])}
+
+
+def cpu_baseline(cfgs, cfg, budget_s=8.0):
     """Time the C restatement (OpenMP, all host threads we are allowed) on a
     bounded sample of the same workload: full-width 1024 rows x a band of rows,
     8-bounce MIS passes, scaled by samples."""
     import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = host_threads()
     rows = 64
     o = O.Oracle(cfg, cfgs, width=W, height=H)
     o.frame(1, rows=(480, 480 + 8), threads=threads)  # warm
@@ -199,7 +231,10 @@ def main():
         out["secondary_refcaps_Msamples_s"] = round(W * H * SPP * args.steps / (time.perf_counter() - t1) / 1e6 *
                                                     (world if world > 1 else 1), 3)
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-        out["cpu_baseline"] = cpu_baseline(cfgs, cfg)
+        js = cpu_baseline_js(args.config)
+        c_port = cpu_baseline(cfgs, cfg)
+        out["cpu_baseline"] = js if js and "value" in js else c_port
+        out["cpu_baseline_c"] = c_port  # the C oracle on the same sample (OpenMP)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -1,0 +1,422 @@
+'use strict';
+// rt0_cpu.js -- the raytracer-0 integrator restated in JavaScript for the CPU.
+//
+// TEST / BASELINE INFRASTRUCTURE ONLY (SURVEY 8d: "the JS CPU integrator ...
+// timed on the GPU box's host in the same run").  The product (librt0.so) never
+// calls this; bench.py times it as `cpu_baseline`, tests/test_cpu_js.py checks
+// it against the C oracle (oracle/rt0_oracle.c), which is pinned to the
+// reference's golden fixtures.
+//
+// It follows shaders/pathtracing/raytracer.glsl (line numbers cited per
+// function) in fp32: every operation is rounded with Math.fround, and the RNG
+// reproduces the reference executor's uint->float conversion, so frame k of a
+// pixel draws the same random numbers as the reference.  Scope: the quadric
+// scenes of the C1/C2 configs -- planes, spheres, boxes, every material, sky,
+// plain NEE and MIS.  SDF, volumetrics, spectral and ReSTIR configs are
+// rejected (the C oracle covers them).
+const f = Math.fround;
+
+// ------------------------------------------------------------------ RNG
+const _fb = new Float32Array(1);
+const _ub = new Uint32Array(_fb.buffer);
+const TWO_M32 = f(1.0 / 4294967296.0);
+function u2f(m) {  // SwiftShader: double rounding above 2^31
+  return m < 0x80000000 ? f(m) : f(f(m - 0x80000000) + 2147483648.0);
+}
+// raytracer.glsl:302-306
+function hash(seed) {
+  _fb[0] = seed;
+  let n = (Math.imul(_ub[0], 747796405) + 2891336453) >>> 0;
+  n = Math.imul(((n >>> ((n >>> 28) + 4)) ^ n) >>> 0, 277803737) >>> 0;
+  return f(u2f(((n >>> 22) ^ n) >>> 0) * TWO_M32);
+}
+const K1031 = f(0.1031), K1030 = f(0.1030), K1919 = f(19.19);
+function fract(x) { return f(x - Math.floor(x)); }
+// raytracer.glsl:308-312 (returns [x, y])
+function hash2(sx, sy) {
+  let x = fract(f(sx * K1031)), y = fract(f(sy * K1030));
+  const d = f(f(x * f(y + K1919)) + f(y * f(x + K1919)));
+  x = f(x + d);
+  y = f(y + d);
+  return [fract(f(f(x + y) * x)), fract(f(f(x + y) * y))];
+}
+
+// ----------------------------------------------------------------- math
+function V(x, y, z) { return { x, y, z }; }
+function add(a, b) { return V(f(a.x + b.x), f(a.y + b.y), f(a.z + b.z)); }
+function sub(a, b) { return V(f(a.x - b.x), f(a.y - b.y), f(a.z - b.z)); }
+function mul(a, b) { return V(f(a.x * b.x), f(a.y * b.y), f(a.z * b.z)); }
+function muls(a, s) { return V(f(a.x * s), f(a.y * s), f(a.z * s)); }
+function dot(a, b) { return f(f(f(a.x * b.x) + f(a.y * b.y)) + f(a.z * b.z)); }
+function isqrt(x) { return f(1.0 / f(Math.sqrt(x))); }
+function normalize(a) { return muls(a, isqrt(dot(a, a))); }
+function length(a) { return f(Math.sqrt(dot(a, a))); }
+function gmax(a, b) { return a > b ? a : b; }
+function gmin(a, b) { return a < b ? a : b; }
+function clamp(x, lo, hi) { return gmin(gmax(x, lo), hi); }
+function sgn(x) { return x > 0 ? 1 : (x < 0 ? -1 : 0); }
+function step(e, x) { return x < e ? 0 : 1; }
+function mixf(x, y, a) { return f(f(a * f(y - x)) + x); }
+function vmaxs(a, s) { return V(gmax(a.x, s), gmax(a.y, s), gmax(a.z, s)); }
+function vmaxc(a) { return gmax(a.x, gmax(a.y, a.z)); }
+function vabs(a) { return V(Math.abs(a.x), Math.abs(a.y), Math.abs(a.z)); }
+function cross(a, b) {
+  return V(f(f(a.y * b.z) - f(a.z * b.y)), f(f(a.z * b.x) - f(a.x * b.z)), f(f(a.x * b.y) - f(a.y * b.x)));
+}
+function reflect(i, n) { return sub(i, muls(n, f(2 * dot(n, i)))); }
+function refract(i, n, eta) {
+  const d = dot(n, i);
+  const k = f(1 - f(f(eta * eta) * f(1 - f(d * d))));
+  if (k < 0) return V(0, 0, 0);
+  return sub(muls(i, eta), muls(n, f(f(eta * d) + f(Math.sqrt(k)))));
+}
+function gpow(x, y) { return f(Math.pow(Math.abs(x), y)); }
+const fsin = (x) => f(Math.sin(x)), fcos = (x) => f(Math.cos(x));
+
+const EPS = f(0.001), INF_T = f(1e4), TWO_PI = f(6.28318531), ONE_OVER_PI = f(0.31830989), FOUR_PI = f(12.5663706);
+const RAD = f(0.01745329);
+
+// ------------------------------------------------------- scene grammar
+const T_SPHERE = 0, T_PLANE = 1, T_BOX = 2;
+const M_LIGHT = 0, M_DIR_LIGHT = 1, M_DIFF = 2, M_SPEC = 3, M_REFR_FRESNEL = 4, M_REFR_SCHLICK = 5, M_COAT = 6;
+// Material table, raytracer.glsl:165-224 ([c, e, nt, type]; textured ones omitted)
+const MATS = {
+  MAT_REFR_CLEAR: [[1, 0.5, 0], [0, 0, 0], 1.53, M_REFR_FRESNEL],
+  MAT_REFR_CLEAR_2: [[1, 1, 1], [0, 0, 0], 1.53, M_REFR_SCHLICK],
+  MAT_REFR_SAPPHIRE: [[1, 1, 1], [0, 0, 0], 1.77, M_REFR_FRESNEL],
+  MAT_REFR_WATER: [[0.25, 0.64, 0.88], [0, 0, 0], 1.33, M_REFR_FRESNEL],
+  MAT_LIGHT_4: [[1, 1, 1], [4, 4, 4], 0, M_LIGHT],
+  MAT_LIGHT_CANDLE_4: [[1.0, 0.57647058823, 0.16078431372], [4, 4, 4], 0, M_LIGHT],
+  MAT_LIGHT_HALOGEN_4: [[1.0, 0.94509803921, 0.87843137254], [4, 4, 4], 0, M_LIGHT],
+  MAT_LIGHT_DEMO: [[1, 1, 1], [10, 10, 10], 0, M_LIGHT],
+  MAT_CLEAR_SKY: [[0.25098039215, 0.61176470588, 1.0], [1, 1, 1], 0, M_DIR_LIGHT],
+  MAT_OVERCAST_SKY: [[0.78823529411, 0.8862745098, 1.0], [1, 1, 1], 0, M_DIR_LIGHT],
+  MAT_DIRECT_SUNLIGHT: [[1, 1, 1], [1, 1, 1], 0, M_DIR_LIGHT],
+  MAT_MIRROR: [[1, 1, 1], [0, 0, 0], 0, M_SPEC],
+  MAT_BLACK: [[0, 0, 0], [0, 0, 0], 0, M_DIFF],
+  MAT_WHITE: [[1, 1, 1], [0, 0, 0], 0, M_DIFF],
+  MAT_RED: [[1, 0, 0], [0, 0, 0], 0, M_DIFF],
+  MAT_GREEN: [[0, 1, 0], [0, 0, 0], 0, M_DIFF],
+  MAT_BLUE: [[0, 0, 1], [0, 0, 0], 0, M_DIFF],
+  MAT_CORNELL_WHITE: [[1, 1, 1], [0, 0, 0], 0, M_DIFF],
+  MAT_CORNELL_RED: [[0.7, 0.12, 0.05], [0, 0, 0], 0, M_DIFF],
+  MAT_CORNELL_GREEN: [[0.2, 0.4, 0.36], [0, 0, 0], 0, M_DIFF],
+  MAT_YELLOW: [[1, 1, 0], [0, 0, 0], 0, M_DIFF],
+  MAT_PURPLE: [[0.50196078431, 0, 0.50196078431], [0, 0, 0], 0, M_DIFF],
+  MAT_COAT_NAVY: [[0, 0, 0.50196078431], [1, 1, 1], 1.4, M_COAT],
+  MAT_COAT_PURPLE: [[0.50196078431, 0, 0.50196078431], [0, 0, 0], 1.4, M_COAT],
+  MAT_COAT_WAX: [[0.9333, 0.6666, 0.6], [0.005, 0.005, 0.005], 1.4, M_COAT],
+};
+const TYPES = { SPHERE: T_SPHERE, PLANE: T_PLANE, BOX: T_BOX };
+
+// parse "vecN(a, b, ...)" with GLSL scalar broadcast
+function parseVec(s, n) {
+  const m = /vec\d\s*\(([^)]*)\)/.exec(s);
+  if (!m) throw new Error('bad vector: ' + s);
+  const v = m[1].split(',').map((t) => f(parseFloat(t)));
+  return { vals: Array.from({ length: n }, (_, i) => (v.length === 1 ? v[0] : v[i])), rest: s.slice(m.index + m[0].length) };
+}
+
+// Scene textarea grammar (index.html:624-653): "MAT, TYPE, vec3(pos), vec4(joker)"
+function parseScene(lines) {
+  const meshes = [], lights = [];
+  lines.forEach((line, i) => {
+    const parts = line.split(',');
+    const mat = parts[0].trim(), type = parts[1].trim();
+    if (!(mat in MATS)) throw new Error('unsupported material for the JS baseline: ' + mat);
+    if (!(type in TYPES)) throw new Error('unsupported mesh type for the JS baseline: ' + type);
+    if (mat.indexOf('MAT_LIGHT') >= 0) lights.push(i);
+    const rest = parts.slice(2).join(',');
+    const p = parseVec(rest, 3), j = parseVec(p.rest, 4);
+    const d = MATS[mat];
+    meshes.push({
+      t: TYPES[type], pos: V(...p.vals), joker: j.vals,
+      c: V(f(d[0][0]), f(d[0][1]), f(d[0][2])), e: V(f(d[1][0]), f(d[1][1]), f(d[1][2])), nt: f(d[2]), mt: d[3],
+    });
+  });
+  if (lights.length === 0) lights.push(-1);
+  return { meshes, lights };
+}
+
+// ---------------------------------------------------------- renderer
+class CpuRenderer {
+  // cfg: a tests/golden/configs.json entry; cornell: cfgs.cornell_lines; camera default
+  constructor(cfg, cornellLines, defaultCamera, width, height) {
+    const defs = Object.assign({ USE_PROCEDURAL_SKY: true, USE_BIASED_SAMPLING: true }, cfg.defines || {});
+    for (const k of ['USE_RESTIR', 'USE_SPECTRAL', 'USE_VOLUMETRICS', 'USE_CUBEMAP'])
+      if (defs[k]) throw new Error(k + ' is outside the JS baseline');
+    const c = Object.assign({
+      MAX_BOUNCES: 12, MAX_DIFF_BOUNCES: 4, MAX_SPEC_BOUNCES: 4, MAX_TRANS_BOUNCES: 12, MAX_SCATTERING_EVENTS: 12,
+      sample_lights: true, use_mis: false, use_restir: false,
+    }, cfg.constants || {});
+    if (c.use_restir) throw new Error('use_restir is outside the JS baseline');
+    this.sky = !!defs.USE_PROCEDURAL_SKY;
+    this.biased = !!defs.USE_BIASED_SAMPLING;
+    this.maxB = c.MAX_BOUNCES; this.maxD = c.MAX_DIFF_BOUNCES; this.maxS = c.MAX_SPEC_BOUNCES;
+    this.maxT = c.MAX_TRANS_BOUNCES; this.maxSc = c.MAX_SCATTERING_EVENTS;
+    this.sampleLights = !!c.sample_lights; this.mis = !!c.use_mis;
+    const sc = parseScene(cfg.scene_lines || cornellLines);
+    this.meshes = sc.meshes; this.lights = sc.lights;
+    this.w = width; this.h = height;
+    const cam = cfg.camera || defaultCamera;
+    this.camPos = V(f(cam.origin[0]), f(cam.origin[1]), f(cam.origin[2]));
+    this.camLook = V(f(cam.lookat[0]), f(cam.lookat[1]), f(cam.lookat[2]));
+    this.camParams = V(f(cam.fov), f(cam.aperture), f(cam.focalLength));
+    this.nIsect = 0;
+  }
+
+  // intersection(), raytracer.glsl:997-1082 -> {t, n, pos, index}
+  intersect(o, d) {
+    this.nIsect++;
+    let tmin = INF_T, type = -1, index = 0, n = V(0, 0, 0);
+    const ms = this.meshes;
+    for (let i = 0; i < ms.length; i++) {
+      const m = ms[i];
+      if (m.joker[0] === 0) continue;
+      if (m.t === T_SPHERE) {  // 818-833
+        const oc = sub(o, m.pos), b = dot(oc, d);
+        const c = f(dot(oc, oc) - f(m.joker[0] * m.joker[0]));
+        const disc = f(f(b * b) - c);
+        if (disc < 0) continue;
+        const sd = f(Math.sqrt(disc));
+        let t = f(-b - sd);
+        if (!(t > EPS && t < tmin)) { t = f(-b + sd); if (!(t > EPS && t < tmin)) continue; }
+        tmin = t; type = T_SPHERE; index = i;
+      } else if (m.t === T_PLANE) {  // 812-815
+        const t = f(f(-m.joker[0] - dot(m.pos, o)) / dot(m.pos, d));
+        if (t > EPS && t < tmin) { tmin = t; type = T_PLANE; index = i; }
+      } else {  // iBox 836-859
+        const mv = V(f(1 / d.x), f(1 / d.y), f(1 / d.z));
+        const nv = mul(mv, sub(m.pos, o));
+        const k = muls(muls(vabs(mv), m.joker[0]), 0.5);
+        const t1 = sub(nv, k), t2 = add(nv, k);
+        const tN = gmax(gmax(t1.x, t1.y), t1.z), tF = gmin(gmin(t2.x, t2.y), t2.z);
+        if (tN > tF || tF < 0) continue;
+        const t = tN > 0 ? tN : tF;
+        if (t < EPS || t >= tmin) continue;
+        const hp = sub(add(o, muls(d, t)), m.pos);
+        const half = f(m.joker[0] * 0.5);
+        const dd = sub(vabs(hp), V(half, half, half));
+        const s = V(sgn(hp.x), sgn(hp.y), sgn(hp.z));
+        const st = V(step(dd.y, dd.x) * step(dd.z, dd.x), step(dd.z, dd.y) * step(dd.x, dd.y),
+          step(dd.x, dd.z) * step(dd.y, dd.z));
+        n = normalize(mul(s, st));
+        tmin = t; type = T_BOX; index = i;
+      }
+    }
+    let pos = V(0, 0, 0);
+    if (type >= 0) {
+      pos = add(muls(d, tmin), o);
+      if (type === T_SPHERE) n = normalize(sub(pos, ms[index].pos));
+      else if (type === T_PLANE) n = normalize(ms[index].pos);
+    }
+    return { t: tmin, n, pos, index };
+  }
+
+  // 1092-1107
+  static binormals(n) {
+    const sig = n.z < 0 ? -1 : 1;
+    if (Math.abs(n.z) > f(0.99999)) return [V(1, 0, 0), V(0, sig, 0)];
+    const a = f(1 / f(sig - n.z)), b = f(f(n.x * n.y) * a);
+    return [V(f(1 + f(f(f(sig * n.x) * n.x) * a)), f(sig * b), f(-sig * n.x)), V(b, f(sig + f(f(n.y * n.y) * a)), -n.y)];
+  }
+  static frameDir(w, u, v, rx, ry) {
+    const om = f(Math.sqrt(f(1 - f(ry * ry))));
+    return normalize(add(add(muls(u, f(fcos(rx) * om)), muls(v, f(fsin(rx) * om))), muls(w, ry)));
+  }
+  // getSampleBiased (1109-1120) / getConeSample (1122-1133)
+  static coneSample(w, extent, seed) {
+    const [u, v] = CpuRenderer.binormals(w);
+    const r = hash2(seed, seed);
+    return CpuRenderer.frameDir(w, u, v, f(r[0] * TWO_PI), f(1 - f(r[1] * extent)));
+  }
+  randomDirection(n, seed) {
+    if (!this.biased) return CpuRenderer.coneSample(n, 1, seed);
+    const [u, v] = CpuRenderer.binormals(n);
+    const r = hash2(seed, seed);
+    return CpuRenderer.frameDir(n, u, v, f(r[0] * TWO_PI), gpow(r[1], f(1 / 2)));
+  }
+
+  // calcDirectLighting, 1174-1230
+  directLight(li, x, nl, seed) {
+    const L = this.meshes[li];
+    if (L.mt === M_LIGHT) {
+      if (L.t !== T_SPHERE) return V(0, 0, 0);
+      const sw = sub(L.pos, x);
+      const r2 = f(L.joker[0] * L.joker[0]), d2 = dot(sw, sw);
+      const cosA = f(Math.sqrt(f(1 - clamp(f(r2 / d2), 0, 1))));
+      const sr = CpuRenderer.coneSample(normalize(sw), f(1 - cosA), f(seed + f(23.1656)));
+      const hit = this.intersect(add(x, muls(nl, EPS)), sr);
+      const mh = this.meshes[hit.index];
+      if (mh.mt !== M_LIGHT) return V(0, 0, 0);
+      const weight = f(2 * f(1 - cosA));
+      return muls(muls(mul(vmaxs(mh.c, f(0.001)), mh.e), weight), gmax(f(0.001), dot(sr, nl)));
+    }
+    if (L.mt === M_DIR_LIGHT) {
+      const hit = this.intersect(add(x, muls(nl, EPS)), L.pos);
+      if (hit.t === INF_T) return muls(mul(L.c, L.e), gmax(f(0.001), dot(L.pos, nl)));
+    }
+    return V(0, 0, 0);
+  }
+  // 1233-1262
+  static power(f1, g1) {
+    const denom = f(f(f1 * f1) + f(g1 * g1));
+    const r = f(f(f1 * f1) / denom);
+    return r > 0 ? r : 0;  // max(0, 0/0) -> 0 (IEEE maxNum; DESIGN.md deviation)
+  }
+  static cosPdf(wi, n) { return f(gmax(0, dot(wi, n)) * ONE_OVER_PI); }
+  static lightPdf(L, x) {
+    if (L.mt !== M_LIGHT) return 0;
+    if (L.t === T_SPHERE) {
+      const d = sub(L.pos, x);
+      const d2 = dot(d, d), r2 = f(L.joker[0] * L.joker[0]);
+      if (d2 <= r2) return 0;
+      const ctm = f(Math.sqrt(gmax(0, f(1 - f(r2 / d2)))));
+      const denom = f(1 - ctm);
+      if (denom < f(1e-6)) return 0;
+      return f(1 / f(TWO_PI * denom));
+    }
+    return f(1 / FOUR_PI);
+  }
+
+  // radiance() + brdf(), 1986-2105 and 1804-1980
+  radiance(ro, rd, seed, frame) {
+    let acc = V(0, 0, 0), mask = V(1, 1, 1), spec = true, prevNl = V(0, 1, 0);
+    let diffB = 0, specB = 0, scat = 0;
+    const fr = f(frame);
+    for (let depth = 0; depth < this.maxB; depth++) {
+      const hit = this.intersect(ro, rd);
+      if (hit.t === INF_T) {
+        if (!spec && this.sampleLights) break;
+        if (this.sky) {
+          const k = clamp(f(f(rd.y * f(0.6)) + 0.5), f(0.3), 1);
+          const sky = V(f(0.5 + f(0.5 * fcos(f(TWO_PI * f(f(0.525) + f(f(0.9) * k)))))),
+            f(0.5 + f(0.5 * fcos(f(TWO_PI * f(f(0.408) + f(f(0.97) * k)))))),
+            f(0.5 + f(0.5 * fcos(f(TWO_PI * f(f(0.409) + f(f(0.8) * k)))))));
+          acc = add(acc, mul(mask, sky));
+        }
+        break;
+      }
+      const m = this.meshes[hit.index];
+      const c = vmaxs(m.c, f(0.001)), e = vmaxs(m.e, f(0.001));
+      const inside = -sgn(dot(rd, hit.n));
+      if (m.mt === M_LIGHT) {
+        mask = mul(mask, c);
+        let w = 1;
+        if (this.mis && !spec && this.sampleLights && depth > 0) {
+          const ld = normalize(sub(hit.pos, ro));
+          w = CpuRenderer.power(CpuRenderer.cosPdf(ld, prevNl), CpuRenderer.lightPdf(m, ro));
+        }
+        acc = add(acc, muls(mul(mask, e), w));
+        break;
+      }
+      prevNl = muls(hit.n, inside);
+      const x = hit.pos, nl = prevNl, bounce = f(depth);
+      const rdir = this.randomDirection(nl, f(f(f(seed + f(f(7.1) * fr)) + f(5681.123)) + f(bounce * f(92.13))));
+      const rough = mul(e, rdir);
+      const nc = f(1.00029), nt = Math.abs(m.nt), mt = m.mt;
+      if (mt === M_DIFF) {
+        ro = add(x, muls(nl, EPS)); rd = rdir; mask = mul(mask, c); diffB++; spec = false;
+      } else if (mt === M_SPEC) {
+        ro = add(x, muls(nl, EPS)); rd = normalize(add(rough, reflect(rd, nl))); mask = mul(mask, c); specB++; spec = true;
+      } else if (mt === M_REFR_FRESNEL || mt === M_REFR_SCHLICK) {
+        const nnt = inside < 0 ? f(nt / nc) : f(nc / nt);
+        let tdir = refract(rd, nl, nnt);
+        if (length(tdir) === 0) {
+          ro = add(x, muls(nl, EPS)); rd = normalize(add(rough, reflect(rd, nl))); specB++; spec = true;
+        } else {
+          tdir = normalize(add(rough, tdir));
+          let Re;
+          if (mt === M_REFR_FRESNEL) {
+            const cosI = dot(rd, nl), cosT = dot(nl, tdir);
+            const rs = f(f(f(nc * cosI) - f(nt * cosT)) / f(f(nc * cosI) + f(nt * cosT)));
+            const rp = f(f(f(nc * cosT) - f(nt * cosI)) / f(f(nc * cosT) + f(nt * cosI)));
+            Re = f(f(f(rs * rs) + f(rp * rp)) * 0.5);
+          } else {
+            const q = f(f(nc - nt) / f(nc + nt)), R0 = f(q * q);
+            Re = f(R0 + f(f(1 - R0) * gpow(f(1 + dot(nl, rd)), 5)));
+          }
+          if (hash(seed) < Re) {
+            ro = add(x, muls(nl, EPS)); rd = normalize(add(rough, reflect(rd, nl))); specB++;
+          } else {
+            ro = sub(x, muls(nl, EPS)); mask = mul(mask, c); rd = tdir; scat++;
+          }
+          spec = true;
+        }
+      } else if (mt === M_COAT) {
+        ro = add(x, muls(nl, EPS));
+        const q = f(f(nc - nt) / f(nc + nt)), R0 = f(q * q);
+        const Re = f(R0 + f(f(1 - R0) * gpow(f(1 + dot(nl, rd)), 5)));
+        if (hash(seed) < Re) { rd = normalize(add(rough, reflect(rd, nl))); specB++; spec = true; } else {
+          rd = rdir; mask = mul(mask, c); diffB++; spec = false;
+        }
+      }
+      if (!spec && this.sampleLights) {  // 1899-1976
+        const base = f(f(f(seed + f(f(8652.1) * fr)) + f(5681.123)) + f(bounce * f(7895.13)));
+        let lc = V(0, 0, 0);
+        for (let i = 0; i < this.lights.length; i++) {
+          const idx = this.lights[i];
+          if (idx < 0) continue;
+          if (this.mis) {
+            const L = this.meshes[idx];
+            if (L.mt !== M_LIGHT) continue;
+            const ls = this.directLight(idx, x, nl, f(base + f(f(i) * f(123.456))));
+            if (dot(ls, ls) > f(0.000001)) {
+              const ld = normalize(sub(L.pos, x));
+              lc = add(lc, muls(ls, CpuRenderer.power(CpuRenderer.lightPdf(L, x), CpuRenderer.cosPdf(ld, nl))));
+            }
+          } else {
+            acc = add(acc, mul(this.directLight(idx, x, nl, base), mask));
+          }
+        }
+        if (this.mis) acc = add(acc, mul(lc, mask));
+      }
+      if (vmaxc(mask) < f(0.01)) break;
+      if (diffB >= this.maxD || specB >= this.maxS || 0 >= this.maxT || scat >= this.maxSc) break;
+    }
+    return acc;
+  }
+
+  // main(), 2111-2180: one sample of pixel (px, py) (py counted from the bottom)
+  sample(px, py, frame) {
+    const rx = f(this.w), ry = f(this.h);
+    const fcx = f(px + 0.5), fcy = f(py + 0.5);
+    const stx = f(f(f(2 * fcx) / rx) - 1), sty = f(f(f(2 * fcy) / ry) - 1);
+    const seed = hash(f(f(f(fcx * f(12.9898)) + f(fcy * f(78.233))) + f(f(1113.1) * f(frame))));
+    const uVLen = f(Math.tan(f(f(this.camParams.x * RAD) * 0.5)));
+    const uULen = f(f(rx / ry) * uVLen);
+    const w = normalize(this.camLook);
+    const u = normalize(cross(w, V(0, 1, 0)));
+    const v = cross(u, w);
+    const ax = hash(f(seed + f(13.271))), ay = hash(f(seed + f(63.216)));
+    const flx = step(0.5, ax), fly = step(0.5, ay);
+    const hx = mixf(ax, f(1 - ax), flx), hy = mixf(ay, f(1 - ay), fly);
+    const sx = f(Math.sqrt(f(2 * hx))), sy = f(Math.sqrt(f(2 * hy)));
+    const dx = f(f(mixf(f(sx - 1), f(1 - sx), flx) / f(rx * 0.5)) + stx);
+    const dy = f(f(mixf(f(sy - 1), f(1 - sy), fly) / f(ry * 0.5)) + sty);
+    const fp = muls(normalize(add(add(muls(muls(u, dx), uULen), muls(muls(v, dy), uVLen)), w)), this.camParams.z);
+    const ang = f(hash(f(seed + f(496.4562))) * TWO_PI);
+    const rad = f(hash(f(seed + f(249.1686))) * this.camParams.y);
+    const ap = muls(add(muls(u, fcos(ang)), muls(v, fsin(ang))), rad);
+    return this.radiance(add(this.camPos, ap), normalize(sub(fp, ap)), seed, frame);
+  }
+
+  // rows [y0, y1) of passes frame0..frame0+n-1 accumulated: Float32Array RGBA
+  render(frame0, n, y0, y1) {
+    const out = new Float32Array((y1 - y0) * this.w * 4);
+    for (let y = y0; y < y1; y++) {
+      for (let x = 0; x < this.w; x++) {
+        const o = ((y - y0) * this.w + x) * 4;
+        for (let k = 0; k < n; k++) {
+          const s = this.sample(x, y, frame0 + k);
+          out[o] = f(out[o] + s.x);
+          out[o + 1] = f(out[o + 1] + s.y);
+          out[o + 2] = f(out[o + 2] + s.z);
+        }
+      }
+    }
+    return out;
+  }
+}
+
+module.exports = { CpuRenderer, hash, hash2, parseScene };
