@@ -82,4 +82,11 @@ struct LaunchParams {
   // *halo_miss (null when the whole image is local).
   int32_t valid_lo, valid_hi;
   uint32_t *halo_miss;
+  // Frame-chunked launch (few pixels per device, e.g. 8-way sharding): grid.z
+  // = chunk index, each lane renders frames [z*frame_chunk, +frame_chunk) of
+  // its pixel into samples[frame][launch pixel]; rt0_sum_kernel then adds them
+  // to the accumulator in frame order (the same sequential sum).  samples ==
+  // null: one chunk, accumulated in registers.
+  int32_t frame_chunk;
+  float4 *samples;
 };

@@ -1139,18 +1139,29 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   if (py >= P.height) return;
   Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT> it(P, sc, cfg);
   const size_t pix = (size_t)py * P.width + px;
-  float4 a = P.accum[pix];
-  for (int f = 0; f < P.nframes; ++f) {
-    it.frame = P.frame0 + (uint32_t)f;
-    v3 s = it.sample(px, py);
-    {
-#pragma clang fp contract(off)
-      a.x += opq(s.x);
-      a.y += opq(s.y);
-      a.z += opq(s.z);
+  if (!RESTIR && P.samples) {  // frame-chunked: samples out, rt0_sum_kernel accumulates
+    const int f0 = (int)blockIdx.z * P.frame_chunk;
+    const int f1 = min(P.nframes, f0 + P.frame_chunk);
+    const size_t plane = (size_t)P.n_band_rows * P.width, lp = (size_t)r * P.width + px;
+    for (int f = f0; f < f1; ++f) {
+      it.frame = P.frame0 + (uint32_t)f;
+      v3 s = it.sample(px, py);
+      P.samples[(size_t)f * plane + lp] = make_float4(s.x, s.y, s.z, 0.f);
     }
+  } else {
+    float4 a = P.accum[pix];
+    for (int f = 0; f < P.nframes; ++f) {
+      it.frame = P.frame0 + (uint32_t)f;
+      v3 s = it.sample(px, py);
+      {
+#pragma clang fp contract(off)
+        a.x += opq(s.x);
+        a.y += opq(s.y);
+        a.z += opq(s.z);
+      }
+    }
+    P.accum[pix] = a;
   }
-  P.accum[pix] = a;
   if constexpr (RESTIR) {
     if (P.rout_main == nullptr || P.rout_aux == nullptr) return;
     if (it.flag(F_RESTIR_DEF)) {
@@ -1169,6 +1180,27 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     atomicAdd(&P.counters[3], it.n_map);
     atomicAdd(&P.counters[4], (unsigned long long)P.nframes);
   }
+}
+
+// Frame-chunked launches: accumulator += samples of frames 0..nframes-1 in
+// order -- the same sequential fp32 sum as the in-register loop above.
+DEV void sum_body(const LaunchParams &P) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int px = blockIdx.x * 16 + (lane & 7) + ((wave & 1) << 3);
+  const int r = blockIdx.y * 16 + (lane >> 3) + ((wave >> 1) << 3);
+  if (px >= P.width || r >= P.n_band_rows) return;
+  const int py = image_row(P, r);
+  if (py >= P.height) return;
+  const size_t pix = (size_t)py * P.width + px;
+  const size_t plane = (size_t)P.n_band_rows * P.width, lp = (size_t)r * P.width + px;
+  float4 a = P.accum[pix];
+  for (int f = 0; f < P.nframes; ++f) {
+    const float4 s = P.samples[(size_t)f * plane + lp];
+    a.x += s.x;
+    a.y += s.y;
+    a.z += s.z;
+  }
+  P.accum[pix] = a;
 }
 
 }  // namespace rt0

@@ -255,9 +255,9 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, void **fn_out, std::
   return RT0_OK;
 }
 
-int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, void *stream) {
+int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, unsigned gz, void *stream) {
   void *args[] = {(void *)p};
-  hipError_t e = hipModuleLaunchKernel((hipFunction_t)fn, gx, gy, 1, 256, 1, 1, 0, (hipStream_t)stream, args, nullptr);
+  hipError_t e = hipModuleLaunchKernel((hipFunction_t)fn, gx, gy, gz, 256, 1, 1, 0, (hipStream_t)stream, args, nullptr);
   return e == hipSuccess ? RT0_OK : RT0_E_HIP;
 }
 

@@ -29,6 +29,6 @@ SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, const int32_t *li, in
 // Compile (or fetch from the process cache) the kernel for this scene/config on
 // `device`; *fn receives a hipFunction_t.
 int jit_get(const SceneDev &s, const JitKey &k, int device, void **fn, std::string &err);
-int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, void *stream);
+int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, unsigned gz, void *stream);
 
 }  // namespace rt0h

@@ -14,6 +14,10 @@ __global__ __launch_bounds__(256) void rt0_pass_kernel(const LaunchParams P) {
   pass_body<DynScene, DynCfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>(P, DynScene{P.scene}, DynCfg(P));
 }
 
+// frame-chunked launches: ordered sum of the per-frame samples (HBM-bound,
+// 16 B/sample read + 32 B/pixel)
+__global__ __launch_bounds__(256) void rt0_sum_kernel(const LaunchParams P) { sum_body(P); }
+
 // tonemapper.glsl:28-33: pow(acc * u_cont, 1/2.2), written to an RGBA8 canvas
 __global__ __launch_bounds__(256) void rt0_tonemap_kernel(const float4 *__restrict__ acc, uchar4 *__restrict__ out,
                                                           int n, float cont) {
@@ -39,6 +43,11 @@ extern "C" hipError_t rt0_launch_pass(int variant, const LaunchParams *p, dim3 g
     case 4: hipLaunchKernelGGL((rt0_pass_kernel<true, true, true, true, true>), grid, block, 0, stream, *p); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t rt0_launch_sum(const LaunchParams *p, dim3 grid, hipStream_t stream) {
+  hipLaunchKernelGGL(rt0_sum_kernel, dim3(grid.x, grid.y), dim3(256), 0, stream, *p);
   return hipGetLastError();
 }
 
