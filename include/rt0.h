@@ -133,6 +133,29 @@ int rt0_get_size(const rt0_ctx *ctx, int *width, int *height);
 /* Display epilogue, tonemapper.glsl:28-33: rgba8 = 255*pow(acc*cont, 1/2.2),
  * alpha 255, cont = 1/passes (index.js:1089). */
 int rt0_tonemap(rt0_ctx *ctx, float contribution, uint8_t *rgba8_out);
+/* Same with a curve: RT0_TONEMAP_GAMMA (= rt0_tonemap), RT0_TONEMAP_ACES
+ * (tonemapper.glsl's unused ACESFilm, 17-26, at its exposure 1.5) or
+ * RT0_TONEMAP_REINHARD (x/(1+x), the README:22 claim) -- the last two are
+ * not used by the reference (parity unpinned); gamma 1/2.2 follows both. */
+#define RT0_TONEMAP_GAMMA 0
+#define RT0_TONEMAP_ACES 1
+#define RT0_TONEMAP_REINHARD 2
+int rt0_tonemap_ex(rt0_ctx *ctx, float contribution, int mode, uint8_t *rgba8_out);
+
+/* Image files: PNG for texture assets and the display canvas, PFM
+ * for the HDR accumulator.  Host-only, no context needed.
+ *   rt0_png_decode / rt0_png_read: 8-bit gray / RGB / palette / gray+alpha /
+ *     RGBA, non-interlaced -> RGBA8, row 0 = the file's first row; the buffer
+ *     is malloc'd, release it with rt0_free.
+ *   rt0_png_write: RGBA8; flip_y = 1 writes row h-1 first (accumulator /
+ *     canvas rows are bottom-up, PNG rows top-down).
+ *   rt0_pfm_write: RGB float32 of a W*H*4 buffer times `scale` (1/passes),
+ *     rows bottom-up as PFM stores them. */
+int rt0_png_decode(const uint8_t *data, size_t size, int *w, int *h, uint8_t **rgba_out);
+int rt0_png_read(const char *path, int *w, int *h, uint8_t **rgba_out);
+int rt0_png_write(const char *path, int w, int h, const uint8_t *rgba, int flip_y);
+int rt0_pfm_write(const char *path, int w, int h, const float *rgba, float scale);
+void rt0_free(void *p);
 
 /* ReSTIR reservoir MRTs (raytracer.glsl:2171-2179).  which: 0 = current output
  * (restir_buffer/aux of the last pass), 1 = history1, 2 = history2.  main/aux:

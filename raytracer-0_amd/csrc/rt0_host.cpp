@@ -21,7 +21,8 @@
 #include "rt0_jit.h"
 
 extern "C" hipError_t rt0_launch_pass(int variant, const LaunchParams *p, dim3 grid, hipStream_t stream);
-extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, float cont, hipStream_t stream);
+extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, float cont, int mode,
+                                         hipStream_t stream);
 extern "C" hipError_t rt0_launch_sum(const LaunchParams *p, dim3 grid, hipStream_t stream);
 
 // A pass launch with fewer than kTargetWaves waves (16 per SIMD of the 1024
@@ -572,11 +573,13 @@ int rt0_get_size(const rt0_ctx *c, int *w, int *h) {
   return RT0_OK;
 }
 
-int rt0_tonemap(rt0_ctx *c, float contribution, uint8_t *out) {
-  if (!c || !out) return RT0_E_ARG;
+int rt0_tonemap(rt0_ctx *c, float contribution, uint8_t *out) { return rt0_tonemap_ex(c, contribution, 0, out); }
+
+int rt0_tonemap_ex(rt0_ctx *c, float contribution, int mode, uint8_t *out) {
+  if (!c || !out || mode < 0 || mode > 2) return RT0_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   int n = c->W * c->H;
-  HIPCHK(c, rt0_launch_tonemap(c->acc(), c->d_tonemap, n, contribution, c->stream));
+  HIPCHK(c, rt0_launch_tonemap(c->acc(), c->d_tonemap, n, contribution, mode, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(out, c->d_tonemap, (size_t)n * sizeof(uchar4), hipMemcpyDeviceToHost));
   return RT0_OK;

@@ -18,14 +18,24 @@ __global__ __launch_bounds__(256) void rt0_pass_kernel(const LaunchParams P) {
 // 16 B/sample read + 32 B/pixel)
 __global__ __launch_bounds__(256) void rt0_sum_kernel(const LaunchParams P) { sum_body(P); }
 
-// tonemapper.glsl:28-33: pow(acc * u_cont, 1/2.2), written to an RGBA8 canvas
+// Display epilogue, written to an RGBA8 canvas.  mode 0 = the reference's
+// tonemapper.glsl:28-33, pow(acc * u_cont, 1/2.2).  Modes 1/2 are not used by
+// the reference (parity unpinned): 1 = its unused ACESFilm (17-26) on
+// exposure 1.5 (12), 2 = the Reinhard curve the README claims (README:22).
 __global__ __launch_bounds__(256) void rt0_tonemap_kernel(const float4 *__restrict__ acc, uchar4 *__restrict__ out,
-                                                          int n, float cont) {
+                                                          int n, float cont, int mode) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float4 a = acc[i];
   auto g = [&](float x) {
-    float v = __powf(fmaxf(x * cont, 0.0f), 1.0f / 2.2f);
+    x = x * cont;
+    if (mode == 1) {
+      x *= 1.5f;
+      x = (x * (2.51f * x + 0.03f)) / (x * (2.43f * x + 0.59f) + 0.14f);
+    } else if (mode == 2) {
+      x = x / (1.0f + x);
+    }
+    float v = __powf(fmaxf(x, 0.0f), 1.0f / 2.2f);
     v = fminf(fmaxf(v, 0.0f), 1.0f);
     return (unsigned char)(v * 255.0f + 0.5f);
   };
@@ -51,7 +61,8 @@ extern "C" hipError_t rt0_launch_sum(const LaunchParams *p, dim3 grid, hipStream
   return hipGetLastError();
 }
 
-extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, float cont, hipStream_t stream) {
-  hipLaunchKernelGGL(rt0_tonemap_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, acc, out, n, cont);
+extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, float cont, int mode,
+                                         hipStream_t stream) {
+  hipLaunchKernelGGL(rt0_tonemap_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, acc, out, n, cont, mode);
   return hipGetLastError();
 }

@@ -28,7 +28,11 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_render_async", "rt0_sync", "rt0_read_accum", "rt0_write_accum", "rt0_clear", "rt0_resize",
            "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
-           "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting", "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version"]
+           "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
+           "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
+           "rt0_png_write", "rt0_pfm_write", "rt0_free"]
+
+TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
 
 
 class Rt0Error(RuntimeError):
@@ -105,6 +109,12 @@ def lib():
         "rt0_read_counters": (c_int, [c_void_p, P(ctypes.c_uint64)]),
         "rt0_last_kernel_ms": (c_int, [c_void_p, P(c_float), P(c_int)]),
         "rt0_version": (ctypes.c_char_p, []),
+        "rt0_tonemap_ex": (c_int, [c_void_p, c_float, c_int, P(ctypes.c_uint8)]),
+        "rt0_png_decode": (c_int, [c_void_p, ctypes.c_size_t, P(c_int), P(c_int), P(P(ctypes.c_uint8))]),
+        "rt0_png_read": (c_int, [ctypes.c_char_p, P(c_int), P(c_int), P(P(ctypes.c_uint8))]),
+        "rt0_png_write": (c_int, [ctypes.c_char_p, c_int, c_int, P(ctypes.c_uint8), c_int]),
+        "rt0_pfm_write": (c_int, [ctypes.c_char_p, c_int, c_int, fp, c_float]),
+        "rt0_free": (None, [c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -147,6 +157,45 @@ def parse_scene(scene_text, sdf_meshes=()):
     if rc != RT0_OK:
         raise Rt0Error(rc, "cannot parse scene")
     return list(meshes[:ne.value + ns.value]), ne.value, ns.value, list(lights[:nl.value])
+
+
+def _check_io(rc, what):
+    if rc != 0:
+        raise Rt0Error(rc, what)
+
+
+def png_decode(data):
+    """PNG bytes -> [h, w, 4] uint8 (row 0 = the file's first row)."""
+    w, h, p = ctypes.c_int(), ctypes.c_int(), ctypes.POINTER(ctypes.c_uint8)()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    _check_io(lib().rt0_png_decode(buf, len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(p)), "png_decode")
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 4)).copy()
+    finally:
+        lib().rt0_free(p)
+
+
+def png_read(path):
+    w, h, p = ctypes.c_int(), ctypes.c_int(), ctypes.POINTER(ctypes.c_uint8)()
+    _check_io(lib().rt0_png_read(str(path).encode(), ctypes.byref(w), ctypes.byref(h), ctypes.byref(p)),
+              "png_read %s" % path)
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 4)).copy()
+    finally:
+        lib().rt0_free(p)
+
+
+def png_write(path, rgba, flip_y=False):
+    a = np.ascontiguousarray(rgba, dtype=np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError("[h, w, 4] uint8 expected")
+    _check_io(lib().rt0_png_write(str(path).encode(), a.shape[1], a.shape[0],
+                                  a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), int(bool(flip_y))), "png_write")
+
+
+def pfm_write(path, rgba, scale=1.0):
+    a = np.ascontiguousarray(rgba, dtype=np.float32)
+    _check_io(lib().rt0_pfm_write(str(path).encode(), a.shape[1], a.shape[0], _fp(a), scale), "pfm_write")
 
 
 def jit_compile(scene_text, sdf_meshes, cfg):
@@ -286,10 +335,19 @@ class Renderer:
         self._chk(lib().rt0_resize(self.h, w, h))
         self.width, self.height = w, h
 
-    def tonemap(self, contribution):
+    def tonemap(self, contribution, mode=TONEMAP_GAMMA):
+        """RGBA8 canvas (rows bottom-up, like the accumulator)."""
         out = np.empty((self.height, self.width, 4), np.uint8)
-        self._chk(lib().rt0_tonemap(self.h, contribution, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        self._chk(lib().rt0_tonemap_ex(self.h, contribution, mode, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return out
+
+    def save_png(self, path, passes, mode=TONEMAP_GAMMA):
+        """Tonemapped image (contribution 1/passes) as a top-down PNG."""
+        png_write(path, self.tonemap(1.0 / max(1, passes), mode), flip_y=True)
+
+    def save_pfm(self, path, passes):
+        """HDR radiance (accumulator / passes) as PFM."""
+        pfm_write(path, self.read_accum(), 1.0 / max(1, passes))
 
     def read_restir(self, which=0):
         m = np.empty((self.height, self.width, 4), np.float32)

@@ -172,3 +172,23 @@ def test_sharded_restir_reports_a_too_small_halo(cfgs, gpu_required):
     assert shards[1][0].halo_misses() > 0  # the middle block reads 16 px away
     with pytest.raises(rt0.Rt0Error):
         shards[0][0].render(3, 2)  # sharded ReSTIR: one pass per call
+
+
+def test_tonemap_curves_and_image_files(cfgs, gpu_required, tmp_path):
+    """Display epilogue variants + PNG/PFM output of a rendered image."""
+    PIL = pytest.importorskip("PIL.Image")
+    r = rt0.Renderer(32, 24)
+    rt0.configure(r, cfg_by_name(cfgs, "c2_cornell_mis_8"), cfgs)
+    r.render(1, 4)
+    acc = r.read_accum()
+    x = np.maximum(acc[..., :3] * 0.25, 0)
+    for mode, curve in ((rt0.TONEMAP_GAMMA, x), (rt0.TONEMAP_REINHARD, x / (1 + x)),
+                        (rt0.TONEMAP_ACES, (1.5 * x * (2.51 * 1.5 * x + 0.03)) / (1.5 * x * (2.43 * 1.5 * x + 0.59) + 0.14))):
+        img = r.tonemap(0.25, mode)
+        ref = np.clip(np.power(np.maximum(curve, 0), 1 / 2.2), 0, 1) * 255
+        assert np.abs(img[..., :3].astype(np.float32) - ref).max() <= 1.0, mode
+    r.save_png(tmp_path / "c.png", 4)
+    assert np.array_equal(np.asarray(PIL.open(tmp_path / "c.png").convert("RGBA")), r.tonemap(0.25)[::-1])
+    r.save_pfm(tmp_path / "c.pfm", 4)
+    raw = open(tmp_path / "c.pfm", "rb").read()
+    assert raw.startswith(b"PF\n32 24\n-1.0\n") and len(raw) == len(b"PF\n32 24\n-1.0\n") + 32 * 24 * 12
