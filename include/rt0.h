@@ -59,7 +59,12 @@ typedef struct rt0_config {
 /* Mesh record = the reference's `Mesh` struct (raytracer.glsl:239-244) with its
  * `Material` (157-163) flattened.  type: 0 SPHERE 1 PLANE 2 BOX 3 SDF.
  * mat_type: 0 LIGHT 1 DIR_LIGHT 2 DIFF 3 SPEC 4 REFR_FRESNEL 5 REFR_SCHLICK 6 COAT.
- * tex_type: -1 = NULL_TEX (the only value supported so far).
+ * tex_type: the material's `Texture.t` (raytracer.glsl:112-121): -1 NULL_TEX,
+ *   0..3 TEXTURE0..3 (image units, rt0_set_texture), 4 VORONOI, 5 GRADIENT_NOISE,
+ *   6 VALUE_NOISE, 7 CHECK, 8 RIPPLE, 9 METAL (4/6/9 read the noise texture).
+ * tex_c_mask / tex_e_mask / tex_params: the rest of that `Texture` (124-128).
+ * mat_opts: Material.opts (161) as bits -- 1 colour texture, 2 emission /
+ *   glossiness texture, 4 bump (unused by the reference), 8 backface flag.
  * sdf_kind (type == SDF only): the index.html:702-717 selector value
  * (0 sdBox 1 udRoundBox 2 sdSphere 3 sdTriPrism 4 sdCone 5 MengerSponge 6 Mandelbulb). */
 typedef struct rt0_mesh {
@@ -72,6 +77,10 @@ typedef struct rt0_mesh {
   float pos[3];
   float joker[4];
   int32_t sdf_kind;
+  float tex_c_mask[3];
+  float tex_e_mask[3];
+  float tex_params[4];
+  uint32_t mat_opts;
 } rt0_mesh;
 
 typedef struct rt0_ctx rt0_ctx;
@@ -106,6 +115,18 @@ int rt0_parse_scene_glsl(const char *scene_text, const char *const *sdf_meshes, 
                          int *n_lights);
 int rt0_get_scene(const rt0_ctx *ctx, rt0_mesh *meshes, int max_meshes, int *n_meshes, int *n_sdfs,
                   int32_t *light_index, int max_lights, int *n_lights);
+
+/* Asset textures, replacing GlslViewport.loadTexture (index.js:699-728) for
+ * the image textures opts.textures[0..3] (units u_tex0..3, index.js:276-296)
+ * and the RGBA noise image rgba_noise256.png (u_rnd_tex, index.js:258-273):
+ * unit 0..3 = TEXTURE0..3, RT0_TEX_NOISE = the noise texture.  rgba8: w*h RGBA
+ * bytes, first row = the image's top row (WebGL's upload without FLIP_Y puts
+ * it at t = 0); sampled GL_LINEAR with GL_REPEAT at level 0 like the
+ * reference.  rgba8 = NULL unbinds the unit (an unbound unit samples
+ * (0,0,0,1), the GL value of an incomplete texture).  Copied to the device;
+ * the caller keeps ownership. */
+#define RT0_TEX_NOISE 4
+int rt0_set_texture(rt0_ctx *ctx, int unit, int w, int h, const uint8_t *rgba8);
 
 /* Uniforms u_camPos, u_camLookAt (a direction), u_camParams = (fov deg,
  * aperture, focal length) (index.js:421-423). */

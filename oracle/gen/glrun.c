@@ -69,6 +69,14 @@ typedef intptr_t GLsizeiptr;
 #define GL_RGBA 0x1908
 #define GL_RGBA32F 0x8814
 #define GL_FLOAT 0x1406
+#define GL_RGBA8 0x8058
+#define GL_RGB 0x1907
+#define GL_RGB8 0x8051
+#define GL_UNSIGNED_BYTE 0x1401
+#define GL_REPEAT 0x2901
+#define GL_TEXTURE_CUBE_MAP 0x8513
+#define GL_TEXTURE_CUBE_MAP_POSITIVE_X 0x8515
+#define GL_UNPACK_ALIGNMENT 0x0CF5
 #define GL_FRAMEBUFFER 0x8D40
 #define GL_COLOR_ATTACHMENT0 0x8CE0
 #define GL_FRAMEBUFFER_COMPLETE 0x8CD5
@@ -108,6 +116,7 @@ F(void, glBindTexture, (GLenum, GLuint))
 F(void, glActiveTexture, (GLenum))
 F(void, glTexParameteri, (GLenum, GLenum, GLint))
 F(void, glTexImage2D, (GLenum, GLint, GLint, GLsizei, GLsizei, GLint, GLenum, GLenum, const void *))
+F(void, glPixelStorei, (GLenum, GLint))
 F(void, glGenFramebuffers, (GLsizei, GLuint *))
 F(void, glBindFramebuffer, (GLenum, GLuint))
 F(void, glFramebufferTexture2D, (GLenum, GLenum, GLenum, GLuint, GLint))
@@ -162,7 +171,7 @@ static void load(void) {
   L(gles, glGenBuffers) L(gles, glBindBuffer) L(gles, glBufferData)
   L(gles, glEnableVertexAttribArray) L(gles, glVertexAttribPointer)
   L(gles, glViewport) L(gles, glDrawArrays) L(gles, glReadPixels)
-  L(gles, glFinish) L(gles, glGetError)
+  L(gles, glFinish) L(gles, glGetError) L(gles, glPixelStorei)
 #undef L
 }
 
@@ -206,6 +215,49 @@ static GLuint mktex(int w, int h, const float *data) {
   return t;
 }
 
+/* An RGBA8 asset texture as GlslViewport.loadTexture creates it (index.js:
+ * 703-727): REPEAT, LINEAR mag/min filtering; file = raw w*h*4 bytes, first row
+ * = the image's first (top) row, which WebGL uploads to t = 0. */
+static unsigned char *slurp_bytes(const char *fn, size_t n) {
+  FILE *f = fopen(fn, "rb");
+  if (!f) die("cannot open texture file");
+  unsigned char *b = (unsigned char *)malloc(n);
+  if (fread(b, 1, n, f) != n) die("short texture file");
+  fclose(f);
+  return b;
+}
+static GLuint mktex8(int w, int h, const char *fn) {
+  unsigned char *b = slurp_bytes(fn, (size_t)w * h * 4);
+  GLuint t;
+  p_glGenTextures(1, &t);
+  p_glBindTexture(GL_TEXTURE_2D, t);
+  p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_WRAP_S, GL_REPEAT);
+  p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_WRAP_T, GL_REPEAT);
+  p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_MAG_FILTER, GL_LINEAR);
+  p_glTexParameteri(GL_TEXTURE_2D, GL_TEXTURE_MIN_FILTER, GL_LINEAR);
+  p_glTexImage2D(GL_TEXTURE_2D, 0, GL_RGBA8, w, h, 0, GL_RGBA, GL_UNSIGNED_BYTE, b);
+  free(b);
+  return t;
+}
+/* The cubemap of index.js:300-331: six RGB8 faces in the reference's target
+ * order (-X, -Y, -Z, +X, +Y, +Z), MIN_FILTER LINEAR, default wrap/mag.
+ * file = 6 consecutive size*size*3 faces. */
+static GLuint mkcube(int size, const char *fn) {
+  size_t face = (size_t)size * size * 3;
+  unsigned char *b = slurp_bytes(fn, face * 6);
+  static const int target_of[6] = {1, 3, 5, 0, 2, 4}; /* -X -Y -Z +X +Y +Z -> GL enum offsets */
+  GLuint t;
+  p_glGenTextures(1, &t);
+  p_glBindTexture(GL_TEXTURE_CUBE_MAP, t);
+  p_glPixelStorei(GL_UNPACK_ALIGNMENT, 1);
+  for (int i = 0; i < 6; i++)
+    p_glTexImage2D(GL_TEXTURE_CUBE_MAP_POSITIVE_X + target_of[i], 0, GL_RGB8, size, size, 0, GL_RGB, GL_UNSIGNED_BYTE,
+                   b + face * i);
+  p_glTexParameteri(GL_TEXTURE_CUBE_MAP, GL_TEXTURE_MIN_FILTER, GL_LINEAR);
+  free(b);
+  return t;
+}
+
 static void dump(const char *prefix, int frame, const char *tag, int w, int h,
                  GLuint fb, int attachment) {
   size_t n = (size_t)w * h * 4;
@@ -227,6 +279,10 @@ int main(int argc, char **argv) {
   int w = 64, h = 64, frames = 4, single = 0, restir_out = 0;
   float cam[9] = {0, 0, 2.8f, 0, 0, -1, 50, 0, 3.5f};
   float time_ms = 0.0f;
+  const char *tex_file[6] = {0};
+  int tex_w[6] = {0}, tex_h[6] = {0};
+  const char *cube_file = NULL;
+  int cube_size = 0;
   int temporal_frames = 5; /* index.js:258 default temporalFrames */
   for (int i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "--frag")) frag = argv[++i];
@@ -237,6 +293,16 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "--single")) single = 1;
     else if (!strcmp(argv[i], "--restir-out")) restir_out = 1;
     else if (!strcmp(argv[i], "--time")) time_ms = (float)atof(argv[++i]);
+    else if (!strcmp(argv[i], "--tex")) { /* --tex UNIT(1..5) W H file.rgba8 */
+      int u = atoi(argv[++i]);
+      if (u < 1 || u > 5) die("--tex unit must be 1..5 (u_tex0..3, u_rnd_tex)");
+      tex_w[u] = atoi(argv[++i]);
+      tex_h[u] = atoi(argv[++i]);
+      tex_file[u] = argv[++i];
+    } else if (!strcmp(argv[i], "--cube")) { /* --cube SIZE file.rgb8 */
+      cube_size = atoi(argv[++i]);
+      cube_file = argv[++i];
+    }
     else if (!strcmp(argv[i], "--cam")) {
       for (int k = 0; k < 9; k++) cam[k] = (float)atof(argv[++i]);
     } else die("unknown argument");
@@ -295,6 +361,11 @@ int main(int argc, char **argv) {
   GLuint h1 = mktex(w, h, zeros), h1a = mktex(w, h, zeros);
   GLuint h2 = mktex(w, h, zeros), h2a = mktex(w, h, zeros);
 
+  GLuint asset[6] = {0};
+  for (int u = 1; u <= 5; u++)
+    if (tex_file[u]) asset[u] = mktex8(tex_w[u], tex_h[u], tex_file[u]);
+  GLuint cube = cube_file ? mkcube(cube_size, cube_file) : 0;
+
   GLuint fb;
   p_glGenFramebuffers(1, &fb);
   p_glBindFramebuffer(GL_FRAMEBUFFER, fb);
@@ -327,6 +398,12 @@ int main(int argc, char **argv) {
     if (tf_loc >= 0) p_glUniform1i(tf_loc, temporal_frames);
     p_glActiveTexture(GL_TEXTURE0 + 0);
     p_glBindTexture(GL_TEXTURE_2D, single ? zero : back);
+    for (int u = 1; u <= 5; u++) {
+      p_glActiveTexture(GL_TEXTURE0 + u);
+      p_glBindTexture(GL_TEXTURE_2D, asset[u]);
+    }
+    p_glActiveTexture(GL_TEXTURE0 + 6);
+    p_glBindTexture(GL_TEXTURE_CUBE_MAP, cube);
     p_glActiveTexture(GL_TEXTURE0 + 7);  p_glBindTexture(GL_TEXTURE_2D, rbuf_back);
     p_glActiveTexture(GL_TEXTURE0 + 8);  p_glBindTexture(GL_TEXTURE_2D, raux_back);
     p_glActiveTexture(GL_TEXTURE0 + 9);  p_glBindTexture(GL_TEXTURE_2D, h1);

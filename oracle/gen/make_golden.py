@@ -79,6 +79,13 @@ def run_config(glrun, cfgs, cfg):
            "--single", "--out", prefix] + cam_args(cfg, cfgs)
     if restir:
         cmd.append("--restir-out")
+    # asset textures (u_tex0..3 = GL units 1..4, u_rnd_tex = unit 5; index.js:149-163)
+    sys.path.insert(0, os.path.dirname(HERE))
+    from textures import textures_for
+    for unit, img in textures_for(cfg).items():
+        fn = "%s_tex%d.rgba8" % (prefix, unit)
+        np.ascontiguousarray(img, np.uint8).tofile(fn)
+        cmd += ["--tex", str(unit + 1), str(img.shape[1]), str(img.shape[0]), fn]
     # volumetric shaders take SwiftShader hours (mostly JIT compile): RT0_GOLDEN_TIMEOUT
     sh(cmd, timeout=int(os.environ.get("RT0_GOLDEN_TIMEOUT", "1800")))
 

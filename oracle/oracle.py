@@ -39,6 +39,8 @@ def lib():
         L.or_hash.restype = ctypes.c_float
         L.or_hash.argtypes = [ctypes.c_float]
         L.or_hash2.argtypes = [ctypes.c_float, ctypes.c_float, fp]
+        L.or_set_texture.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_uint8)]
         L.or_pixel_seed.restype = ctypes.c_float
         L.or_pixel_seed.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_uint]
         _lib = L
@@ -79,6 +81,17 @@ class Oracle:
         L.or_set_camera(self.h, _fp(pos), _fp(look), _fp(par))
         L.or_set_resolution(self.h, width, height)
         self.restir = bool(cfg.get("defines", {}).get("USE_RESTIR"))
+        self._tex = {}
+        from textures import textures_for
+        for unit, img in textures_for(cfg).items():
+            self.set_texture(unit, img)
+
+    def set_texture(self, unit, rgba8):
+        """u_tex0..3 (unit 0..3) / u_rnd_tex (4): uint8 [h, w, 4], first row = t 0."""
+        a = np.ascontiguousarray(rgba8, np.uint8)
+        self._tex[unit] = a  # the C side keeps a pointer
+        self._chk(lib().or_set_texture(self.h, unit, a.shape[1], a.shape[0],
+                                       a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
 
     def _chk(self, rc):
         if rc != 0:

@@ -183,6 +183,9 @@ typedef struct {
   int ghost;
   /* camera uniforms (index.js:421-423) */
   v3 cam_pos, cam_look, cam_params;
+  /* asset textures (index.js:256-296): 0..3 u_tex0..3, 4 u_rnd_tex; RGBA8 */
+  const unsigned char *tex_img[5];
+  int tex_w[5], tex_h[5];
   char err[256];
 } Oracle;
 
@@ -204,6 +207,8 @@ typedef struct {
 typedef struct {
   v3 n, pos;
   int index;
+  v2 uv;      /* raytracer.glsl:102 */
+  float texel[4];
 } Hit;
 
 /* ------------------------------------------------------------- SDFs */
@@ -373,6 +378,118 @@ static int iSDF(Frag *F, v3 o, v3 d, float tmin, float *t, v3 *n, int *index) {
   return 1;
 }
 
+
+/* -------------------------------------------------------------- textures */
+/* GL texture() on an RGBA8 asset: GL_LINEAR, GL_REPEAT, level 0
+ * (GlslViewport.loadTexture, index.js:703-708); unbound = (0,0,0,1). */
+static void tex_fetch(const Oracle *o, int unit, float u, float v, float out[4]) {
+  const unsigned char *img = o->tex_img[unit];
+  if (!img) { out[0] = out[1] = out[2] = 0.0f; out[3] = 1.0f; return; }
+  int w = o->tex_w[unit], h = o->tex_h[unit];
+  float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+  float fx = floorf(x), fy = floorf(y);
+  float a = x - fx, b = y - fy;
+#ifdef OR_TEX_WEIGHT_BITS /* experiment: quantised sub-texel weights */
+  a = floorf(a * (float)(1 << OR_TEX_WEIGHT_BITS)) / (float)(1 << OR_TEX_WEIGHT_BITS);
+  b = floorf(b * (float)(1 << OR_TEX_WEIGHT_BITS)) / (float)(1 << OR_TEX_WEIGHT_BITS);
+#endif
+  int x0 = ((int)fx % w + w) % w, y0 = ((int)fy % h + h) % h;
+  int x1 = (x0 + 1) % w, y1 = (y0 + 1) % h;
+  for (int c = 0; c < 4; c++) {
+    float t00 = img[((size_t)y0 * w + x0) * 4 + c], t10 = img[((size_t)y0 * w + x1) * 4 + c];
+    float t01 = img[((size_t)y1 * w + x0) * 4 + c], t11 = img[((size_t)y1 * w + x1) * 4 + c];
+    float top = t00 + a * (t10 - t00), bot = t01 + a * (t11 - t01);
+    out[c] = (top + b * (bot - top)) / 255.0f;
+  }
+}
+static float glsl_mod(float x, float y) { return x - y * floorf(x / y); }
+/* raytracer.glsl:393-401 */
+static float value_noise(const Oracle *o, v3 x) {
+  v3 p = V(floorf(x.x), floorf(x.y), floorf(x.z));
+  v3 f = sub(x, p);
+  f = V(f.x * f.x * (3.0f - 2.0f * f.x), f.y * f.y * (3.0f - 2.0f * f.y), f.z * f.z * (3.0f - 2.0f * f.z));
+  float ux = (p.x + 37.0f * p.z) + f.x, uy = (p.y + 17.0f * p.z) + f.y;
+  float t[4];
+  tex_fetch(o, 4, (ux + 0.5f) / 256.0f, (uy + 0.5f) / 256.0f, t);
+  return mixf(t[1], t[0], f.z); /* .yx */
+}
+/* raytracer.glsl:404-431 */
+static v3 voronoi(const Oracle *o, v3 x) {
+  v3 p = V(floorf(x.x), floorf(x.y), floorf(x.z));
+  v3 f = sub(x, p);
+  float id = 0.0f, r0 = 100.0f, r1 = 100.0f;
+  for (int k = -1; k <= 1; ++k)
+    for (int j = -1; j <= 1; ++j)
+      for (int i = -1; i <= 1; ++i) {
+        v3 b = V((float)i, (float)j, (float)k);
+        v3 hx = add(p, b);
+        float t[4];
+        tex_fetch(o, 4, ((hx.x + 3.0f * hx.z) + 0.5f) / 256.0f, ((hx.y + 1.0f * hx.z) + 0.5f) / 256.0f, t);
+        v3 r = add(sub(b, f), V(t[0], t[1], t[2]));
+        float d = dot3(r, r);
+        if (d < r0) { id = dot3(add(p, b), V(1.0f, 57.0f, 113.0f)); r1 = r0; r0 = d; }
+        else if (d < r1) r1 = d;
+      }
+  return V(sqrtf(r0), sqrtf(r1), fabsf(id));
+}
+/* raytracer.glsl:363-387 */
+static v3 gradient_hash(v3 p) {
+  v3 q = V(dot3(p, V(127.1f, 311.7f, 74.7f)), dot3(p, V(269.5f, 183.3f, 246.1f)), dot3(p, V(113.5f, 271.9f, 124.6f)));
+  return V(-1.0f + 2.0f * fract(sinf(q.x) * 43758.5453f), -1.0f + 2.0f * fract(sinf(q.y) * 43758.5453f),
+           -1.0f + 2.0f * fract(sinf(q.z) * 43758.5453f));
+}
+static float gradient_noise(v3 p) {
+  v3 i = V(floorf(p.x), floorf(p.y), floorf(p.z));
+  v3 f = sub(p, i);
+  v3 u = V(f.x * f.x * (3.0f - 2.0f * f.x), f.y * f.y * (3.0f - 2.0f * f.y), f.z * f.z * (3.0f - 2.0f * f.z));
+  float c[8];
+  for (int k = 0; k < 8; k++) {
+    v3 of = V((float)(k & 1), (float)((k >> 1) & 1), (float)(k >> 2));
+    c[k] = dot3(gradient_hash(add(i, of)), sub(f, of));
+  }
+  return mixf(mixf(mixf(c[0], c[1], u.x), mixf(c[2], c[3], u.x), u.y),
+              mixf(mixf(c[4], c[5], u.x), mixf(c[6], c[7], u.x), u.y), u.z);
+}
+/* getTexel, raytracer.glsl:726-772 */
+static void getTexel(const Oracle *o, const Material *mat, const Hit *hit, float out[4]) {
+  int t = mat->tex_t;
+  const float *P = mat->tex_params;
+  if (t >= 0 && t <= 3) { tex_fetch(o, t, hit->uv.x, hit->uv.y, out); return; }
+  if (t == 7) {
+    float x = glsl_mod(floorf(P[0] * hit->uv.x) + floorf(P[1] * hit->uv.y), P[2]);
+    out[0] = out[1] = out[2] = out[3] = x;
+    return;
+  }
+  if (t == 8) {
+    float du = hit->uv.x - P[0], dv = hit->uv.y - P[1];
+    float x = glsl_mod(ceilf(sqrtf(du * du + dv * dv) * P[2]), P[3]);
+    out[0] = out[1] = out[2] = out[3] = x;
+    return;
+  }
+  v3 sp = mul(V(P[0], P[1], P[2]), hit->pos);
+  float x = 0.0f;
+  if (t == 4) {
+    v3 r = voronoi(o, sp);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = 0.0f;
+    return;
+  } else if (t == 5) {
+    float f = gradient_noise(sp);
+    float q = gclamp((f + 0.7f) / 1.4f, 0.0f, 1.0f);
+    x = q * q * (3.0f - 2.0f * q);
+  } else if (t == 6) {
+    x = value_noise(o, sp);
+  } else if (t == 9) {
+    v3 m = V(-1.2f, 1.99f, -1.6f), q = sp;
+    float f = 0.5f * value_noise(o, q);
+    q = muls(mul(m, q), 2.01f);
+    f += 0.25f * value_noise(o, q);
+    q = muls(mul(m, q), 2.02f);
+    f += 0.125f * value_noise(o, q);
+    x = f;
+  }
+  out[0] = out[1] = out[2] = out[3] = x;
+}
+
 /* intersection(), raytracer.glsl:997-1082 (texture/uv parsing omitted: every
  * supported material has NULL_TEX, so hit.uv / hit.texel never reach the output). */
 static float intersection(Frag *F, v3 o, v3 d, Hit *hit) {
@@ -381,6 +498,8 @@ static float intersection(Frag *F, v3 o, v3 d, Hit *hit) {
   hit->n = V(0, 0, 0);
   hit->pos = V(0, 0, 0);
   hit->index = 0;
+  hit->uv = (v2){-1.0f, -1.0f};
+  hit->texel[0] = hit->texel[1] = hit->texel[2] = hit->texel[3] = 0.0f;
   int type = -1;
   float tt = INF_T, tmin = INF_T;
   if (op->n_meshes > 0) {
@@ -401,8 +520,19 @@ static float intersection(Frag *F, v3 o, v3 d, Hit *hit) {
   }
   if (type + 1) {
     hit->pos = add(muls(d, tmin), o);
-    if (type == T_SPHERE) hit->n = normalize(sub(hit->pos, op->meshes[hit->index].pos));
-    else if (type == T_PLANE) hit->n = normalize(op->meshes[hit->index].pos);
+    if (type == T_SPHERE) {
+      /* cartesianToSpherical of the world position (467-471, 1057-1059) */
+      float rho = sqrtf(hit->pos.x * hit->pos.x + hit->pos.y * hit->pos.y + hit->pos.z * hit->pos.z);
+      hit->uv = (v2){asinf(hit->pos.y / rho) / PI_F, atan2f(hit->pos.z, hit->pos.x) / TWO_PI};
+      hit->n = normalize(sub(hit->pos, op->meshes[hit->index].pos));
+    } else if (type == T_PLANE) hit->n = normalize(op->meshes[hit->index].pos);
+    if (hit->uv.x < 0.0f) { /* 1069-1076 */
+      v3 nl = vabs(hit->n);
+      if (nl.x > nl.y && nl.x > nl.z) hit->uv = (v2){-hit->pos.z, -hit->pos.y};
+      else if (nl.y > nl.x && nl.y > nl.z) hit->uv = (v2){hit->pos.x, hit->pos.z};
+      else hit->uv = (v2){hit->pos.x, -hit->pos.y};
+    }
+    if (op->meshes[hit->index].mat.tex_t != TEX_NULL) getTexel(op, &op->meshes[hit->index].mat, hit, hit->texel);
   }
   return tmin;
 }
@@ -492,7 +622,7 @@ static v3 calcDirectLighting(Frag *F, const Mesh *light, v3 x, v3 nl, float seed
       if (mh->mat.t == M_LIGHT) {
         float weight = 2.0f * (1.0f - cos_a_max);
         float T_fog = o->use_vol ? expf(-VOL_SIGMA_T * t) : 1.0f;
-        v3 c = vmax3s(mh->mat.c, 0.001f);
+        v3 c = vmax3s(mix3(mh->mat.c, V(hit.texel[0], hit.texel[1], hit.texel[2]), hit.texel[3]), 0.001f);
         dl = add(dl, muls(muls(muls(mul(c, mh->mat.e), weight), gmax(0.001f, dot3(sr, nl))), T_fog));
       }
     } else if (light->t == T_SDF) {
@@ -501,7 +631,7 @@ static v3 calcDirectLighting(Frag *F, const Mesh *light, v3 x, v3 nl, float seed
       intersection(F, add(x, muls(nl, EPSILON)), sr, &hit);
       const Mesh *mh = &o->meshes[hit.index];
       if (mh->mat.t == M_LIGHT) {
-        v3 c = vmax3s(mh->mat.c, 0.001f);
+        v3 c = vmax3s(mix3(mh->mat.c, V(hit.texel[0], hit.texel[1], hit.texel[2]), hit.texel[3]), 0.001f);
         dl = add(dl, muls(mul(c, mh->mat.e), gmax(0.001f, dot3(sr, nl))));
       }
     }
@@ -1007,9 +1137,10 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
       break;
     }
     const Mesh *mesh = &o->meshes[hit.index];
-    v3 c = vmax3s(mesh->mat.c, 0.001f);
+    v3 trgb = V(hit.texel[0], hit.texel[1], hit.texel[2]);
+    v3 c = vmax3s(mix3(mesh->mat.c, mul(trgb, mesh->mat.tex_c_mask), (float)mesh->mat.opts[0] * hit.texel[3]), 0.001f);
     float inside = -gsign(dot3(rd, hit.n));
-    v3 e = vmax3s(mesh->mat.e, 0.001f);
+    v3 e = vmax3s(mix3(mesh->mat.e, mul(trgb, mesh->mat.tex_e_mask), (float)mesh->mat.opts[1] * hit.texel[3]), 0.001f);
     st_c = c; st_e = e; st_inside = inside;
     if (mesh->mat.t == M_LIGHT) {
       mask = mul(mask, c);
@@ -1104,6 +1235,20 @@ static int lookup_material(const char *name, Material *m) {
       m->nt = d->nt;
       m->t = d->t;
       m->tex_t = d->tex;
+      /* TEX_1 (135), TEX_CHECK (140), TEX_METAL (141); NULL_TEX (131) */
+      m->tex_c_mask = V(1, 1, 1);
+      m->tex_e_mask = V(1, 1, 1);
+      memset(m->tex_params, 0, sizeof m->tex_params);
+      if (d->tex == TX_1) m->tex_params[3] = 1.0f;
+      if (d->tex == TX_CHECK) {
+        m->tex_e_mask = V(0, 0, 0);
+        m->tex_params[0] = 5.0f; m->tex_params[1] = 5.0f; m->tex_params[2] = 2.0f;
+      }
+      if (d->tex == TX_METAL) {
+        m->tex_c_mask = V(0.7f, 0.25f, 0.055f);
+        m->tex_e_mask = V(0.6f, 0.2f, 0.6f);
+        m->tex_params[0] = 16.0f; m->tex_params[1] = 10.0f; m->tex_params[2] = 16.0f;
+      }
       m->opts[0] = d->o0;
       m->opts[1] = d->o1;
       m->opts[2] = m->opts[3] = 0;
@@ -1185,7 +1330,6 @@ int or_set_scene_lines(void *h, const char *text, const int *sdf_kinds, int n_ki
     Mesh *m = &tmp[n];
     memset(m, 0, sizeof *m);
     if (lookup_material(mat, &m->mat)) { snprintf(o->err, sizeof o->err, "unknown material %s", mat); return -1; }
-    if (m->mat.tex_t != TEX_NULL) { snprintf(o->err, sizeof o->err, "textured material %s not supported", mat); return -1; }
     if (strstr(mat, "MAT_LIGHT")) lights[nl++] = n;
     if (!strcmp(typ, "SPHERE")) m->t = T_SPHERE;
     else if (!strcmp(typ, "PLANE")) m->t = T_PLANE;
@@ -1263,6 +1407,16 @@ void or_set_camera(void *h, const float *pos, const float *look, const float *pa
   o->cam_pos = V(pos[0], pos[1], pos[2]);
   o->cam_look = V(look[0], look[1], look[2]);
   o->cam_params = V(params[0], params[1], params[2]);
+}
+/* loadTexture (index.js:699-728): unit 0..3 = u_tex0..3, 4 = u_rnd_tex; the
+ * caller keeps the RGBA8 buffer alive while rendering (NULL = unbound). */
+int or_set_texture(void *h, int unit, int w, int hh, const unsigned char *rgba8) {
+  Oracle *o = (Oracle *)h;
+  if (unit < 0 || unit > 4) return -1;
+  o->tex_img[unit] = rgba8;
+  o->tex_w[unit] = w;
+  o->tex_h[unit] = hh;
+  return 0;
 }
 void or_set_resolution(void *h, int w, int hh) { ((Oracle *)h)->w = w; ((Oracle *)h)->h = hh; }
 

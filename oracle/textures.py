@@ -1,0 +1,70 @@
+"""Deterministic synthetic asset textures for the texture fixtures.
+
+TEST INFRASTRUCTURE ONLY (imported by oracle/gen/make_golden.py and tests/).
+The reference samples four image textures (textures/tex0-3.png, index.html:262)
+and an RGBA noise image (textures/rgba_noise/rgba_noise256.png, index.js:258-273).
+Those assets are not shipped; the fixtures use stand-ins of the same kind,
+generated here by integer hashing only (bit-identical on every machine and
+numpy version), so that the SwiftShader run of the reference shader, the C
+restatement and the GPU see the same texels:
+
+* noise256: 256x256 RGBA8; R, B, A are hash noise and G is R shifted by
+  (37, 17) texels -- G(x, y) = R(x - 37, y - 17) -- the layout value_noise()
+  relies on (raytracer.glsl:397-399 reads .yx at uv + (37, 17)*z), so the
+  noise is continuous across integer z like with the reference asset.
+* image(w, h, seed): RGBA8 with smooth colour gradients, a hash-noise term and
+  an alpha channel that varies over the image (MAT_LIGHT_4_TEX / MAT_TEST mix
+  by texel.a, raytracer.glsl:1203, 2071).
+"""
+import numpy as np
+
+
+def _hash32(x):
+    """lowbias32 integer hash, uint32 -> uint32 (numpy, wrap-around)."""
+    x = np.asarray(x, np.uint32).copy()
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def _noise_plane(w, h, salt):
+    y, x = np.mgrid[0:h, 0:w].astype(np.uint32)
+    return (_hash32(x + np.uint32(w) * y + np.uint32((salt * 0x9E3779B9) & 0xFFFFFFFF)) >> np.uint32(24)).astype(np.uint8)
+
+
+def noise256():
+    n = 256
+    r = _noise_plane(n, n, 1)
+    g = np.roll(np.roll(r, 17, axis=0), 37, axis=1)  # g[y, x] = r[y - 17, x - 37]
+    b = _noise_plane(n, n, 2)
+    a = _noise_plane(n, n, 3)
+    return np.stack([r, g, b, a], axis=-1)
+
+
+def image(w, h, seed):
+    y, x = np.mgrid[0:h, 0:w].astype(np.int64)
+    nz = _noise_plane(w, h, 100 + seed).astype(np.int64)
+    r = (x * 255) // max(1, w - 1)
+    g = (y * 255) // max(1, h - 1)
+    b = ((x + y + 64 * seed) * 3) % 256
+    a = 64 + ((x * 7 + y * 3 + 17 * seed) % 192)
+    px = np.stack([(r * 3 + nz) // 4, (g * 3 + nz) // 4, (b * 3 + nz) // 4, a], axis=-1)
+    return px.astype(np.uint8)
+
+
+def textures_for(cfg):
+    """{unit: uint8 [h, w, 4]} for a configs.json entry's "textures" list
+    ("noise" -> unit 4 = u_rnd_tex; "imageN" -> unit N = u_texN)."""
+    out = {}
+    for name in cfg.get("textures", []):
+        if name == "noise":
+            out[4] = noise256()
+        elif name.startswith("image"):
+            k = int(name[5:])
+            out[k] = image(64 + 32 * k, 64 + 16 * k, k)
+        else:
+            raise KeyError(name)
+    return out

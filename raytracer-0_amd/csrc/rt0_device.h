@@ -37,10 +37,25 @@ struct MatRec {
   float nt;
 };
 
+// Material texture, raytracer.glsl:124-128 (`Texture`) + Material.opts (161),
+// 48 B.  type -1 = NULL_TEX; opts bit 0 = colour texture, bit 1 = emission.
+struct TexRec {
+  float cmr, cmg, cmb;
+  int32_t type;
+  float emr, emg, emb;
+  uint32_t opts;
+  float p0, p1, p2, p3;
+};
+
+// Asset texture units (index.js:149-163): 0..3 = u_tex0..3, 4 = u_rnd_tex.
+#define RT0_TEX_UNITS 5
+
 struct SceneDev {
   int32_t n_meshes, n_sdfs, n_lights, n_total;
+  int32_t any_tex;  // some mesh has tex.type != NULL (texel code runs at all)
   GeomRec geom[RT0_MAX_MESH];
   MatRec mat[RT0_MAX_MESH];
+  TexRec tex[RT0_MAX_MESH];
   float j3[RT0_MAX_MESH];  // joker.w (udRoundBox radius)
   int32_t sdf_kind[RT0_MAX_MESH];
   int32_t light_index[RT0_MAX_LIGHTS];
@@ -89,4 +104,8 @@ struct LaunchParams {
   // null: one chunk, accumulated in registers.
   int32_t frame_chunk;
   float4 *samples;
+  // Asset textures: RGBA8 texels (R in the low byte), row 0 = t 0; null =
+  // unbound unit.
+  const uint32_t *tex_img[RT0_TEX_UNITS];
+  int32_t tex_w[RT0_TEX_UNITS], tex_h[RT0_TEX_UNITS];
 };

@@ -63,6 +63,8 @@ struct rt0_ctx {
   float4 *d_samples = nullptr;   // per-frame samples of frame-chunked launches
   size_t samples_bytes = 0;
   int max_frames_per_launch = 64;
+  uint32_t *d_tex[RT0_TEX_UNITS] = {};  // asset textures (rt0_set_texture)
+  int tex_w[RT0_TEX_UNITS] = {}, tex_h[RT0_TEX_UNITS] = {};
   SceneDev host_scene;   // what d_scene holds (also the JIT's scene data)
   bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
   std::string jit_err;
@@ -151,6 +153,8 @@ void rt0_destroy(rt0_ctx *c) {
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_halo_miss) (void)hipFree(c->d_halo_miss);
   if (c->d_samples) (void)hipFree(c->d_samples);
+  for (auto &t : c->d_tex)
+    if (t) (void)hipFree(t);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -209,6 +213,20 @@ static int upload_scene(rt0_ctx *c) {
     r.eb = m.e[2];
     r.nt = m.nt;
     r.type = m.mat_type;
+    TexRec &t = s.tex[i];
+    t.type = m.tex_type;
+    t.cmr = m.tex_c_mask[0];
+    t.cmg = m.tex_c_mask[1];
+    t.cmb = m.tex_c_mask[2];
+    t.emr = m.tex_e_mask[0];
+    t.emg = m.tex_e_mask[1];
+    t.emb = m.tex_e_mask[2];
+    t.opts = m.mat_opts;
+    t.p0 = m.tex_params[0];
+    t.p1 = m.tex_params[1];
+    t.p2 = m.tex_params[2];
+    t.p3 = m.tex_params[3];
+    if (m.tex_type != -1) s.any_tex = 1;
   }
   for (int i = 0; i < s.n_lights; i++) s.light_index[i] = c->lights[i];
   HIPCHK(c, hipSetDevice(c->device));
@@ -225,7 +243,7 @@ static int validate_and_store(rt0_ctx *c, const rt0_mesh *m, int ne, int ns, con
   if (nl > RT0_MAX_LIGHTS) return fail(c, RT0_E_UNSUPPORTED, "too many lights");
   if (ne + ns == 0) return fail(c, RT0_E_ARG, "empty scene");  // meshes[hit.index] needs meshes[0]
   for (int i = 0; i < ne + ns; i++) {
-    if (m[i].tex_type != -1) return fail(c, RT0_E_UNSUPPORTED, "textured materials are not supported yet");
+    if (m[i].tex_type < -1 || m[i].tex_type > 9) return fail(c, RT0_E_ARG, "bad texture type");
     bool sdf = m[i].type == 3;
     if ((i < ne) == sdf) return fail(c, RT0_E_ARG, "meshes[0..n_meshes) must be Euclidean, the rest SDF");
     if (!sdf && (m[i].type < 0 || m[i].type > 2)) return fail(c, RT0_E_UNSUPPORTED, "unsupported mesh type");
@@ -288,6 +306,25 @@ int rt0_get_scene(const rt0_ctx *c, rt0_mesh *meshes, int max_meshes, int *n_mes
     for (int i = 0; i < n && i < max_meshes; i++) meshes[i] = c->meshes[i];
   if (light_index)
     for (int i = 0; i < (int)c->lights.size() && i < max_lights; i++) light_index[i] = c->lights[i];
+  return RT0_OK;
+}
+
+int rt0_set_texture(rt0_ctx *c, int unit, int w, int h, const uint8_t *rgba8) {
+  if (!c || unit < 0 || unit >= RT0_TEX_UNITS) return RT0_E_ARG;
+  if (rgba8 && (w <= 0 || h <= 0 || (long long)w * h > (1ll << 28)))
+    return fail(c, RT0_E_ARG, "texture size out of range");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // a running pass may read the old texels
+  if (c->d_tex[unit]) HIPCHK(c, hipFree(c->d_tex[unit]));
+  c->d_tex[unit] = nullptr;
+  c->tex_w[unit] = c->tex_h[unit] = 0;
+  if (!rgba8) return RT0_OK;
+  const size_t n = (size_t)w * h * 4;
+  HIPCHK(c, hipMalloc(&c->d_tex[unit], n));
+  HIPCHK(c, hipMemcpyAsync(c->d_tex[unit], rgba8, n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->tex_w[unit] = w;
+  c->tex_h[unit] = h;
   return RT0_OK;
 }
 
@@ -365,6 +402,11 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   int owned = total_bands / c->n_shards + (c->shard < total_bands % c->n_shards ? 1 : 0);
   p.n_band_rows = owned * c->band;
   p.scene = c->d_scene;
+  for (int u = 0; u < RT0_TEX_UNITS; u++) {
+    p.tex_img[u] = c->d_tex[u];
+    p.tex_w[u] = c->tex_w[u];
+    p.tex_h[u] = c->tex_h[u];
+  }
   p.accum = c->acc();
   p.counters = c->d_counters;
   if (c->n_shards > 1) {  // one contiguous block per shard (checked for ReSTIR in render_impl)

@@ -148,6 +148,8 @@ struct DynScene {
   DEV float j3(int i) const { return S->j3[i]; }
   DEV int sdf_kind(int i) const { return S->sdf_kind[i]; }
   DEV int light(int i) const { return S->light_index[i]; }
+  DEV bool any_tex() const { return S->any_tex != 0; }
+  DEV TexRec tex(int i) const { return S->tex[i]; }
 };
 
 // DynCfg: defines/constants as wave-uniform kernel arguments.  A JIT config
@@ -202,6 +204,7 @@ DEV void for_sdfs(const Scene &sc, F &&f) {
 struct Hit {
   v3 n, pos;
   int index;
+  int type;  // -1 miss, else T_* (the uv/texel parser's dispatch, raytracer.glsl:1049-1078)
 };
 
 // SDF primitives, raytracer.glsl:496-528, 642-698
@@ -406,6 +409,7 @@ struct Geometry {
         }
       }
     }
+    hit.type = type;
     if (type >= 0) {
       hit.pos = d * tmin + o;
       if (type == T_SPHERE) {
@@ -537,6 +541,153 @@ DEV v3 wavelength_to_rgb(float l) {
   return mk(fmaxf(0.0f, rgb.x) / 0.378f, fmaxf(0.0f, rgb.y) / 0.298f, fmaxf(0.0f, rgb.z) / 0.285f);
 }
 
+
+// --------------------------------------------------------------- textures
+// raytracer.glsl:363-433 (noise), 726-772 (getTexel), 1049-1078 (uv parser).
+// The texel is evaluated lazily -- only where the reference reads
+// hit.texel (shading 2071/2077, light hits in calcDirectLighting 1203/1215) --
+// which is the same value: it depends only on the hit's mesh, position,
+// normal and uv.
+struct T4 {
+  float r, g, b, a;
+};
+DEV T4 t4s(float x) { return T4{x, x, x, x}; }
+// GLSL mod(x, y) = x - y*floor(x/y) (correctly rounded division)
+DEV float glsl_mod(float x, float y) { return x - y * floorf(x / y); }
+DEV float smoothstep_(float e0, float e1, float x) {
+  float t = fminf(fmaxf((x - e0) / (e1 - e0), 0.0f), 1.0f);
+  return t * t * (3.0f - 2.0f * t);
+}
+// GL_LINEAR + GL_REPEAT fetch at level 0 of an RGBA8 asset texture
+// (GlslViewport.loadTexture, index.js:703-708); unbound unit = (0,0,0,1).
+DEV T4 tex_rgba8(const LaunchParams &P, int unit, float u, float v) {
+  const uint32_t *__restrict__ img = P.tex_img[unit];
+  if (img == nullptr) return T4{0.f, 0.f, 0.f, 1.f};
+  const int w = P.tex_w[unit], h = P.tex_h[unit];
+  const float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+  const float fx = floorf(x), fy = floorf(y);
+  const float a = x - fx, b = y - fy;
+  int x0 = (int)fx % w, y0 = (int)fy % h;
+  x0 += x0 < 0 ? w : 0;
+  y0 += y0 < 0 ? h : 0;
+  const int x1 = x0 + 1 == w ? 0 : x0 + 1, y1 = y0 + 1 == h ? 0 : y0 + 1;
+  const uint32_t q00 = img[y0 * w + x0], q10 = img[y0 * w + x1], q01 = img[y1 * w + x0], q11 = img[y1 * w + x1];
+  float r[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float t00 = (float)((q00 >> (8 * c)) & 255u), t10 = (float)((q10 >> (8 * c)) & 255u);
+    const float t01 = (float)((q01 >> (8 * c)) & 255u), t11 = (float)((q11 >> (8 * c)) & 255u);
+    const float top = t00 + a * (t10 - t00), bot = t01 + a * (t11 - t01);
+    r[c] = (top + b * (bot - top)) / 255.0f;  // unorm8, correctly rounded like the restatement
+  }
+  return T4{r[0], r[1], r[2], r[3]};
+}
+// value_noise, 393-401 (the .yx swizzle: mix(G, R, f.z))
+DEV float value_noise(const LaunchParams &P, v3 x) {
+  const v3 p = mk(floorf(x.x), floorf(x.y), floorf(x.z));
+  v3 f = x - p;
+  f = mk(f.x * f.x * (3.0f - 2.0f * f.x), f.y * f.y * (3.0f - 2.0f * f.y), f.z * f.z * (3.0f - 2.0f * f.z));
+  const float ux = (p.x + 37.0f * p.z) + f.x, uy = (p.y + 17.0f * p.z) + f.y;
+  const T4 t = tex_rgba8(P, 4, (ux + 0.5f) * (1.0f / 256.0f), (uy + 0.5f) * (1.0f / 256.0f));
+  return mixf(t.g, t.r, f.z);
+}
+// voronoi, 404-431
+DEV v3 voronoi(const LaunchParams &P, v3 x) {
+  const v3 p = mk(floorf(x.x), floorf(x.y), floorf(x.z));
+  const v3 f = x - p;
+  float id = 0.0f, r0 = 100.0f, r1 = 100.0f;
+  for (int k = -1; k <= 1; ++k)
+    for (int j = -1; j <= 1; ++j)
+      for (int i = -1; i <= 1; ++i) {
+        const v3 b = mk((float)i, (float)j, (float)k);
+        const v3 hx = p + b;
+        const T4 t = tex_rgba8(P, 4, ((hx.x + 3.0f * hx.z) + 0.5f) * (1.0f / 256.0f),
+                               ((hx.y + 1.0f * hx.z) + 0.5f) * (1.0f / 256.0f));
+        const v3 r = (b - f) + mk(t.r, t.g, t.b);
+        const float d = dot(r, r);
+        if (d < r0) {
+          id = dot(p + b, mk(1.0f, 57.0f, 113.0f));
+          r1 = r0;
+          r0 = d;
+        } else if (d < r1) {
+          r1 = d;
+        }
+      }
+  return mk(sqrtf(r0), sqrtf(r1), fabsf(id));
+}
+// gradient_hash / gradient_noise, 363-387 (sin of large arguments times
+// 43758.5: executor-dependent in the last bits; no reference material uses it)
+DEV v3 gradient_hash(v3 p) {
+  const v3 q = mk(dot(p, mk(127.1f, 311.7f, 74.7f)), dot(p, mk(269.5f, 183.3f, 246.1f)),
+                  dot(p, mk(113.5f, 271.9f, 124.6f)));
+  const float sx = sinf(q.x) * 43758.5453f, sy = sinf(q.y) * 43758.5453f, sz = sinf(q.z) * 43758.5453f;
+  return mk(-1.0f + 2.0f * (sx - floorf(sx)), -1.0f + 2.0f * (sy - floorf(sy)), -1.0f + 2.0f * (sz - floorf(sz)));
+}
+DEV float gradient_noise(v3 p) {
+  const v3 i = mk(floorf(p.x), floorf(p.y), floorf(p.z));
+  const v3 f = p - i;
+  const v3 u = mk(f.x * f.x * (3.0f - 2.0f * f.x), f.y * f.y * (3.0f - 2.0f * f.y), f.z * f.z * (3.0f - 2.0f * f.z));
+  float c[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const v3 o = mk((float)(k & 1), (float)((k >> 1) & 1), (float)(k >> 2));
+    c[k] = dot(gradient_hash(i + o), f - o);
+  }
+  const float x00 = mixf(c[0], c[1], u.x), x10 = mixf(c[2], c[3], u.x);
+  const float x01 = mixf(c[4], c[5], u.x), x11 = mixf(c[6], c[7], u.x);
+  return mixf(mixf(x00, x10, u.y), mixf(x01, x11, u.y), u.z);
+}
+// getTexel, 726-772
+DEV T4 get_texel(const LaunchParams &P, const TexRec &t, v3 pos, float u, float v) {
+  if (t.type >= 0 && t.type <= 3) return tex_rgba8(P, t.type, u, v);
+  if (t.type == 7) return t4s(glsl_mod(floorf(t.p0 * u) + floorf(t.p1 * v), t.p2));  // CHECK
+  if (t.type == 8) {                                                                 // RIPPLE
+    const float du = u - t.p0, dv = v - t.p1;
+    return t4s(glsl_mod(ceilf(sqrtf(du * du + dv * dv) * t.p2), t.p3));
+  }
+  const v3 sp = mk(t.p0, t.p1, t.p2) * pos;
+  if (t.type == 4) {  // VORONOI
+    const v3 r = voronoi(P, sp);
+    return T4{r.x, r.y, r.z, 0.0f};
+  }
+  if (t.type == 5) return t4s(smoothstep_(-0.7f, 0.7f, gradient_noise(sp)));  // GRADIENT_NOISE
+  if (t.type == 6) return t4s(value_noise(P, sp));                             // VALUE_NOISE
+  if (t.type == 9) {                                                           // METAL
+    const v3 m = mk(-1.2f, 1.99f, -1.6f);
+    v3 q = sp;
+    float f = 0.5f * value_noise(P, q);
+    q = (m * q) * 2.01f;
+    f += 0.25f * value_noise(P, q);
+    q = (m * q) * 2.02f;
+    f += 0.125f * value_noise(P, q);
+    return t4s(f);
+  }
+  return t4s(0.0f);
+}
+// hit.uv (1051-1076) + getTexel for a hit on a textured mesh (type >= 0)
+DEV T4 hit_texel(const LaunchParams &P, const TexRec &t, const Hit &h) {
+  float u = -1.0f, v = -1.0f;
+  if (h.type == T_SPHERE) {  // cartesianToSpherical of the WORLD position (467-471)
+    const float rho = sqrtf(dot(h.pos, h.pos));
+    u = asinf(h.pos.y / rho) / PI_F;
+    v = atan2f(h.pos.z, h.pos.x) / TWO_PI;
+  }
+  if (u < 0.0f) {
+    const v3 a = vabs(h.n);
+    if (a.x > a.y && a.x > a.z) {
+      u = -h.pos.z;
+      v = -h.pos.y;
+    } else if (a.y > a.x && a.y > a.z) {
+      u = h.pos.x;
+      v = h.pos.z;
+    } else {
+      u = h.pos.x;
+      v = -h.pos.y;
+    }
+  }
+  return get_texel(P, t, h.pos, u, v);
+}
+
 // ---------------------------------------------------------------- ReSTIR
 // raytracer.glsl:1264-1802.
 struct Res {
@@ -593,6 +744,20 @@ struct Integrator {
     return G::template intersect<SDF>(sc, C, o, d, h, n_map);
   }
 
+  // mix(mesh.mat.c, hit.texel.rgb, hit.texel.a) of a shadow ray's light hit
+  // (raytracer.glsl:1203, 1215); hit.texel is HIT_MISS's zero on a miss
+  DEV v3 light_color(const Hit &h, const MatRec &m) {
+    v3 c = mk(m.cr, m.cg, m.cb);
+    if (sc.any_tex() && h.type >= 0) {
+      const TexRec tr = sc.tex(h.index);
+      if (tr.type >= 0) {
+        const T4 tx = hit_texel(P, tr, h);
+        c = mk(mixf(c.x, tx.r, tx.a), mixf(c.y, tx.g, tx.a), mixf(c.z, tx.b, tx.a));
+      }
+    }
+    return c;
+  }
+
   // calcDirectLighting, raytracer.glsl:1174-1230
   DEV v3 direct_light(int li, v3 x, v3 nl, float seed) {
     if (COUNT) ++n_nee;
@@ -617,7 +782,7 @@ struct Integrator {
           float weight = 2.0f * (1.0f - cos_a_max);
           float T_fog = 1.0f;
           if (VOL && flag(F_VOL)) T_fog = fexp(-VOL_SIGMA_T * t);
-          v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
+          v3 c = vmaxs(light_color(hit, mh), 0.001f);
           dl = (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
         }
       } else if (SDF && g.type == T_SDF) {
@@ -626,7 +791,7 @@ struct Integrator {
         isect(x + nl * EPSILON, sr, hit);
         const MatRec mh = sc.mat(hit.index);
         if (mh.type == M_LIGHT) {
-          v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
+          v3 c = vmaxs(light_color(hit, mh), 0.001f);
           dl = (c * mk(mh.er, mh.eg, mh.eb)) * fmaxf(0.001f, dot(sr, nl));
         }
       }
@@ -989,9 +1154,24 @@ struct Integrator {
       }
       const GeomRec g = sc.geom(hit.index);
       const MatRec mt = sc.mat(hit.index);
-      v3 c = vmaxs(mk(mt.cr, mt.cg, mt.cb), 0.001f);
+      v3 c = mk(mt.cr, mt.cg, mt.cb), e = mk(mt.er, mt.eg, mt.eb);
+      if (sc.any_tex()) {  // raytracer.glsl:2071, 2077
+        const TexRec tr = sc.tex(hit.index);
+        if (tr.type >= 0 && (tr.opts & 3u)) {
+          const T4 tx = hit_texel(P, tr, hit);
+          if (tr.opts & 1u) {
+            const float a = tx.a;
+            c = mk(mixf(c.x, tx.r * tr.cmr, a), mixf(c.y, tx.g * tr.cmg, a), mixf(c.z, tx.b * tr.cmb, a));
+          }
+          if (tr.opts & 2u) {
+            const float a = tx.a;
+            e = mk(mixf(e.x, tx.r * tr.emr, a), mixf(e.y, tx.g * tr.emg, a), mixf(e.z, tx.b * tr.emb, a));
+          }
+        }
+      }
+      c = vmaxs(c, 0.001f);
       float inside = -sgn(dot(rd, hit.n));
-      v3 e = vmaxs(mk(mt.er, mt.eg, mt.eb), 0.001f);
+      e = vmaxs(e, 0.001f);
       if (mt.type == M_LIGHT) {
         mask = mask * c;
         float w = 1.0f;

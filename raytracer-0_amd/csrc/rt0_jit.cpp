@@ -75,6 +75,13 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "{" << fl(m.cr) << "," << fl(m.cg) << "," << fl(m.cb) << "," << m.type << "," << fl(m.er) << "," << fl(m.eg)
       << "," << fl(m.eb) << "," << fl(m.nt) << "},";
   }
+  o << "};\n__constant__ const TexRec kJitTex[" << (nt > 0 ? nt : 1) << "] = {";
+  for (int i = 0; i < nt; i++) {
+    const TexRec &t = s.tex[i];
+    o << "{" << fl(t.cmr) << "," << fl(t.cmg) << "," << fl(t.cmb) << "," << t.type << "," << fl(t.emr) << ","
+      << fl(t.emg) << "," << fl(t.emb) << "," << t.opts << "u," << fl(t.p0) << "," << fl(t.p1) << "," << fl(t.p2)
+      << "," << fl(t.p3) << "},";
+  }
   o << "};\n__constant__ const float kJitJ3[" << (nt > 0 ? nt : 1) << "] = {";
   for (int i = 0; i < nt; i++) o << fl(s.j3[i]) << ",";
   o << "};\n__constant__ const int kJitSdfKind[" << (nt > 0 ? nt : 1) << "] = {";
@@ -96,6 +103,9 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
        "  __device__ static float j3(int i) { return kJitJ3[i]; }\n"
        "  __device__ static int sdf_kind(int i) { return kJitSdfKind[i]; }\n"
        "  __device__ static int light(int i) { return kJitLights[i]; }\n"
+       "  __device__ static TexRec tex(int i) { return kJitTex[i]; }\n"
+       "  __device__ static constexpr bool any_tex() { return "
+    << (s.any_tex ? "true" : "false") << "; }\n"
        "};\n";
   o << "struct JitCfg {\n"
        "  __device__ static constexpr uint32_t flags() { return "

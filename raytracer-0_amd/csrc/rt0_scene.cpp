@@ -18,47 +18,66 @@
 
 namespace rt0h {
 
-// Material table, raytracer.glsl:165-224 (texture ids: 112-141).
+// Texture table, raytracer.glsl:112-141: the textures the material table
+// references, keyed by their type (each type has one definition there).
+struct TexDef {
+  int type;
+  float cm[3], em[3], params[4];
+};
+static const TexDef kTextures[] = {
+    {-1, {1, 1, 1}, {1, 1, 1}, {0, 0, 0, 0}},        // NULL_TEX (131)
+    {0, {1, 1, 1}, {1, 1, 1}, {0, 0, 0, 1}},         // TEX_0 (134)
+    {1, {1, 1, 1}, {1, 1, 1}, {0, 0, 0, 1}},         // TEX_1
+    {2, {1, 1, 1}, {1, 1, 1}, {0, 0, 0, 1}},         // TEX_2
+    {3, {1, 1, 1}, {1, 1, 1}, {0, 0, 0, 1}},         // TEX_3
+    {6, {1, 1, 1}, {1, 1, 1}, {16, 16, 16, 16}},     // TEX_VALUE_NOISE (139)
+    {7, {1, 1, 1}, {0, 0, 0}, {5, 5, 2, 0}},         // TEX_CHECK (140)
+    {9, {0.7f, 0.25f, 0.055f}, {0.6f, 0.2f, 0.6f}, {16, 10, 16, 0}},  // TEX_METAL (141)
+};
+
+// Material table, raytracer.glsl:165-224; opts = Material.opts bits (1 colour
+// texture, 2 emission texture).
 struct MatDef {
   const char *name;
   float c[3], e[3], nt;
   int type, tex;
+  unsigned opts;
 };
 static const float IOR_GLASS = 1.53f, IOR_SAPPHIRE = 1.77f, IOR_WATER = 1.33f, IOR_COAT = 1.4f;
 static const MatDef kMaterials[] = {
-    {"NULL_MAT", {0, 0, 0}, {0, 0, 0}, 0.f, -1, -1},
-    {"MAT_REFR_CLEAR", {1.f, 0.5f, 0.f}, {0, 0, 0}, IOR_GLASS, 4, -1},
-    {"MAT_REFR_CLEAR_2", {1, 1, 1}, {0, 0, 0}, IOR_GLASS, 5, -1},
-    {"MAT_REFR_SAPPHIRE", {1, 1, 1}, {0, 0, 0}, IOR_SAPPHIRE, 4, -1},
-    {"MAT_REFR_WATER", {0.25f, 0.64f, 0.88f}, {0, 0, 0}, IOR_WATER, 4, -1},
-    {"MAT_REFR_TEST", {1, 1, 1}, {0, 0, 0}, IOR_GLASS, 4, 1},
-    {"MAT_LIGHT_4", {1, 1, 1}, {4, 4, 4}, 0.f, 0, -1},
-    {"MAT_LIGHT_CANDLE_4", {1.0f, 0.57647058823f, 0.16078431372f}, {4, 4, 4}, 0.f, 0, -1},
-    {"MAT_LIGHT_HALOGEN_4", {1.0f, 0.94509803921f, 0.87843137254f}, {4, 4, 4}, 0.f, 0, -1},
-    {"MAT_LIGHT_DEMO", {1, 1, 1}, {10, 10, 10}, 0.f, 0, -1},
-    {"MAT_LIGHT_4_TEX", {1, 1, 1}, {1, 1, 1}, 0.f, 0, 1},
-    {"MAT_CLEAR_SKY", {0.25098039215f, 0.61176470588f, 1.0f}, {1, 1, 1}, 0.f, 1, -1},
-    {"MAT_OVERCAST_SKY", {0.78823529411f, 0.8862745098f, 1.0f}, {1, 1, 1}, 0.f, 1, -1},
-    {"MAT_DIRECT_SUNLIGHT", {1, 1, 1}, {1, 1, 1}, 0.f, 1, -1},
-    {"MAT_MIRROR", {1, 1, 1}, {0, 0, 0}, 0.f, 3, -1},
-    {"MAT_METAL", {0.6f, 0.6f, 0.6f}, {0, 0, 0}, 0.f, 3, 9},
-    {"MAT_BLACK", {0, 0, 0}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_WHITE", {1, 1, 1}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_RED", {1, 0, 0}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_GREEN", {0, 1, 0}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_BLUE", {0, 0, 1}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_CORNELL_WHITE", {1, 1, 1}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_CORNELL_RED", {0.7f, 0.12f, 0.05f}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_CORNELL_GREEN", {0.2f, 0.4f, 0.36f}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_YELLOW", {1, 1, 0}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_PURPLE", {0.50196078431f, 0, 0.50196078431f}, {0, 0, 0}, 0.f, 2, -1},
-    {"MAT_CHECK_WHITE", {0, 0, 0}, {0, 0, 0}, 0.f, 2, 7},
-    {"MAT_COAT_NAVY", {0, 0, 0.50196078431f}, {1, 1, 1}, IOR_COAT, 6, -1},
-    {"MAT_COAT_PURPLE", {0.50196078431f, 0, 0.50196078431f}, {0, 0, 0}, IOR_COAT, 6, -1},
-    {"MAT_COAT_WAX", {0.9333f, 0.6666f, 0.6f}, {0.005f, 0.005f, 0.005f}, IOR_COAT, 6, -1},
-    {"MAT_TEST", {1, 1, 1}, {0, 0, 0}, 0.f, 2, 1},
-    {"MAT_SPECTRAL_FLINT", {1, 1, 1}, {0, 0, 0}, -1.7167f, 4, -1},
-    {"MAT_SPECTRAL_DIAMOND", {1, 1, 1}, {0, 0, 0}, -2.3991f, 4, -1},
+    {"NULL_MAT", {0, 0, 0}, {0, 0, 0}, 0.f, -1, -1, 0u},
+    {"MAT_REFR_CLEAR", {1.f, 0.5f, 0.f}, {0, 0, 0}, IOR_GLASS, 4, -1, 0u},
+    {"MAT_REFR_CLEAR_2", {1, 1, 1}, {0, 0, 0}, IOR_GLASS, 5, -1, 0u},
+    {"MAT_REFR_SAPPHIRE", {1, 1, 1}, {0, 0, 0}, IOR_SAPPHIRE, 4, -1, 0u},
+    {"MAT_REFR_WATER", {0.25f, 0.64f, 0.88f}, {0, 0, 0}, IOR_WATER, 4, -1, 0u},
+    {"MAT_REFR_TEST", {1, 1, 1}, {0, 0, 0}, IOR_GLASS, 4, 1, 1u},
+    {"MAT_LIGHT_4", {1, 1, 1}, {4, 4, 4}, 0.f, 0, -1, 0u},
+    {"MAT_LIGHT_CANDLE_4", {1.0f, 0.57647058823f, 0.16078431372f}, {4, 4, 4}, 0.f, 0, -1, 0u},
+    {"MAT_LIGHT_HALOGEN_4", {1.0f, 0.94509803921f, 0.87843137254f}, {4, 4, 4}, 0.f, 0, -1, 0u},
+    {"MAT_LIGHT_DEMO", {1, 1, 1}, {10, 10, 10}, 0.f, 0, -1, 0u},
+    {"MAT_LIGHT_4_TEX", {1, 1, 1}, {1, 1, 1}, 0.f, 0, 1, 1u},
+    {"MAT_CLEAR_SKY", {0.25098039215f, 0.61176470588f, 1.0f}, {1, 1, 1}, 0.f, 1, -1, 0u},
+    {"MAT_OVERCAST_SKY", {0.78823529411f, 0.8862745098f, 1.0f}, {1, 1, 1}, 0.f, 1, -1, 0u},
+    {"MAT_DIRECT_SUNLIGHT", {1, 1, 1}, {1, 1, 1}, 0.f, 1, -1, 0u},
+    {"MAT_MIRROR", {1, 1, 1}, {0, 0, 0}, 0.f, 3, -1, 0u},
+    {"MAT_METAL", {0.6f, 0.6f, 0.6f}, {0, 0, 0}, 0.f, 3, 9, 2u},
+    {"MAT_BLACK", {0, 0, 0}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_WHITE", {1, 1, 1}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_RED", {1, 0, 0}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_GREEN", {0, 1, 0}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_BLUE", {0, 0, 1}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_CORNELL_WHITE", {1, 1, 1}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_CORNELL_RED", {0.7f, 0.12f, 0.05f}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_CORNELL_GREEN", {0.2f, 0.4f, 0.36f}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_YELLOW", {1, 1, 0}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_PURPLE", {0.50196078431f, 0, 0.50196078431f}, {0, 0, 0}, 0.f, 2, -1, 0u},
+    {"MAT_CHECK_WHITE", {0, 0, 0}, {0, 0, 0}, 0.f, 2, 7, 1u},
+    {"MAT_COAT_NAVY", {0, 0, 0.50196078431f}, {1, 1, 1}, IOR_COAT, 6, -1, 0u},
+    {"MAT_COAT_PURPLE", {0.50196078431f, 0, 0.50196078431f}, {0, 0, 0}, IOR_COAT, 6, -1, 0u},
+    {"MAT_COAT_WAX", {0.9333f, 0.6666f, 0.6f}, {0.005f, 0.005f, 0.005f}, IOR_COAT, 6, -1, 0u},
+    {"MAT_TEST", {1, 1, 1}, {0, 0, 0}, 0.f, 2, 1, 1u},
+    {"MAT_SPECTRAL_FLINT", {1, 1, 1}, {0, 0, 0}, -1.7167f, 4, -1, 0u},
+    {"MAT_SPECTRAL_DIAMOND", {1, 1, 1}, {0, 0, 0}, -2.3991f, 4, -1, 0u},
 };
 
 static std::string strip_comments(const char *s) {
@@ -135,6 +154,15 @@ int lookup_material(const std::string &name, rt0_mesh &m) {
       m.nt = d.nt;
       m.mat_type = d.type;
       m.tex_type = d.tex;
+      m.mat_opts = d.opts;
+      for (const TexDef &t : kTextures) {
+        if (t.type != d.tex) continue;
+        for (int i = 0; i < 3; i++) {
+          m.tex_c_mask[i] = t.cm[i];
+          m.tex_e_mask[i] = t.em[i];
+        }
+        for (int i = 0; i < 4; i++) m.tex_params[i] = t.params[i];
+      }
       return 0;
     }
   }

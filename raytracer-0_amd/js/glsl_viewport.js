@@ -119,6 +119,27 @@ class GlslViewport {
     this.loadTime = Date.now();
     this._h = addon.create(this.canvas.width, this.canvas.height, this.device);
     this._compiled = null;
+    this.images = {};
+    // index.js:256-296: the RGBA noise image (u_rnd_tex) and opts.textures[0..3]
+    // (u_tex0..3), each loaded like loadTexture does (REPEAT, LINEAR).  Paths or
+    // {width, height, data} objects; the reference's asset paths are relative
+    // to its page, so the caller names them (opts.rndTexture for the noise).
+    if (opts.rndTexture) this.loadTexture({ name: 'rnd_tex' }, opts.rndTexture);
+    (opts.textures || []).forEach((t, i) => this.loadTexture({ name: 'tex' + i }, t));
+  }
+
+  // index.js:699-728 (assets only: the framebuffer textures live in librt0)
+  loadTexture(opts, img) {
+    const name = (opts && opts.name) || 'tex0';
+    const unit = name === 'rnd_tex' ? 4 : Number(name.replace('tex', ''));
+    if (!(unit >= 0 && unit <= 4)) throw new Error('unknown texture unit ' + name);
+    if (typeof img === 'string') img = addon.readPng(img);
+    if (img === null) {
+      addon.setTexture(this._h, unit, 0, 0, null);
+      return;
+    }
+    addon.setTexture(this._h, unit, img.width, img.height, img.data);
+    this.images[name === 'rnd_tex' ? 'rnd_img' : 'img' + unit] = img;
   }
 
   // index.js:384-440 (uniform upload); here also the "recompile" of scene/flags

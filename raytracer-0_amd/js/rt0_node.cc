@@ -290,6 +290,59 @@ static napi_value Resize(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+// setTexture(h, unit, width, height, rgba8: Uint8Array | null) -- loadTexture
+// (index.js:699-728) for u_tex0..3 (unit 0..3) and u_rnd_tex (unit 4)
+static napi_value SetTexture(napi_env env, napi_callback_info info) {
+  napi_value argv[5];
+  if (!get_args(env, info, 5, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  int32_t unit = 0, w = 0, h = 0;
+  napi_get_value_int32(env, argv[1], &unit);
+  napi_get_value_int32(env, argv[2], &w);
+  napi_get_value_int32(env, argv[3], &h);
+  const uint8_t *px = nullptr;
+  bool is_ta = false;
+  napi_is_typedarray(env, argv[4], &is_ta);
+  if (is_ta) {
+    napi_typedarray_type tt;
+    size_t len = 0, off = 0;
+    void *data = nullptr;
+    napi_value ab;
+    NAPI_OK(env, napi_get_typedarray_info(env, argv[4], &tt, &len, &data, &ab, &off));
+    if (tt != napi_uint8_array && tt != napi_uint8_clamped_array) return throw_rt0(env, RT0_E_ARG, "texture must be a Uint8Array");
+    if (len != (size_t)w * h * 4) return throw_rt0(env, RT0_E_ARG, "texture length != width*height*4");
+    px = (const uint8_t *)data;
+  }
+  RC_OR_THROW(rt0_set_texture(c, unit, w, h, px));
+  return nullptr;
+}
+
+// readPng(path) -> {width, height, data: Uint8Array (RGBA8, first row = top)}
+static napi_value ReadPng(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return nullptr;
+  std::string path = get_string(env, argv[0]);
+  int w = 0, h = 0;
+  uint8_t *px = nullptr;
+  int rc = rt0_png_read(path.c_str(), &w, &h, &px);
+  if (rc != RT0_OK) return throw_rt0(env, rc, ("cannot read PNG " + path).c_str());
+  void *data = nullptr;
+  napi_value ab, ta, o;
+  size_t n = (size_t)w * h * 4;
+  if (napi_create_arraybuffer(env, n, &data, &ab) != napi_ok) {
+    rt0_free(px);
+    return throw_rt0(env, RT0_E_ARG, "out of memory");
+  }
+  memcpy(data, px, n);
+  rt0_free(px);
+  NAPI_OK(env, napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta));
+  napi_create_object(env, &o);
+  set(env, o, "width", num(env, w));
+  set(env, o, "height", num(env, h));
+  set(env, o, "data", ta);
+  return o;
+}
+
 static napi_value LastKernelMs(napi_env env, napi_callback_info info) {
   napi_value argv[1];
   if (!get_args(env, info, 1, argv)) return nullptr;
@@ -321,6 +374,8 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"clear", nullptr, Clear, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"resize", nullptr, Resize, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"lastKernelMs", nullptr, LastKernelMs, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setTexture", nullptr, SetTexture, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"readPng", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   return exports;

@@ -30,8 +30,9 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
-           "rt0_png_write", "rt0_pfm_write", "rt0_free"]
+           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture"]
 
+TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
 
 
@@ -54,7 +55,9 @@ class Config(ctypes.Structure):
 class Mesh(ctypes.Structure):
     _fields_ = [("c", ctypes.c_float * 3), ("e", ctypes.c_float * 3), ("nt", ctypes.c_float),
                 ("mat_type", ctypes.c_int32), ("tex_type", ctypes.c_int32), ("type", ctypes.c_int32),
-                ("pos", ctypes.c_float * 3), ("joker", ctypes.c_float * 4), ("sdf_kind", ctypes.c_int32)]
+                ("pos", ctypes.c_float * 3), ("joker", ctypes.c_float * 4), ("sdf_kind", ctypes.c_int32),
+                ("tex_c_mask", ctypes.c_float * 3), ("tex_e_mask", ctypes.c_float * 3),
+                ("tex_params", ctypes.c_float * 4), ("mat_opts", ctypes.c_uint32)]
 
 
 _lib = None
@@ -84,6 +87,7 @@ def lib():
                                          P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
         "rt0_get_scene": (c_int, [c_void_p, P(Mesh), c_int, P(c_int), P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
         "rt0_set_camera": (c_int, [c_void_p, fp, fp, fp]),
+        "rt0_set_texture": (c_int, [c_void_p, c_int, c_int, c_int, P(ctypes.c_uint8)]),
         "rt0_render": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
         "rt0_render_async": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
         "rt0_sync": (c_int, [c_void_p]),
@@ -306,6 +310,18 @@ class Renderer:
                                       ctypes.byref(nl)))
         return list(meshes[:ne.value + ns.value]), ne.value, ns.value, list(lights[:nl.value])
 
+    def set_texture(self, unit, rgba8):
+        """loadTexture (index.js:699-728): unit 0..3 = u_tex0..3, TEX_NOISE = u_rnd_tex.
+        rgba8: uint8 [h, w, 4], first row = the image's top row; None unbinds."""
+        if rgba8 is None:
+            self._chk(lib().rt0_set_texture(self.h, unit, 0, 0, None))
+            return
+        a = np.ascontiguousarray(rgba8, np.uint8)
+        if a.ndim != 3 or a.shape[2] != 4:
+            raise ValueError("texture must be uint8 [h, w, 4]")
+        self._chk(lib().rt0_set_texture(self.h, unit, a.shape[1], a.shape[0],
+                                        a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+
     def set_camera(self, pos, lookat, params):
         a = [np.asarray(v, np.float32) for v in (pos, lookat, params)]
         self._chk(lib().rt0_set_camera(self.h, *[_fp(x) for x in a]))
@@ -456,6 +472,21 @@ class GlslViewport:
         self.temporalFrames = 5
         self.renderer = Renderer(self.width, self.height, device)
         self._compiled = None
+        self.images = {}
+        # index.js:256-296: noise image (u_rnd_tex) + opts.textures[0..3]; paths or uint8 arrays
+        if opts.get("rndTexture") is not None:
+            self.loadTexture({"name": "rnd_tex"}, opts["rndTexture"])
+        for i, t in enumerate(opts.get("textures", [])):
+            self.loadTexture({"name": "tex%d" % i}, t)
+
+    def loadTexture(self, opts, img):
+        """index.js:699-728 for the asset units (the framebuffers live in librt0)."""
+        name = (opts or {}).get("name", "tex0")
+        unit = TEX_NOISE if name == "rnd_tex" else int(name[3:])
+        if isinstance(img, str):
+            img = png_read(img)
+        self.renderer.set_texture(unit, img)
+        self.images["rnd_img" if unit == TEX_NOISE else "img%d" % unit] = img
 
     # index.js:384-440 -- uploads camera; here also (re)applies scene + flags
     def updateFrontTarget(self):

@@ -192,3 +192,29 @@ def test_tonemap_curves_and_image_files(cfgs, gpu_required, tmp_path):
     r.save_pfm(tmp_path / "c.pfm", 4)
     raw = open(tmp_path / "c.pfm", "rb").read()
     assert raw.startswith(b"PF\n32 24\n-1.0\n") and len(raw) == len(b"PF\n32 24\n-1.0\n") + 32 * 24 * 12
+
+
+def test_texture_api(cfgs, gpu_required):
+    """rt0_set_texture argument checks; re-binding a unit takes effect at the
+    next render; an unbound unit samples (0,0,0,1) (GL incomplete texture)."""
+    from textures import textures_for
+    cfg = [c for c in cfgs["configs"] if c["name"] == "tex_light_sphere"][0]
+    r = rt0.Renderer(32, 32)
+    rt0.configure(r, cfg, cfgs)
+    with pytest.raises(rt0.Rt0Error):
+        r.set_texture(5, np.zeros((4, 4, 4), np.uint8))
+    with pytest.raises(ValueError):
+        r.set_texture(0, np.zeros((4, 4, 3), np.uint8))
+    r.render(1, 1)
+    unbound = r.read_accum()
+    tex = textures_for(cfg)
+    r.set_texture(1, tex[1])
+    r.clear()
+    r.render(1, 1)
+    bound = r.read_accum()
+    assert not np.array_equal(bound, unbound)
+    # an all-(0,0,0,255) texture is what an unbound unit samples
+    r.set_texture(1, np.tile(np.array([0, 0, 0, 255], np.uint8), (8, 8, 1)))
+    r.clear()
+    r.render(1, 1)
+    assert np.array_equal(r.read_accum(), unbound)

@@ -87,3 +87,43 @@ console.log(vp.passes);
         raise AssertionError("%.4f of pixels differ (max %.3g); js vs py-aot %.4f, py vs py-aot %.4f, js rerun %.4f" % (
             bad.mean(), np.abs(a - b).max(), (a != c).any(-1).mean(), (b != c).any(-1).mean(),
             (a2 != a).any(-1).mean()))
+
+
+@pytest.mark.gpu
+def test_js_textures_from_png_match_python(cfgs, gpu_required, tmp_path):
+    """opts.textures / opts.rndTexture PNG paths (index.js:256-296) -> the same
+    texels and the same image as the Python host's set_texture."""
+    from textures import textures_for
+    cfg = [c for c in cfgs["configs"] if c["name"] == "tex_check_test"][0]
+    tex = textures_for(cfg)
+    paths = {}
+    for unit, img in tex.items():
+        paths[unit] = str(tmp_path / ("t%d.png" % unit))
+        rt0.png_write(paths[unit], img)
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    defines, consts = rt0.config_strings(cfg)
+    out = tmp_path / "acc.bin"
+    src = """
+const fs = require('fs');
+const v = require(%r);
+const vp = new v.GlslViewport(null, {width: 48, height: 48, rndTexture: %r, textures: %s});
+vp.defines = %s; vp.constants = %s; vp.scene = %s; vp.sdf_meshes = %s;
+vp.render(2);
+fs.writeFileSync(%r, Buffer.from(vp.accumulator().buffer));
+console.log(vp.passes);
+""" % (VIEWPORT, paths[4], json.dumps([paths[k] for k in range(4)]), json.dumps(defines), json.dumps(consts),
+       json.dumps(scene), json.dumps(sdf), str(out))
+    assert run_node(src).strip() == "2"
+    a = np.fromfile(str(out), np.float32).reshape(48, 48, 4)
+    r = rt0.Renderer(48, 48)
+    rt0.configure(r, cfg, cfgs)
+    for unit, img in tex.items():
+        r.set_texture(unit, img)
+    r.render(1, 2)
+    b = r.read_accum()
+    assert np.array_equal(a, b), (a != b).any(-1).mean()
+    # and the texture matters: without it the image differs
+    r.set_texture(1, None)
+    r.clear()
+    r.render(1, 2)
+    assert not np.array_equal(r.read_accum(), b)

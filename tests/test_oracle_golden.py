@@ -29,7 +29,13 @@ REL_TOL = 1e-3
 # Menger sponge: every path grazes many SDF edges where mod()/floor() ulp drift
 # flips the march (1.2% measured, all flips: median error 0).
 BAD_FRAC = {"default": 0.005, "c4_mandelbulb_vol": 0.02, "spectral_vol": 0.02, "menger_coat": 0.02,
-            "restir_mis_demo": 0.01}
+            "restir_mis_demo": 0.01,
+            # glossy METAL (value-noise roughness) reflections grazing the slab's
+            # front edge: SwiftShader's bilinear filtering of the noise texture
+            # differs from exact fp32 bilinear by ~6e-4 median (measured with a
+            # value_noise KAT shader), enough to move those reflections across
+            # the edge; 3.4% measured
+            "tex_sdf_metal": 0.04}
 
 
 def pixel_match(got, ref):
@@ -78,7 +84,8 @@ def test_rng_hash_schedule_bitexact():
 
 
 NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
-              "c4_mandelbulb_vol", "spectral_vol", "mis_demo_sdfbox", "menger_coat", "thinlens_glass"]
+              "c4_mandelbulb_vol", "spectral_vol", "mis_demo_sdfbox", "menger_coat", "thinlens_glass",
+              "tex_sdf_metal", "tex_light_sphere", "tex_check_test"]
 
 
 @pytest.mark.parametrize("name", NON_RESTIR)
