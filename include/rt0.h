@@ -128,6 +128,15 @@ int rt0_get_scene(const rt0_ctx *ctx, rt0_mesh *meshes, int max_meshes, int *n_m
 #define RT0_TEX_NOISE 4
 int rt0_set_texture(rt0_ctx *ctx, int unit, int w, int h, const uint8_t *rgba8);
 
+/* The environment cubemap (u_cubemap, used with USE_CUBEMAP), replacing the
+ * load_cubemap promise of index.js:298-331: six size x size RGB8 faces in the
+ * reference's upload order -X, -Y, -Z, +X, +Y, +Z (index.js:301-302; the
+ * page passes left, bottom, back, right, top, front, index.html:267-270),
+ * each first row = the image's top row (t = 0).  Sampled GL_LINEAR on the
+ * selected face with its edges clamped.  faces = NULL unbinds (samples
+ * (0,0,0,1)).  Copied; the caller keeps ownership. */
+int rt0_set_cubemap(rt0_ctx *ctx, int size, const uint8_t *const faces[6]);
+
 /* Uniforms u_camPos, u_camLookAt (a direction), u_camParams = (fov deg,
  * aperture, focal length) (index.js:421-423). */
 int rt0_set_camera(rt0_ctx *ctx, const float pos[3], const float lookat[3], const float params[3]);

@@ -81,7 +81,12 @@ def run_config(glrun, cfgs, cfg):
         cmd.append("--restir-out")
     # asset textures (u_tex0..3 = GL units 1..4, u_rnd_tex = unit 5; index.js:149-163)
     sys.path.insert(0, os.path.dirname(HERE))
-    from textures import textures_for
+    from textures import cubemap_for, textures_for
+    faces = cubemap_for(cfg)
+    if faces is not None:  # u_cubemap = GL unit 6, faces in the reference's upload order
+        fn = "%s_cube.rgb8" % prefix
+        np.concatenate([np.ascontiguousarray(f, np.uint8).ravel() for f in faces]).tofile(fn)
+        cmd += ["--cube", str(faces[0].shape[0]), fn]
     for unit, img in textures_for(cfg).items():
         fn = "%s_tex%d.rgba8" % (prefix, unit)
         np.ascontiguousarray(img, np.uint8).tofile(fn)

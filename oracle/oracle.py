@@ -41,6 +41,7 @@ def lib():
         L.or_hash2.argtypes = [ctypes.c_float, ctypes.c_float, fp]
         L.or_set_texture.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_uint8)]
+        L.or_set_cubemap.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))]
         L.or_pixel_seed.restype = ctypes.c_float
         L.or_pixel_seed.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_uint]
         _lib = L
@@ -82,9 +83,20 @@ class Oracle:
         L.or_set_resolution(self.h, width, height)
         self.restir = bool(cfg.get("defines", {}).get("USE_RESTIR"))
         self._tex = {}
-        from textures import textures_for
+        from textures import cubemap_for, textures_for
         for unit, img in textures_for(cfg).items():
             self.set_texture(unit, img)
+        faces = cubemap_for(cfg)
+        if faces is not None:
+            self.set_cubemap(faces)
+
+    def set_cubemap(self, faces):
+        """u_cubemap: six uint8 [n, n, 3] faces, reference order -X -Y -Z +X +Y +Z."""
+        arrs = [np.ascontiguousarray(f, np.uint8) for f in faces]
+        self._cube = arrs
+        P = ctypes.POINTER(ctypes.c_uint8)
+        ptrs = (P * 6)(*[a.ctypes.data_as(P) for a in arrs])
+        self._chk(lib().or_set_cubemap(self.h, arrs[0].shape[0], ptrs))
 
     def set_texture(self, unit, rgba8):
         """u_tex0..3 (unit 0..3) / u_rnd_tex (4): uint8 [h, w, 4], first row = t 0."""

@@ -186,6 +186,9 @@ typedef struct {
   /* asset textures (index.js:256-296): 0..3 u_tex0..3, 4 u_rnd_tex; RGBA8 */
   const unsigned char *tex_img[5];
   int tex_w[5], tex_h[5];
+  /* u_cubemap: 6 RGB8 faces in the reference's order -X -Y -Z +X +Y +Z */
+  const unsigned char *cube[6];
+  int cube_size;
   char err[256];
 } Oracle;
 
@@ -488,6 +491,61 @@ static void getTexel(const Oracle *o, const Material *mat, const Hit *hit, float
     x = f;
   }
   out[0] = out[1] = out[2] = out[3] = x;
+}
+
+/* texture(u_cubemap, d): GLES 3.0 cube face selection (major axis, table
+ * 3.21) and GL_LINEAR with seamless filtering (always on in ES 3.0, 3.8.10):
+ * a footprint texel beyond the face edge is fetched from the adjacent face
+ * (the texel centre mapped back to a direction and re-projected).  Measured:
+ * SwiftShader 4.1 does the same (cube_spheres: 99.2% -> 100% of pixels when
+ * edge clamping is replaced by this).  Unbound cubemap = (0,0,0,1). */
+static int cube_face(v3 d, float *s, float *t) { /* face in the reference order -X -Y -Z +X +Y +Z */
+  float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z), sc, tc, ma;
+  int face;
+  if (ax >= ay && ax >= az) { face = d.x >= 0 ? 3 : 0; sc = d.x >= 0 ? -d.z : d.z; tc = -d.y; ma = ax; }
+  else if (ay >= az) { face = d.y >= 0 ? 4 : 1; sc = d.x; tc = d.y >= 0 ? d.z : -d.z; ma = ay; }
+  else { face = d.z >= 0 ? 5 : 2; sc = d.z >= 0 ? d.x : -d.x; tc = -d.y; ma = az; }
+  *s = 0.5f * (sc / ma + 1.0f);
+  *t = 0.5f * (tc / ma + 1.0f);
+  return face;
+}
+static const unsigned char *cube_texel(const Oracle *o, int face, int i, int j) {
+  int n = o->cube_size;
+  if (i < 0 || i >= n || j < 0 || j >= n) {
+    float scn = 2.0f * ((float)i + 0.5f) / (float)n - 1.0f, tcn = 2.0f * ((float)j + 0.5f) / (float)n - 1.0f;
+    v3 d;
+    switch (face) { /* the face table inverted: a direction with major-axis component 1 */
+      case 3: d = V(1, -tcn, -scn); break;
+      case 0: d = V(-1, -tcn, scn); break;
+      case 4: d = V(scn, 1, tcn); break;
+      case 1: d = V(scn, -1, -tcn); break;
+      case 5: d = V(scn, -tcn, 1); break;
+      default: d = V(-scn, -tcn, -1); break;
+    }
+    float s, t;
+    face = cube_face(d, &s, &t);
+    i = (int)floorf(s * n);
+    j = (int)floorf(t * n);
+    i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+    j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+  }
+  return o->cube[face] + ((size_t)j * n + i) * 3;
+}
+static v3 cube_sample(const Oracle *o, v3 d) {
+  if (!o->cube[0]) return V(0, 0, 0);
+  float s, t;
+  int face = cube_face(d, &s, &t), n = o->cube_size;
+  float x = s * (float)n - 0.5f, y = t * (float)n - 0.5f;
+  float fx = floorf(x), fy = floorf(y), a = x - fx, b = y - fy;
+  int x0 = (int)fx, y0 = (int)fy;
+  const unsigned char *q00 = cube_texel(o, face, x0, y0), *q10 = cube_texel(o, face, x0 + 1, y0);
+  const unsigned char *q01 = cube_texel(o, face, x0, y0 + 1), *q11 = cube_texel(o, face, x0 + 1, y0 + 1);
+  float r[3];
+  for (int c = 0; c < 3; c++) {
+    float top = q00[c] + a * ((float)q10[c] - q00[c]), bot = q01[c] + a * ((float)q11[c] - q01[c]);
+    r[c] = (top + b * (bot - top)) / 255.0f;
+  }
+  return V(r[0], r[1], r[2]);
 }
 
 /* intersection(), raytracer.glsl:997-1082 (texture/uv parsing omitted: every
@@ -989,6 +1047,12 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
     }
   }
 
+  if (!*spec && o->use_cubemap) { /* environment NEE, raytracer.glsl:1887-1897 */
+    Hit eh;
+    v3 sr = getRandomDirection(o, nl, seed + bounce * 965.325f);
+    float te = intersection(F, add(x, muls(nl, EPSILON)), sr, &eh);
+    if (te == INF_T) *acc = add(*acc, mul(*mask, cube_sample(o, sr)));
+  }
   if (!*spec && o->sample_lights) {
     float base = seed + 8652.1f * fr;
     if (o->use_restir && o->use_mis) {
@@ -1127,7 +1191,9 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         if (o->ghost) ghost_brdf(F, &hit, st_c, st_e, st_inside, ro, rd, mask, spec, seed, depth);
         break;
       }
-      if (o->use_sky) {
+      if (o->use_cubemap) {
+        acc = add(acc, mul(mask, cube_sample(o, rd)));
+      } else if (o->use_sky) {
         float k = gclamp(rd.y * 0.6f + 0.5f, 0.3f, 1.0f);
         v3 sky = V(0.5f + 0.5f * cosf(TWO_PI * (0.525f + 0.9f * k)), 0.5f + 0.5f * cosf(TWO_PI * (0.408f + 0.97f * k)),
                    0.5f + 0.5f * cosf(TWO_PI * (0.409f + 0.8f * k)));
@@ -1375,7 +1441,6 @@ int or_set_define(void *h, const char *name, int on) {
   else if (!strcmp(name, "USE_SPECTRAL")) o->use_spectral = on;
   else if (!strcmp(name, "USE_VOLUMETRICS")) o->use_vol = on;
   else { snprintf(o->err, sizeof o->err, "unknown define %s", name); return -1; }
-  if (o->use_cubemap) { snprintf(o->err, sizeof o->err, "USE_CUBEMAP not supported"); return -1; }
   return 0;
 }
 
@@ -1416,6 +1481,13 @@ int or_set_texture(void *h, int unit, int w, int hh, const unsigned char *rgba8)
   o->tex_img[unit] = rgba8;
   o->tex_w[unit] = w;
   o->tex_h[unit] = hh;
+  return 0;
+}
+/* load_cubemap (index.js:298-331): 6 RGB8 faces, reference order; NULL unbinds */
+int or_set_cubemap(void *h, int size, const unsigned char *const *faces) {
+  Oracle *o = (Oracle *)h;
+  for (int i = 0; i < 6; i++) o->cube[i] = faces ? faces[i] : NULL;
+  o->cube_size = faces ? size : 0;
   return 0;
 }
 void or_set_resolution(void *h, int w, int hh) { ((Oracle *)h)->w = w; ((Oracle *)h)->h = hh; }

@@ -55,6 +55,25 @@ def image(w, h, seed):
     return px.astype(np.uint8)
 
 
+def cube_faces(n=64):
+    """Six smooth RGB8 n x n faces (reference upload order -X -Y -Z +X +Y +Z):
+    per-face gradients with a distinct blue level, so the sky a ray sees
+    depends on the face and the position on it."""
+    y, x = np.mgrid[0:n, 0:n].astype(np.int64)
+    faces = []
+    for i in range(6):
+        r = (x * 255) // (n - 1) if i % 2 == 0 else 255 - (x * 255) // (n - 1)
+        g = (y * 200) // (n - 1) + 20 * (i // 2)
+        b = np.full_like(x, 30 + 40 * i)
+        faces.append(np.stack([r, g, b], axis=-1).astype(np.uint8))
+    return faces
+
+
+def cubemap_for(cfg):
+    """Cube faces for a configs.json entry with "cubemap": true, else None."""
+    return cube_faces(64) if cfg.get("cubemap") else None
+
+
 def textures_for(cfg):
     """{unit: uint8 [h, w, 4]} for a configs.json entry's "textures" list
     ("noise" -> unit 4 = u_rnd_tex; "imageN" -> unit N = u_texN)."""

@@ -71,6 +71,7 @@ enum : uint32_t {
   F_RESTIR_DEF = 1u << 5,  // #define USE_RESTIR
   F_SPECTRAL = 1u << 6,
   F_VOL = 1u << 7,
+  F_CUBEMAP = 1u << 8,  // #define USE_CUBEMAP
 };
 
 struct LaunchParams {
@@ -108,4 +109,8 @@ struct LaunchParams {
   // unbound unit.
   const uint32_t *tex_img[RT0_TEX_UNITS];
   int32_t tex_w[RT0_TEX_UNITS], tex_h[RT0_TEX_UNITS];
+  // Cubemap (u_cubemap): 6 faces of cube_size^2 RGBA8 texels in GL face
+  // order +X -X +Y -Y +Z -Z, row 0 = t 0; null = unbound.
+  const uint32_t *cube;
+  int32_t cube_size;
 };

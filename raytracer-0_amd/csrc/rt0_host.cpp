@@ -65,6 +65,8 @@ struct rt0_ctx {
   int max_frames_per_launch = 64;
   uint32_t *d_tex[RT0_TEX_UNITS] = {};  // asset textures (rt0_set_texture)
   int tex_w[RT0_TEX_UNITS] = {}, tex_h[RT0_TEX_UNITS] = {};
+  uint32_t *d_cube = nullptr;  // cubemap faces, GL order (rt0_set_cubemap)
+  int cube_size = 0;
   SceneDev host_scene;   // what d_scene holds (also the JIT's scene data)
   bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
   std::string jit_err;
@@ -155,6 +157,7 @@ void rt0_destroy(rt0_ctx *c) {
   if (c->d_samples) (void)hipFree(c->d_samples);
   for (auto &t : c->d_tex)
     if (t) (void)hipFree(t);
+  if (c->d_cube) (void)hipFree(c->d_cube);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -171,7 +174,6 @@ int rt0_parse_config(const char *const *defines, int nd, const char *const *cons
 
 int rt0_set_config(rt0_ctx *c, const rt0_config *cfg) {
   if (!c || !cfg) return RT0_E_ARG;
-  if (cfg->defines & RT0_USE_CUBEMAP) return fail(c, RT0_E_UNSUPPORTED, "USE_CUBEMAP is not supported yet");
   if (cfg->render_mode != 0) return fail(c, RT0_E_UNSUPPORTED, "RENDER_MODE 1 (animated) is not supported");
   if (cfg->max_bounces < 0 || cfg->marching_steps < 0) return fail(c, RT0_E_ARG, "negative loop bound");
   c->cfg = *cfg;
@@ -328,6 +330,36 @@ int rt0_set_texture(rt0_ctx *c, int unit, int w, int h, const uint8_t *rgba8) {
   return RT0_OK;
 }
 
+int rt0_set_cubemap(rt0_ctx *c, int size, const uint8_t *const faces[6]) {
+  if (!c) return RT0_E_ARG;
+  if (faces && (size <= 0 || size > 16384)) return fail(c, RT0_E_ARG, "cubemap face size out of range");
+  if (faces)
+    for (int i = 0; i < 6; i++)
+      if (!faces[i]) return fail(c, RT0_E_ARG, "cubemap face is NULL");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->d_cube) HIPCHK(c, hipFree(c->d_cube));
+  c->d_cube = nullptr;
+  c->cube_size = 0;
+  if (!faces) return RT0_OK;
+  // reference order (-X, -Y, -Z, +X, +Y, +Z; index.js:301-302) -> GL order
+  // (+X, -X, +Y, -Y, +Z, -Z); RGB8 -> RGBA8 so a texel is one aligned dword
+  static const int gl_of_ref[6] = {1, 3, 5, 0, 2, 4};
+  const size_t n = (size_t)size * size;
+  std::vector<uint32_t> host(n * 6);
+  for (int i = 0; i < 6; i++) {
+    uint32_t *dst = host.data() + n * gl_of_ref[i];
+    const uint8_t *src = faces[i];
+    for (size_t k = 0; k < n; k++)
+      dst[k] = (uint32_t)src[3 * k] | ((uint32_t)src[3 * k + 1] << 8) | ((uint32_t)src[3 * k + 2] << 16) | 0xff000000u;
+  }
+  HIPCHK(c, hipMalloc(&c->d_cube, host.size() * 4));
+  HIPCHK(c, hipMemcpyAsync(c->d_cube, host.data(), host.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->cube_size = size;
+  return RT0_OK;
+}
+
 int rt0_set_camera(rt0_ctx *c, const float pos[3], const float lookat[3], const float params[3]) {
   if (!c || !pos || !lookat || !params) return RT0_E_ARG;
   memcpy(c->cam_pos, pos, sizeof c->cam_pos);
@@ -386,6 +418,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   if (g.defines & RT0_USE_RESTIR) f |= F_RESTIR_DEF;
   if (g.defines & RT0_USE_SPECTRAL) f |= F_SPECTRAL;
   if (g.defines & RT0_USE_VOLUMETRICS) f |= F_VOL;
+  if (g.defines & RT0_USE_CUBEMAP) f |= F_CUBEMAP;
   p.flags = f;
   p.max_bounces = g.max_bounces;
   p.max_diff = g.max_diff_bounces;
@@ -407,6 +440,8 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
     p.tex_w[u] = c->tex_w[u];
     p.tex_h[u] = c->tex_h[u];
   }
+  p.cube = c->d_cube;
+  p.cube_size = c->cube_size;
   p.accum = c->acc();
   p.counters = c->d_counters;
   if (c->n_shards > 1) {  // one contiguous block per shard (checked for ReSTIR in render_impl)
@@ -433,7 +468,6 @@ static int choose_variant(const rt0_ctx *c) {
 static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
   if (!c || n < 0) return RT0_E_ARG;
   if (!c->has_scene) return fail(c, RT0_E_STATE, "rt0_render before rt0_set_scene*");
-  if (c->cfg.defines & RT0_USE_CUBEMAP) return fail(c, RT0_E_UNSUPPORTED, "USE_CUBEMAP is not supported yet");
   const bool restir = (c->cfg.defines & RT0_USE_RESTIR) != 0;
   // ReSTIR reads neighbouring pixels of the previous passes' reservoirs: a
   // shard must own one contiguous row block, whose halo the caller exchanges

@@ -664,6 +664,87 @@ DEV T4 get_texel(const LaunchParams &P, const TexRec &t, v3 pos, float u, float 
   }
   return t4s(0.0f);
 }
+// texture(u_cubemap, d) (raytracer.glsl:1895, 2060): GL ES 3.0 cube face
+// selection (major axis, table 3.21) and GL_LINEAR with seamless filtering
+// (always on in ES 3.0): a footprint texel beyond the face edge is fetched
+// from the adjacent face (its centre mapped back to a direction and
+// re-projected) -- what the reference executor does.  Faces in
+// GL order +X -X +Y -Y +Z -Z; unbound = (0,0,0,1).
+DEV int cube_face(v3 d, float &s, float &t) {
+  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  int face;
+  float sc, tc, ma;
+  if (ax >= ay && ax >= az) {
+    face = d.x >= 0.f ? 0 : 1;
+    sc = d.x >= 0.f ? -d.z : d.z;
+    tc = -d.y;
+    ma = ax;
+  } else if (ay >= az) {
+    face = d.y >= 0.f ? 2 : 3;
+    sc = d.x;
+    tc = d.y >= 0.f ? d.z : -d.z;
+    ma = ay;
+  } else {
+    face = d.z >= 0.f ? 4 : 5;
+    sc = d.z >= 0.f ? d.x : -d.x;
+    tc = -d.y;
+    ma = az;
+  }
+  s = 0.5f * (sc / ma + 1.0f);
+  t = 0.5f * (tc / ma + 1.0f);
+  return face;
+}
+DEV uint32_t cube_texel(const LaunchParams &P, int face, int i, int j) {
+  const int n = P.cube_size;
+  if (i < 0 || i >= n || j < 0 || j >= n) {  // seamless: the neighbouring face's texel
+    const float scn = 2.0f * ((float)i + 0.5f) / (float)n - 1.0f, tcn = 2.0f * ((float)j + 0.5f) / (float)n - 1.0f;
+    v3 d;
+    switch (face) {  // the face table inverted (major-axis component 1)
+      case 0: d = mk(1.f, -tcn, -scn); break;
+      case 1: d = mk(-1.f, -tcn, scn); break;
+      case 2: d = mk(scn, 1.f, tcn); break;
+      case 3: d = mk(scn, -1.f, -tcn); break;
+      case 4: d = mk(scn, -tcn, 1.f); break;
+      default: d = mk(-scn, -tcn, -1.f); break;
+    }
+    float s, t;
+    face = cube_face(d, s, t);
+    i = min(max((int)floorf(s * (float)n), 0), n - 1);
+    j = min(max((int)floorf(t * (float)n), 0), n - 1);
+  }
+  return P.cube[((size_t)face * n + j) * n + i];
+}
+DEV T4 cube_sample(const LaunchParams &P, v3 d) {
+  if (P.cube == nullptr) return T4{0.f, 0.f, 0.f, 1.f};
+  float s, t;
+  const int face = cube_face(d, s, t), n = P.cube_size;
+  const float x = s * (float)n - 0.5f, y = t * (float)n - 0.5f;
+  const float fx = floorf(x), fy = floorf(y);
+  const float a = x - fx, b = y - fy;
+  const int x0 = (int)fx, y0 = (int)fy;
+  uint32_t q00, q10, q01, q11;
+  if (x0 >= 0 && y0 >= 0 && x0 + 1 < n && y0 + 1 < n) {  // footprint inside the face (the common case)
+    const uint32_t *__restrict__ img = P.cube + ((size_t)face * n + y0) * n + x0;
+    q00 = img[0];
+    q10 = img[1];
+    q01 = img[n];
+    q11 = img[n + 1];
+  } else {
+    q00 = cube_texel(P, face, x0, y0);
+    q10 = cube_texel(P, face, x0 + 1, y0);
+    q01 = cube_texel(P, face, x0, y0 + 1);
+    q11 = cube_texel(P, face, x0 + 1, y0 + 1);
+  }
+  float r[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float t00 = (float)((q00 >> (8 * c)) & 255u), t10 = (float)((q10 >> (8 * c)) & 255u);
+    const float t01 = (float)((q01 >> (8 * c)) & 255u), t11 = (float)((q11 >> (8 * c)) & 255u);
+    const float top = t00 + a * (t10 - t00), bot = t01 + a * (t11 - t01);
+    r[c] = (top + b * (bot - top)) / 255.0f;
+  }
+  return T4{r[0], r[1], r[2], 1.0f};
+}
 // hit.uv (1051-1076) + getTexel for a hit on a textured mesh (type >= 0)
 DEV T4 hit_texel(const LaunchParams &P, const TexRec &t, const Hit &h) {
   float u = -1.0f, v = -1.0f;
@@ -1144,7 +1225,10 @@ struct Integrator {
       }
       if (t == INF_T) {
         if (!spec && flag(F_SAMPLE_LIGHTS)) break;
-        if (flag(F_SKY)) {
+        if (flag(F_CUBEMAP)) {  // 2059-2060 (USE_CUBEMAP wins over the procedural sky)
+          const T4 cm = cube_sample(P, rd);
+          acc = acc + mask * mk(cm.r, cm.g, cm.b);
+        } else if (flag(F_SKY)) {
           float k = fminf(fmaxf(rd.y * 0.6f + 0.5f, 0.3f), 1.0f);
           v3 sky = mk(0.5f + 0.5f * fcos(TWO_PI * (0.525f + 0.9f * k)), 0.5f + 0.5f * fcos(TWO_PI * (0.408f + 0.97f * k)),
                       0.5f + 0.5f * fcos(TWO_PI * (0.409f + 0.8f * k)));
@@ -1245,6 +1329,15 @@ struct Integrator {
           mask = mask * c;
           ++diff_b;
           spec = false;
+        }
+      }
+      if (!spec && flag(F_CUBEMAP)) {  // environment NEE, 1887-1897
+        const float s = nc_addmul(seed, bounce, 965.325f);
+        const v3 sr = flag(F_BIASED) ? sample_cosine(nl, s) : sample_cone(nl, 1.0f, s);
+        Hit eh;
+        if (isect(x + nl * EPSILON, sr, eh) == INF_T) {
+          const T4 cm = cube_sample(P, sr);
+          acc = acc + mask * mk(cm.r, cm.g, cm.b);
         }
       }
       if (!spec && flag(F_SAMPLE_LIGHTS)) acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;

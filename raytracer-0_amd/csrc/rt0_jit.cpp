@@ -285,6 +285,7 @@ uint32_t flags_from_config(const rt0_config &g) {
   if (g.defines & RT0_USE_RESTIR) f |= F_RESTIR_DEF;
   if (g.defines & RT0_USE_SPECTRAL) f |= F_SPECTRAL;
   if (g.defines & RT0_USE_VOLUMETRICS) f |= F_VOL;
+  if (g.defines & RT0_USE_CUBEMAP) f |= F_CUBEMAP;
   return f;
 }
 

@@ -126,6 +126,31 @@ class GlslViewport {
     // to its page, so the caller names them (opts.rndTexture for the noise).
     if (opts.rndTexture) this.loadTexture({ name: 'rnd_tex' }, opts.rndTexture);
     (opts.textures || []).forEach((t, i) => this.loadTexture({ name: 'tex' + i }, t));
+    // index.js:298-331: opts.cubemap = six faces (left, bottom, back, right,
+    // top, front = -X -Y -Z +X +Y +Z), paths or {width, height, data} (RGB or RGBA)
+    if (opts.cubemap) this.loadCubemap(opts.cubemap);
+  }
+
+  loadCubemap(faces) {
+    if (!faces) {
+      addon.setCubemap(this._h, 0, null);
+      return;
+    }
+    const rgb = faces.map((f) => {
+      const img = typeof f === 'string' ? addon.readPng(f) : f;
+      const n = img.width * img.height;
+      if (img.data.length === n * 3) return { img, data: img.data };
+      const d = new Uint8Array(n * 3);
+      for (let k = 0; k < n; k++) {
+        d[3 * k] = img.data[4 * k]; d[3 * k + 1] = img.data[4 * k + 1]; d[3 * k + 2] = img.data[4 * k + 2];
+      }
+      return { img, data: d };
+    });
+    const size = rgb[0].img.width;
+    if (rgb.length !== 6 || rgb.some((f) => f.img.width !== size || f.img.height !== size))
+      throw new Error('cubemap: six square faces of one size expected');
+    addon.setCubemap(this._h, size, rgb.map((f) => f.data));
+    rgb.forEach((f, i) => { this.images['cubemap_img' + i] = f.img; });
   }
 
   // index.js:699-728 (assets only: the framebuffer textures live in librt0)

@@ -317,6 +317,39 @@ static napi_value SetTexture(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+// setCubemap(h, size, faces: Uint8Array[6] (RGB8, reference order -X -Y -Z
+// +X +Y +Z) | null) -- load_cubemap, index.js:298-331
+static napi_value SetCubemap(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  int32_t size = 0;
+  napi_get_value_int32(env, argv[1], &size);
+  bool is_arr = false;
+  napi_is_array(env, argv[2], &is_arr);
+  if (!is_arr) {
+    RC_OR_THROW(rt0_set_cubemap(c, 0, nullptr));
+    return nullptr;
+  }
+  const uint8_t *faces[6];
+  for (uint32_t i = 0; i < 6; i++) {
+    napi_value e;
+    bool is_ta = false;
+    if (napi_get_element(env, argv[2], i, &e) != napi_ok) return throw_rt0(env, RT0_E_ARG, "six faces expected");
+    napi_is_typedarray(env, e, &is_ta);
+    if (!is_ta) return throw_rt0(env, RT0_E_ARG, "cubemap face must be a Uint8Array");
+    napi_typedarray_type tt;
+    size_t len = 0, off = 0;
+    void *data = nullptr;
+    napi_value ab;
+    NAPI_OK(env, napi_get_typedarray_info(env, e, &tt, &len, &data, &ab, &off));
+    if (len != (size_t)size * size * 3) return throw_rt0(env, RT0_E_ARG, "cubemap face length != size*size*3");
+    faces[i] = (const uint8_t *)data;
+  }
+  RC_OR_THROW(rt0_set_cubemap(c, size, faces));
+  return nullptr;
+}
+
 // readPng(path) -> {width, height, data: Uint8Array (RGBA8, first row = top)}
 static napi_value ReadPng(napi_env env, napi_callback_info info) {
   napi_value argv[1];
@@ -376,6 +409,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"lastKernelMs", nullptr, LastKernelMs, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setTexture", nullptr, SetTexture, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readPng", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setCubemap", nullptr, SetCubemap, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   return exports;

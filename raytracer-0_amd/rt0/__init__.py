@@ -30,7 +30,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
-           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture"]
+           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap"]
 
 TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
@@ -88,6 +88,7 @@ def lib():
         "rt0_get_scene": (c_int, [c_void_p, P(Mesh), c_int, P(c_int), P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
         "rt0_set_camera": (c_int, [c_void_p, fp, fp, fp]),
         "rt0_set_texture": (c_int, [c_void_p, c_int, c_int, c_int, P(ctypes.c_uint8)]),
+        "rt0_set_cubemap": (c_int, [c_void_p, c_int, P(P(ctypes.c_uint8))]),
         "rt0_render": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
         "rt0_render_async": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
         "rt0_sync": (c_int, [c_void_p]),
@@ -187,6 +188,11 @@ def png_read(path):
         return np.ctypeslib.as_array(p, shape=(h.value, w.value, 4)).copy()
     finally:
         lib().rt0_free(p)
+
+
+def image_read(path):
+    """An asset file -> [h, w, 4] uint8 (PNG; JPEG for the reference's cubemap faces)."""
+    return png_read(path)
 
 
 def png_write(path, rgba, flip_y=False):
@@ -321,6 +327,20 @@ class Renderer:
             raise ValueError("texture must be uint8 [h, w, 4]")
         self._chk(lib().rt0_set_texture(self.h, unit, a.shape[1], a.shape[0],
                                         a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+
+    def set_cubemap(self, faces):
+        """load_cubemap (index.js:298-331): six uint8 [n, n, 3] faces in the
+        reference's order -X, -Y, -Z, +X, +Y, +Z (left, bottom, back, right,
+        top, front); None unbinds."""
+        if faces is None:
+            self._chk(lib().rt0_set_cubemap(self.h, 0, None))
+            return
+        arrs = [np.ascontiguousarray(f, np.uint8) for f in faces]
+        if len(arrs) != 6 or any(a.ndim != 3 or a.shape[2] != 3 or a.shape[:2] != arrs[0].shape[:2] or
+                                 a.shape[0] != a.shape[1] for a in arrs):
+            raise ValueError("six square uint8 [n, n, 3] faces expected")
+        ptrs = (ctypes.POINTER(ctypes.c_uint8) * 6)(*[a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) for a in arrs])
+        self._chk(lib().rt0_set_cubemap(self.h, arrs[0].shape[0], ptrs))
 
     def set_camera(self, pos, lookat, params):
         a = [np.asarray(v, np.float32) for v in (pos, lookat, params)]
@@ -478,13 +498,26 @@ class GlslViewport:
             self.loadTexture({"name": "rnd_tex"}, opts["rndTexture"])
         for i, t in enumerate(opts.get("textures", [])):
             self.loadTexture({"name": "tex%d" % i}, t)
+        # index.js:298-331: six faces left, bottom, back, right, top, front (-X -Y -Z +X +Y +Z)
+        if opts.get("cubemap") is not None:
+            self.loadCubemap(opts["cubemap"])
+
+    def loadCubemap(self, faces):
+        """Six faces (paths or uint8 [n, n, 3|4] arrays) in the reference's order."""
+        if faces is None:
+            self.renderer.set_cubemap(None)
+            return
+        imgs = [image_read(f) if isinstance(f, str) else np.asarray(f, np.uint8) for f in faces]
+        self.renderer.set_cubemap([a[..., :3] for a in imgs])
+        for i, a in enumerate(imgs):
+            self.images["cubemap_img%d" % i] = a
 
     def loadTexture(self, opts, img):
         """index.js:699-728 for the asset units (the framebuffers live in librt0)."""
         name = (opts or {}).get("name", "tex0")
         unit = TEX_NOISE if name == "rnd_tex" else int(name[3:])
         if isinstance(img, str):
-            img = png_read(img)
+            img = image_read(img)
         self.renderer.set_texture(unit, img)
         self.images["rnd_img" if unit == TEX_NOISE else "img%d" % unit] = img
 

@@ -16,7 +16,7 @@ import pytest
 
 import oracle as O
 import rt0
-from textures import textures_for
+from textures import cubemap_for, textures_for
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -29,7 +29,7 @@ BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol": 0.03, "m
             # glossy METAL reflections grazing the slab's front edge; the noise
             # texture's bilinear weights differ from SwiftShader's by ~6e-4
             # (measured), which moves the reflection direction
-            "tex_sdf_metal": 0.05}
+            "tex_sdf_metal": 0.05, "cube_sdf_metal": 0.08}
 
 
 def cfg_by_name(cfgs, name):
@@ -48,6 +48,9 @@ def configure(r, cfg, cfgs):
     rt0.configure(r, cfg, cfgs)
     for unit, img in textures_for(cfg).items():
         r.set_texture(unit, img)
+    faces = cubemap_for(cfg)
+    if faces is not None:
+        r.set_cubemap(faces)
 
 
 def make(cfgs, name, w, h):
@@ -68,7 +71,7 @@ def have(name):
 
 NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
               "mis_demo_sdfbox", "menger_coat", "thinlens_glass", "c4_mandelbulb_vol", "spectral_vol",
-              "tex_sdf_metal", "tex_light_sphere", "tex_check_test"]
+              "tex_sdf_metal", "tex_light_sphere", "tex_check_test", "cube_spheres", "cube_sdf_metal"]
 
 
 @pytest.mark.parametrize("name", NON_RESTIR)
@@ -131,7 +134,7 @@ def test_gpu_restir_chain_matches_oracle_chain(cfgs, gpu_required):
 
 @pytest.mark.parametrize("name,size,frames", [("c2_cornell_mis_8", 128, 2), ("cornell_nee_plain", 96, 1),
                                               ("c4_mandelbulb_vol", 48, 1), ("tex_check_test", 96, 2),
-                                              ("tex_light_sphere", 96, 1)])
+                                              ("tex_light_sphere", 96, 1), ("cube_spheres", 96, 2)])
 def test_gpu_matches_oracle_beyond_fixtures(name, size, frames, cfgs, gpu_required):
     cfg = cfg_by_name(cfgs, name)
     over = {"MAX_BOUNCES": 12} if name == "c4_mandelbulb_vol" else {}
@@ -167,7 +170,7 @@ def test_gpu_accumulation_is_sequential_sum(cfgs, gpu_required):
 
 
 @pytest.mark.parametrize("name", ["c2_cornell_mis_8", "c3_outdoor_restir", "spectral_vol", "mis_demo_sdfbox",
-                                  "tex_check_test", "tex_sdf_metal"])
+                                  "tex_check_test", "tex_sdf_metal", "cube_spheres"])
 def test_jit_matches_aot(name, cfgs, gpu_required):
     """Scene-specialised kernels == ahead-of-time kernels (same arithmetic up
     to FMA placement, so compare with the parity tolerance)."""

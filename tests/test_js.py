@@ -127,3 +127,44 @@ console.log(vp.passes);
     r.clear()
     r.render(1, 2)
     assert not np.array_equal(r.read_accum(), b)
+
+
+@pytest.mark.gpu
+def test_js_cubemap_faces_match_python(cfgs, gpu_required, tmp_path):
+    """opts.cubemap (index.js:298-331) as six PNG faces through the addon ==
+    the Python host's set_cubemap, bit for bit; unbinding changes the image."""
+    from textures import cubemap_for
+    cfg = [c for c in cfgs["configs"] if c["name"] == "cube_spheres"][0]
+    faces = cubemap_for(cfg)
+    paths = []
+    for i, f in enumerate(faces):
+        paths.append(str(tmp_path / ("f%d.png" % i)))
+        rgba = np.concatenate([f, np.full(f.shape[:2] + (1,), 255, np.uint8)], axis=-1)
+        rt0.png_write(paths[-1], rgba)
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    defines, consts = rt0.config_strings(cfg)
+    cam = cfg["camera"]
+    out = tmp_path / "acc.bin"
+    src = """
+const fs = require('fs');
+const v = require(%r);
+const vp = new v.GlslViewport(null, {width: 48, height: 48, cubemap: %s});
+vp.defines = %s; vp.constants = %s; vp.scene = %s; vp.sdf_meshes = %s;
+vp.camera.origin = new v.Vector3(%r, %r, %r); vp.camera.lookat = new v.Vector3(%r, %r, %r); vp.camera.fov = %r;
+vp.render(2);
+fs.writeFileSync(%r, Buffer.from(vp.accumulator().buffer));
+console.log(vp.passes);
+""" % (VIEWPORT, json.dumps(paths), json.dumps(defines), json.dumps(consts), json.dumps(scene), json.dumps(sdf),
+       *cam["origin"], *cam["lookat"], cam["fov"], str(out))
+    assert run_node(src).strip() == "2"
+    a = np.fromfile(str(out), np.float32).reshape(48, 48, 4)
+    r = rt0.Renderer(48, 48)
+    rt0.configure(r, cfg, cfgs)
+    r.set_cubemap(faces)
+    r.render(1, 2)
+    b = r.read_accum()
+    assert np.array_equal(a, b), (a != b).any(-1).mean()
+    r.set_cubemap(None)
+    r.clear()
+    r.render(1, 2)
+    assert not np.array_equal(r.read_accum(), b)

@@ -35,7 +35,16 @@ BAD_FRAC = {"default": 0.005, "c4_mandelbulb_vol": 0.02, "spectral_vol": 0.02, "
             # differs from exact fp32 bilinear by ~6e-4 median (measured with a
             # value_noise KAT shader), enough to move those reflections across
             # the edge; 3.4% measured
-            "tex_sdf_metal": 0.04}
+            "tex_sdf_metal": 0.04,
+            # the same scene under a cubemap: the metal's glossy reflections now
+            # see a textured environment instead of the smooth procedural sky
+            "cube_sdf_metal": 0.07}
+# Mean-radiance tolerance (default 2e-3).  cube_sdf_metal: in this SDF-only
+# scene SwiftShader's image depends on the ORDER of the two SDF statements
+# (mean 0.4244 vs 0.4310 when swapped; with a plain mirror instead of METAL the
+# mismatch stays 6.4%), while GLSL semantics -- and the restatement, 0.4177 vs
+# 0.4179 -- are order-independent: an executor artefact, DESIGN.md sec. 2.
+MEAN_TOL = {"cube_sdf_metal": 0.02}
 
 
 def pixel_match(got, ref):
@@ -85,7 +94,7 @@ def test_rng_hash_schedule_bitexact():
 
 NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
               "c4_mandelbulb_vol", "spectral_vol", "mis_demo_sdfbox", "menger_coat", "thinlens_glass",
-              "tex_sdf_metal", "tex_light_sphere", "tex_check_test"]
+              "tex_sdf_metal", "tex_light_sphere", "tex_check_test", "cube_spheres", "cube_sdf_metal"]
 
 
 @pytest.mark.parametrize("name", NON_RESTIR)
@@ -102,7 +111,7 @@ def test_oracle_radiance_matches_reference(name, cfgs):
     assert nan.mean() < 0.001
     # mean radiance agrees tightly (a systematic error would shift it)
     m = ~nan
-    assert abs(got[m].mean() - gold[m].mean()) <= 2e-3 * max(1.0, abs(gold[m].mean()))
+    assert abs(got[m].mean() - gold[m].mean()) <= MEAN_TOL.get(name, 2e-3) * max(1.0, abs(gold[m].mean()))
 
 
 @pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo"])
