@@ -185,6 +185,12 @@ int rt0_png_decode(const uint8_t *data, size_t size, int *w, int *h, uint8_t **r
 int rt0_png_read(const char *path, int *w, int *h, uint8_t **rgba_out);
 int rt0_png_write(const char *path, int w, int h, const uint8_t *rgba, int flip_y);
 int rt0_pfm_write(const char *path, int w, int h, const float *rgba, float scale);
+/* Baseline JPEG (SOF0, 8-bit, 1 or 3 components, sampling factors 1..2,
+ * restart markers; JFIF YCbCr) -> RGBA8, the format of the reference's
+ * cubemap faces (the .jpg files under cubemaps/, loaded at index.js:298-331).
+ * Progressive / arithmetic / 12-bit files return RT0_E_UNSUPPORTED. */
+int rt0_jpeg_decode(const uint8_t *data, size_t size, int *w, int *h, uint8_t **rgba_out);
+int rt0_jpeg_read(const char *path, int *w, int *h, uint8_t **rgba_out);
 void rt0_free(void *p);
 
 /* ReSTIR reservoir MRTs (raytracer.glsl:2171-2179).  which: 0 = current output

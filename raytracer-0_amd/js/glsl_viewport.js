@@ -137,7 +137,7 @@ class GlslViewport {
       return;
     }
     const rgb = faces.map((f) => {
-      const img = typeof f === 'string' ? addon.readPng(f) : f;
+      const img = typeof f === 'string' ? addon.readImage(f) : f;
       const n = img.width * img.height;
       if (img.data.length === n * 3) return { img, data: img.data };
       const d = new Uint8Array(n * 3);
@@ -158,7 +158,7 @@ class GlslViewport {
     const name = (opts && opts.name) || 'tex0';
     const unit = name === 'rnd_tex' ? 4 : Number(name.replace('tex', ''));
     if (!(unit >= 0 && unit <= 4)) throw new Error('unknown texture unit ' + name);
-    if (typeof img === 'string') img = addon.readPng(img);
+    if (typeof img === 'string') img = addon.readImage(img);
     if (img === null) {
       addon.setTexture(this._h, unit, 0, 0, null);
       return;

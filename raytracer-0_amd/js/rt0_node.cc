@@ -8,6 +8,7 @@
 #include <node_api.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -350,15 +351,23 @@ static napi_value SetCubemap(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
-// readPng(path) -> {width, height, data: Uint8Array (RGBA8, first row = top)}
+// readPng(path) / readImage(path) -> {width, height, data: Uint8Array (RGBA8,
+// first row = top)}; PNG or baseline JPEG
 static napi_value ReadPng(napi_env env, napi_callback_info info) {
   napi_value argv[1];
   if (!get_args(env, info, 1, argv)) return nullptr;
   std::string path = get_string(env, argv[0]);
   int w = 0, h = 0;
   uint8_t *px = nullptr;
-  int rc = rt0_png_read(path.c_str(), &w, &h, &px);
-  if (rc != RT0_OK) return throw_rt0(env, rc, ("cannot read PNG " + path).c_str());
+  // PNG or baseline JPEG by signature (textures are PNG, cubemap faces JPEG)
+  unsigned char sig[2] = {0, 0};
+  if (FILE *f = fopen(path.c_str(), "rb")) {
+    if (fread(sig, 1, 2, f) != 2) sig[0] = 0;
+    fclose(f);
+  }
+  int rc = (sig[0] == 0xFF && sig[1] == 0xD8) ? rt0_jpeg_read(path.c_str(), &w, &h, &px)
+                                               : rt0_png_read(path.c_str(), &w, &h, &px);
+  if (rc != RT0_OK) return throw_rt0(env, rc, ("cannot read image " + path).c_str());
   void *data = nullptr;
   napi_value ab, ta, o;
   size_t n = (size_t)w * h * 4;
@@ -409,6 +418,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"lastKernelMs", nullptr, LastKernelMs, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setTexture", nullptr, SetTexture, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readPng", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"readImage", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setCubemap", nullptr, SetCubemap, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);

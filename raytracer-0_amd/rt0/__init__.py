@@ -30,7 +30,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
-           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap"]
+           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read"]
 
 TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
@@ -120,6 +120,8 @@ def lib():
         "rt0_png_write": (c_int, [ctypes.c_char_p, c_int, c_int, P(ctypes.c_uint8), c_int]),
         "rt0_pfm_write": (c_int, [ctypes.c_char_p, c_int, c_int, fp, c_float]),
         "rt0_free": (None, [c_void_p]),
+        "rt0_jpeg_decode": (c_int, [c_void_p, ctypes.c_size_t, P(c_int), P(c_int), P(P(ctypes.c_uint8))]),
+        "rt0_jpeg_read": (c_int, [ctypes.c_char_p, P(c_int), P(c_int), P(P(ctypes.c_uint8))]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -190,8 +192,25 @@ def png_read(path):
         lib().rt0_free(p)
 
 
+def jpeg_decode(data):
+    """Baseline JPEG bytes -> [h, w, 4] uint8."""
+    w, h, p = ctypes.c_int(), ctypes.c_int(), ctypes.POINTER(ctypes.c_uint8)()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    _check_io(lib().rt0_jpeg_decode(buf, len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(p)), "jpeg_decode")
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 4)).copy()
+    finally:
+        lib().rt0_free(p)
+
+
 def image_read(path):
-    """An asset file -> [h, w, 4] uint8 (PNG; JPEG for the reference's cubemap faces)."""
+    """An asset file -> [h, w, 4] uint8: PNG (textures) or baseline JPEG (the
+    reference's cubemap faces), told apart by the file signature."""
+    with open(path, "rb") as f:
+        head = f.read(2)
+    if head == b"\xff\xd8":
+        with open(path, "rb") as f:
+            return jpeg_decode(f.read())
     return png_read(path)
 
 

@@ -30,6 +30,10 @@ BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol": 0.03, "m
             # texture's bilinear weights differ from SwiftShader's by ~6e-4
             # (measured), which moves the reflection direction
             "tex_sdf_metal": 0.05, "cube_sdf_metal": 0.08}
+# mean radiance vs the fixture (default 5e-3); cube_sdf_metal: SwiftShader's
+# image of this SDF-only scene depends on the order of its SDF statements
+# (tests/test_oracle_golden.py MEAN_TOL)
+MEAN_TOL = {"cube_sdf_metal": 0.025}
 
 
 def cfg_by_name(cfgs, name):
@@ -88,7 +92,7 @@ def test_gpu_matches_reference_fixture(name, cfgs, gpu_required):
     assert not np.isnan(got).any()
     m = ~nan
     g, s = gold[..., :3][m], got[..., :3][m]
-    assert abs(s.mean() - g.mean()) <= 5e-3 * max(1.0, abs(g.mean()))
+    assert abs(s.mean() - g.mean()) <= MEAN_TOL.get(name, 5e-3) * max(1.0, abs(g.mean()))
 
 
 @pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo"])

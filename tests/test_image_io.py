@@ -71,3 +71,36 @@ def test_pfm_write(tmp_path):
     assert raw.startswith(head)
     data = np.frombuffer(raw[len(head):], "<f4").reshape(6, 9, 3)
     assert np.array_equal(data, (acc[..., :3] * np.float32(0.25)).astype(np.float32))
+
+
+def test_jpeg_decode_matches_libjpeg():
+    """Baseline JPEG (the reference's cubemap format) decodes within 3 levels of
+    libjpeg (Pillow), for 4:4:4, 4:2:2 and 4:2:0 chroma and a restart interval."""
+    PIL = pytest.importorskip("PIL.Image")
+    import io
+    y, x = np.mgrid[0:70, 0:93]
+    img = np.stack([(x * 2.7) % 256, (y * 3.1) % 256, ((x + y) * 1.3) % 256], -1)
+    img = (img * 0.8 + (np.arange(70 * 93 * 3).reshape(70, 93, 3) * 7919 % 50)).clip(0, 255).astype(np.uint8)
+    for sub, extra in [(0, {}), (1, {}), (2, {}), (2, {"restart_marker_blocks": 3})]:
+        b = io.BytesIO()
+        try:
+            PIL.fromarray(img).save(b, "JPEG", quality=90, subsampling=sub, **extra)
+        except TypeError:
+            continue
+        data = b.getvalue()
+        ref = np.asarray(PIL.open(io.BytesIO(data)).convert("RGB")).astype(int)
+        got = rt0.jpeg_decode(data)
+        assert got.shape == (70, 93, 4) and (got[..., 3] == 255).all()
+        assert np.abs(got[..., :3].astype(int) - ref).max() <= 3, sub
+
+
+def test_jpeg_rejects_non_baseline(tmp_path):
+    PIL = pytest.importorskip("PIL.Image")
+    import io
+    b = io.BytesIO()
+    PIL.fromarray(np.zeros((16, 16, 3), np.uint8)).save(b, "JPEG", progressive=True)
+    with pytest.raises(rt0.Rt0Error) as e:
+        rt0.jpeg_decode(b.getvalue())
+    assert e.value.code == -3
+    with pytest.raises(rt0.Rt0Error):
+        rt0.jpeg_decode(b"\x00\x01garbage")
