@@ -59,6 +59,9 @@ typedef struct rt0_config {
 /* Mesh record = the reference's `Mesh` struct (raytracer.glsl:239-244) with its
  * `Material` (157-163) flattened.  type: 0 SPHERE 1 PLANE 2 BOX 3 SDF.
  * mat_type: 0 LIGHT 1 DIR_LIGHT 2 DIFF 3 SPEC 4 REFR_FRESNEL 5 REFR_SCHLICK 6 COAT.
+ * type 5 TRIANGLE (raytracer.glsl:236): an instance of triangle model k
+ *   (k-th TRIANGLE entry; geometry from rt0_set_model) translated by pos and
+ *   scaled by joker.x (0 = skipped, like every mesh with joker.x == 0).
  * tex_type: the material's `Texture.t` (raytracer.glsl:112-121): -1 NULL_TEX,
  *   0..3 TEXTURE0..3 (image units, rt0_set_texture), 4 VORONOI, 5 GRADIENT_NOISE,
  *   6 VALUE_NOISE, 7 CHECK, 8 RIPPLE, 9 METAL (4/6/9 read the noise texture).
@@ -105,16 +108,34 @@ int rt0_get_config(const rt0_ctx *ctx, rt0_config *out);
  * or index.html:657-676) and the sdf_meshes statements (index.html:702-717). */
 int rt0_set_scene_glsl(rt0_ctx *ctx, const char *scene_text, const char *const *sdf_meshes, int n_sdf);
 /* Same from already-flattened records; meshes[0..n_meshes) are Euclidean,
- * meshes[n_meshes..n_meshes+n_sdfs) SDFs; light_index as in the GLSL scene. */
-int rt0_set_scene(rt0_ctx *ctx, const rt0_mesh *meshes, int n_meshes, int n_sdfs, const int32_t *light_index,
-                  int n_lights);
+ * then n_sdfs SDFs, then n_models TRIANGLE instances (the reference's
+ * meshes[NUM_MESHES + NUM_SDFS + NUM_MODELS], index.html:669); light_index as
+ * in the GLSL scene. */
+int rt0_set_scene(rt0_ctx *ctx, const rt0_mesh *meshes, int n_meshes, int n_sdfs, int n_models,
+                  const int32_t *light_index, int n_lights);
 /* Pure parser (no device needed): scene text + sdf statements -> records.
  * Fails with RT0_E_ARG if max_meshes / max_lights are too small. */
 int rt0_parse_scene_glsl(const char *scene_text, const char *const *sdf_meshes, int n_sdf, rt0_mesh *meshes,
-                         int max_meshes, int *n_meshes, int *n_sdfs, int32_t *light_index, int max_lights,
-                         int *n_lights);
-int rt0_get_scene(const rt0_ctx *ctx, rt0_mesh *meshes, int max_meshes, int *n_meshes, int *n_sdfs,
+                         int max_meshes, int *n_meshes, int *n_sdfs, int *n_models, int32_t *light_index,
+                         int max_lights, int *n_lights);
+int rt0_get_scene(const rt0_ctx *ctx, rt0_mesh *meshes, int max_meshes, int *n_meshes, int *n_sdfs, int *n_models,
                   int32_t *light_index, int max_lights, int *n_lights);
+
+/* Triangle model k for the k-th TRIANGLE scene entry (replaces the
+ * reference's unshipped mesh.js/bvh.js path; its iTriangle is the commented
+ * Moller-Trumbore of raytracer.glsl:864-892): positions = n_vertices x 3
+ * floats (object space), indices = n_triangles x 3 vertex indices.  Copied.
+ * The next render builds one LBVH over all instances in world space on the
+ * device (Morton codes + radix sort + Karras hierarchy + refit, rt0_bvh.hip);
+ * traversal is part of intersection() (after the quadrics, before the SDF
+ * march).  rt0_model_info builds now if needed and reports the triangle count
+ * and tree depth (RT0_E_UNSUPPORTED if deeper than the traversal stack). */
+int rt0_set_model(rt0_ctx *ctx, int model, const float *positions, int n_vertices, const int32_t *indices,
+                  int n_triangles);
+int rt0_model_info(rt0_ctx *ctx, int *n_triangles, int *bvh_depth);
+/* Wavefront OBJ (v / f records; polygons fan-triangulated; v/vt/vn and
+ * negative indices accepted) -> malloc'd positions / indices (rt0_free). */
+int rt0_obj_read(const char *path, float **positions, int *n_vertices, int32_t **indices, int *n_triangles);
 
 /* Asset textures, replacing GlslViewport.loadTexture (index.js:699-728) for
  * the image textures opts.textures[0..3] (units u_tex0..3, index.js:276-296)

@@ -41,6 +41,8 @@ def lib():
         L.or_hash2.argtypes = [ctypes.c_float, ctypes.c_float, fp]
         L.or_set_texture.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_uint8)]
+        L.or_set_triangles.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int),
+                                       ctypes.c_int]
         L.or_set_cubemap.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))]
         L.or_pixel_seed.restype = ctypes.c_float
         L.or_pixel_seed.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_uint]
@@ -89,6 +91,15 @@ class Oracle:
         faces = cubemap_for(cfg)
         if faces is not None:
             self.set_cubemap(faces)
+
+    def set_triangles(self, v9, model):
+        """World-space triangles float32 [n, 9] and their owner model index
+        (bit 30 = back-face culling); brute-force closest hit."""
+        v = np.ascontiguousarray(v9, np.float32).reshape(-1, 9)
+        m = np.ascontiguousarray(model, np.int32).reshape(-1)
+        self._tris = (v, m)  # the C side keeps pointers
+        self._chk(lib().or_set_triangles(self.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                         m.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), v.shape[0]))
 
     def set_cubemap(self, faces):
         """u_cubemap: six uint8 [n, n, 3] faces, reference order -X -Y -Z +X +Y +Z."""

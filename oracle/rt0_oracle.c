@@ -186,6 +186,12 @@ typedef struct {
   /* asset textures (index.js:256-296): 0..3 u_tex0..3, 4 u_rnd_tex; RGBA8 */
   const unsigned char *tex_img[5];
   int tex_w[5], tex_h[5];
+  /* world-space triangles of the TRIANGLE models (9 floats each) and their
+   * owner model (bit 30: back-face culling); brute force, no BVH: the oracle
+   * for the product's LBVH closest hit */
+  const float *tri_v;
+  const int *tri_model;
+  int n_tris;
   /* u_cubemap: 6 RGB8 faces in the reference's order -X -Y -Z +X +Y +Z */
   const unsigned char *cube[6];
   int cube_size;
@@ -548,6 +554,25 @@ static v3 cube_sample(const Oracle *o, v3 d) {
   return V(r[0], r[1], r[2]);
 }
 
+/* iTriangle, the reference's commented-out Moller-Trumbore (raytracer.glsl:
+ * 864-892), evaluated as written (no FMA: -ffp-contract=off). */
+static int iTriangle(const float *v, int cull, v3 o, v3 d, float tmin, float *t) {
+  v3 v1 = V(v[0], v[1], v[2]), e0 = sub(V(v[3], v[4], v[5]), v1), e1 = sub(V(v[6], v[7], v[8]), v1);
+  v3 h = cross(d, e1);
+  float a = dot3(e0, h);
+  if (cull && a < EPSILON) return 0;
+  if (!cull && a > -EPSILON && a < EPSILON) return 0;
+  float f = 1.0f / a;
+  v3 s = sub(o, v1);
+  float u = f * dot3(s, h);
+  if (u < 0.0f || u > 1.0f) return 0;
+  v3 q = cross(s, e0);
+  float vv = f * dot3(d, q);
+  if (vv < 0.0f || u + vv > 1.0f) return 0;
+  *t = f * dot3(e1, q);
+  return *t > EPSILON && *t < tmin;
+}
+
 /* intersection(), raytracer.glsl:997-1082 (texture/uv parsing omitted: every
  * supported material has NULL_TEX, so hit.uv / hit.texel never reach the output). */
 static float intersection(Frag *F, v3 o, v3 d, Hit *hit) {
@@ -571,6 +596,18 @@ static float intersection(Frag *F, v3 o, v3 d, Hit *hit) {
       } else if (m->t == T_BOX) {
         if (iBox(m, o, d, tmin, &tt, &hit->n)) { tmin = tt; type = T_BOX; hit->index = i; }
       }
+    }
+  }
+  if (op->n_models > 0) { /* every triangle, lowest index wins ties (strict <) */
+    int best = -1;
+    for (int i = 0; i < op->n_tris; ++i)
+      if (iTriangle(op->tri_v + 9 * (size_t)i, (op->tri_model[i] >> 30) & 1, o, d, tmin, &tt)) { tmin = tt; best = i; }
+    if (best >= 0) {
+      const float *v = op->tri_v + 9 * (size_t)best;
+      v3 v1 = V(v[0], v[1], v[2]);
+      hit->n = normalize(cross(sub(V(v[3], v[4], v[5]), v1), sub(V(v[6], v[7], v[8]), v1)));
+      hit->index = op->n_meshes + op->n_sdfs + (op->tri_model[best] & 0x3fffffff);
+      type = T_TRIANGLE;
     }
   }
   if (op->n_sdfs > 0) {
@@ -1401,6 +1438,7 @@ int or_set_scene_lines(void *h, const char *text, const int *sdf_kinds, int n_ki
     else if (!strcmp(typ, "PLANE")) m->t = T_PLANE;
     else if (!strcmp(typ, "BOX")) m->t = T_BOX;
     else if (!strcmp(typ, "SDF")) m->t = T_SDF;
+    else if (!strcmp(typ, "TRIANGLE")) m->t = T_TRIANGLE;
     else { snprintf(o->err, sizeof o->err, "unsupported mesh type %s", typ); return -1; }
     float pos[3], jk[4];
     const char *q = p;
@@ -1412,16 +1450,20 @@ int or_set_scene_lines(void *h, const char *text, const int *sdf_kinds, int n_ki
   }
   /* the reference orders meshes as written; SDFs must follow the Euclidean
    * meshes for meshes[NUM_MESHES + i] to address them (index.html:702-717) */
-  int ne = 0, ns = 0;
+  int ne = 0, ns = 0, nm = 0;
   for (int i = 0; i < n; i++) {
-    if (types[i] == T_SDF) ns++;
-    else {
-      if (ns) { snprintf(o->err, sizeof o->err, "SDF meshes must follow Euclidean meshes"); return -1; }
+    if (types[i] == T_TRIANGLE) nm++;
+    else if (types[i] == T_SDF) {
+      if (nm) { snprintf(o->err, sizeof o->err, "TRIANGLE models must follow SDF meshes"); return -1; }
+      ns++;
+    } else {
+      if (ns || nm) { snprintf(o->err, sizeof o->err, "SDF meshes must follow Euclidean meshes"); return -1; }
       ne++;
     }
   }
   o->n_meshes = ne;
   o->n_sdfs = ns;
+  o->n_models = nm;
   o->n_total = n;
   memcpy(o->meshes, tmp, sizeof(Mesh) * n);
   for (int i = 0; i < ns; i++) o->sdf_kind[i] = (i < n_kinds) ? sdf_kinds[i] : 0;
@@ -1481,6 +1523,15 @@ int or_set_texture(void *h, int unit, int w, int hh, const unsigned char *rgba8)
   o->tex_img[unit] = rgba8;
   o->tex_w[unit] = w;
   o->tex_h[unit] = hh;
+  return 0;
+}
+/* world-space triangles (caller keeps the arrays alive); model ids may carry
+ * bit 30 = back-face culling */
+int or_set_triangles(void *h, const float *v9, const int *model, int n) {
+  Oracle *o = (Oracle *)h;
+  o->tri_v = v9;
+  o->tri_model = model;
+  o->n_tris = n;
   return 0;
 }
 /* load_cubemap (index.js:298-331): 6 RGB8 faces, reference order; NULL unbinds */

@@ -50,8 +50,32 @@ struct TexRec {
 // Asset texture units (index.js:149-163): 0..3 = u_tex0..3, 4 = u_rnd_tex.
 #define RT0_TEX_UNITS 5
 
+// Triangle models (TRIANGLE scene entries, raytracer.glsl:236; the
+// reference's commented-out iTriangle, 864-892).  One LBVH over the triangles
+// of all models, built on the device (rt0_bvh.hip) in world space:
+//   TriDev  48 B: v0 + model index, e0 = v1 - v0, e1 = v2 - v0 (the three
+//           Moller-Trumbore operands), stored in Morton (leaf) order;
+//   BvhNode 64 B: both children's boxes + child links (>= 0 internal node,
+//           < 0 leaf ~triangle), so one node fetch tests two boxes.
+struct TriDev {
+  float v0x, v0y, v0z;
+  int32_t model;  // owner model k (scene entry n_meshes + n_sdfs + k)
+  float e0x, e0y, e0z;
+  int32_t cull;   // Material.opts[3]: back-face culling (iTriangle, 869-872)
+  float e1x, e1y, e1z, pad;
+};
+#define RT0_TRI_CULL_BIT (1 << 30)  // set in the build's model ids for culling models
+struct BvhNode {
+  float lx0, ly0, lz0, rx0;
+  float lx1, ly1, lz1, ry0;
+  float rz0, rx1, ry1, rz1;
+  int32_t left, right, pad0, pad1;
+};
+#define RT0_BVH_STACK 48  // traversal stack entries per lane (LDS); the build checks the depth
+
 struct SceneDev {
   int32_t n_meshes, n_sdfs, n_lights, n_total;
+  int32_t n_models;  // TRIANGLE entries: geom/mat[n_meshes + n_sdfs + k]
   int32_t any_tex;  // some mesh has tex.type != NULL (texel code runs at all)
   GeomRec geom[RT0_MAX_MESH];
   MatRec mat[RT0_MAX_MESH];
@@ -113,4 +137,8 @@ struct LaunchParams {
   // order +X -X +Y -Y +Z -Z, row 0 = t 0; null = unbound.
   const uint32_t *cube;
   int32_t cube_size;
+  // Triangle models: LBVH nodes (root 0) and triangles in leaf order; n_tris 0 = none.
+  const BvhNode *bvh;
+  const TriDev *tris;
+  int32_t n_tris;
 };

@@ -24,6 +24,8 @@ extern "C" hipError_t rt0_launch_pass(int variant, const LaunchParams *p, dim3 g
 extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, float cont, int mode,
                                          hipStream_t stream);
 extern "C" hipError_t rt0_launch_sum(const LaunchParams *p, dim3 grid, hipStream_t stream);
+extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_model, float3 lo, float3 hi,
+                                    BvhNode *d_nodes, TriDev *d_tris, int *depth_out, hipStream_t s);
 
 // A pass launch with fewer than kTargetWaves waves (16 per SIMD of the 1024
 // SIMDs) is frame-chunked up to kChunkWaves (measured on one 1/2/4/8-way band
@@ -41,8 +43,19 @@ struct rt0_ctx {
   rt0_config cfg{};
   bool has_scene = false;
   std::vector<rt0_mesh> meshes;
-  int n_meshes = 0, n_sdfs = 0;
+  int n_meshes = 0, n_sdfs = 0, n_models = 0;
   std::vector<int32_t> lights;
+  // triangle models (rt0_set_model), object space; instanced by the scene's
+  // TRIANGLE entries (pos = translation, joker.x = scale) into one world-space LBVH
+  struct Model {
+    std::vector<float> pos;
+    std::vector<int32_t> tri;
+  };
+  std::vector<Model> models;
+  bool bvh_dirty = false;
+  BvhNode *d_bvh = nullptr;
+  TriDev *d_tris = nullptr;
+  int n_tris = 0, bvh_depth = 0;
   SceneDev *d_scene = nullptr;
   float cam_pos[3] = {0.f, 0.f, 2.8f}, cam_look[3] = {0.f, 0.f, -1.f}, cam_params[3] = {50.f, 0.f, 3.5f};
   float4 *d_accum = nullptr;
@@ -158,6 +171,8 @@ void rt0_destroy(rt0_ctx *c) {
   for (auto &t : c->d_tex)
     if (t) (void)hipFree(t);
   if (c->d_cube) (void)hipFree(c->d_cube);
+  if (c->d_bvh) (void)hipFree(c->d_bvh);
+  if (c->d_tris) (void)hipFree(c->d_tris);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -187,122 +202,85 @@ int rt0_get_config(const rt0_ctx *c, rt0_config *out) {
 }
 
 static int upload_scene(rt0_ctx *c) {
-  SceneDev s;
-  memset(&s, 0, sizeof s);
-  s.n_meshes = c->n_meshes;
-  s.n_sdfs = c->n_sdfs;
-  s.n_lights = (int)c->lights.size();
-  s.n_total = c->n_meshes + c->n_sdfs;
-  for (int i = 0; i < s.n_total; i++) {
-    const rt0_mesh &m = c->meshes[i];
-    GeomRec &g = s.geom[i];
-    g.px = m.pos[0];
-    g.py = m.pos[1];
-    g.pz = m.pos[2];
-    g.j0 = m.joker[0];
-    g.j1 = m.joker[1];
-    g.j2 = m.joker[2];
-    g.type = m.type;
-    g.d0 = m.type == 0 ? m.joker[0] * m.joker[0] : m.type == 1 ? -m.joker[0] : m.joker[0] * 0.5f;
-    s.j3[i] = m.joker[3];
-    s.sdf_kind[i] = m.sdf_kind;
-    MatRec &r = s.mat[i];
-    r.cr = m.c[0];
-    r.cg = m.c[1];
-    r.cb = m.c[2];
-    r.er = m.e[0];
-    r.eg = m.e[1];
-    r.eb = m.e[2];
-    r.nt = m.nt;
-    r.type = m.mat_type;
-    TexRec &t = s.tex[i];
-    t.type = m.tex_type;
-    t.cmr = m.tex_c_mask[0];
-    t.cmg = m.tex_c_mask[1];
-    t.cmb = m.tex_c_mask[2];
-    t.emr = m.tex_e_mask[0];
-    t.emg = m.tex_e_mask[1];
-    t.emb = m.tex_e_mask[2];
-    t.opts = m.mat_opts;
-    t.p0 = m.tex_params[0];
-    t.p1 = m.tex_params[1];
-    t.p2 = m.tex_params[2];
-    t.p3 = m.tex_params[3];
-    if (m.tex_type != -1) s.any_tex = 1;
-  }
-  for (int i = 0; i < s.n_lights; i++) s.light_index[i] = c->lights[i];
+  SceneDev s = rt0h::make_scene_dev(c->meshes.data(), c->n_meshes, c->n_sdfs, c->n_models, c->lights.data(),
+                                    (int)c->lights.size());
   HIPCHK(c, hipSetDevice(c->device));
   c->host_scene = s;
   HIPCHK(c, hipMemcpyAsync(c->d_scene, &s, sizeof s, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->has_scene = true;
+  c->bvh_dirty = true;  // the TRIANGLE entries' transforms / materials may have changed
   return RT0_OK;
 }
 
-static int validate_and_store(rt0_ctx *c, const rt0_mesh *m, int ne, int ns, const int32_t *li, int nl) {
-  if (ne < 0 || ns < 0 || nl < 0) return fail(c, RT0_E_ARG, "negative count");
-  if (ne + ns > RT0_MAX_MESH) return fail(c, RT0_E_UNSUPPORTED, "too many meshes");
+static int validate_and_store(rt0_ctx *c, const rt0_mesh *m, int ne, int ns, int nm, const int32_t *li, int nl) {
+  if (ne < 0 || ns < 0 || nm < 0 || nl < 0) return fail(c, RT0_E_ARG, "negative count");
+  if (ne + ns + nm > RT0_MAX_MESH) return fail(c, RT0_E_UNSUPPORTED, "too many meshes");
   if (nl > RT0_MAX_LIGHTS) return fail(c, RT0_E_UNSUPPORTED, "too many lights");
-  if (ne + ns == 0) return fail(c, RT0_E_ARG, "empty scene");  // meshes[hit.index] needs meshes[0]
-  for (int i = 0; i < ne + ns; i++) {
+  if (ne + ns + nm == 0) return fail(c, RT0_E_ARG, "empty scene");  // meshes[hit.index] needs meshes[0]
+  for (int i = 0; i < ne + ns + nm; i++) {
     if (m[i].tex_type < -1 || m[i].tex_type > 9) return fail(c, RT0_E_ARG, "bad texture type");
-    bool sdf = m[i].type == 3;
-    if ((i < ne) == sdf) return fail(c, RT0_E_ARG, "meshes[0..n_meshes) must be Euclidean, the rest SDF");
-    if (!sdf && (m[i].type < 0 || m[i].type > 2)) return fail(c, RT0_E_UNSUPPORTED, "unsupported mesh type");
+    bool sdf = m[i].type == 3, tri = m[i].type == 5;
+    if (i >= ne + ns ? !tri : (i >= ne ? !sdf : (sdf || tri)))
+      return fail(c, RT0_E_ARG, "meshes must be n_meshes Euclidean, then n_sdfs SDF, then n_models TRIANGLE entries");
+    if (!sdf && !tri && (m[i].type < 0 || m[i].type > 2)) return fail(c, RT0_E_UNSUPPORTED, "unsupported mesh type");
     if (sdf && (m[i].sdf_kind < 0 || m[i].sdf_kind > 6)) return fail(c, RT0_E_ARG, "bad sdf_kind");
     if (m[i].mat_type < -1 || m[i].mat_type > 6) return fail(c, RT0_E_ARG, "bad material type");
   }
   for (int i = 0; i < nl; i++)
-    if (li[i] >= ne + ns) return fail(c, RT0_E_ARG, "light_index out of range");
-  c->meshes.assign(m, m + ne + ns);
+    if (li[i] >= ne + ns + nm) return fail(c, RT0_E_ARG, "light_index out of range");
+  c->meshes.assign(m, m + ne + ns + nm);
   c->n_meshes = ne;
   c->n_sdfs = ns;
+  c->n_models = nm;
   c->lights.assign(li, li + nl);
   return upload_scene(c);
 }
 
-int rt0_set_scene(rt0_ctx *c, const rt0_mesh *meshes, int n_meshes, int n_sdfs, const int32_t *light_index,
-                  int n_lights) {
-  if (!c || (!meshes && n_meshes + n_sdfs > 0) || (!light_index && n_lights > 0)) return RT0_E_ARG;
-  return validate_and_store(c, meshes, n_meshes, n_sdfs, light_index, n_lights);
+int rt0_set_scene(rt0_ctx *c, const rt0_mesh *meshes, int n_meshes, int n_sdfs, int n_models,
+                  const int32_t *light_index, int n_lights) {
+  if (!c || (!meshes && n_meshes + n_sdfs + n_models > 0) || (!light_index && n_lights > 0)) return RT0_E_ARG;
+  return validate_and_store(c, meshes, n_meshes, n_sdfs, n_models, light_index, n_lights);
 }
 
 int rt0_set_scene_glsl(rt0_ctx *c, const char *scene_text, const char *const *sdf_meshes, int n_sdf) {
   if (!c) return RT0_E_ARG;
   std::vector<rt0_mesh> m;
   std::vector<int32_t> l;
-  int ne = 0, ns = 0;
+  int ne = 0, ns = 0, nm = 0;
   std::string err;
-  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, l, err);
+  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, nm, l, err);
   if (rc != RT0_OK) return fail(c, rc, err);
-  return validate_and_store(c, m.data(), ne, ns, l.data(), (int)l.size());
+  return validate_and_store(c, m.data(), ne, ns, nm, l.data(), (int)l.size());
 }
 
 int rt0_parse_scene_glsl(const char *scene_text, const char *const *sdf_meshes, int n_sdf, rt0_mesh *meshes,
-                         int max_meshes, int *n_meshes, int *n_sdfs, int32_t *light_index, int max_lights,
-                         int *n_lights) {
+                         int max_meshes, int *n_meshes, int *n_sdfs, int *n_models, int32_t *light_index,
+                         int max_lights, int *n_lights) {
   std::vector<rt0_mesh> m;
   std::vector<int32_t> l;
-  int ne = 0, ns = 0;
+  int ne = 0, ns = 0, nm = 0;
   std::string err;
-  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, l, err);
+  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, nm, l, err);
   if (rc != RT0_OK) return rc;
   if ((int)m.size() > max_meshes || (int)l.size() > max_lights) return RT0_E_ARG;
   for (size_t i = 0; i < m.size(); i++) meshes[i] = m[i];
   for (size_t i = 0; i < l.size(); i++) light_index[i] = l[i];
   if (n_meshes) *n_meshes = ne;
   if (n_sdfs) *n_sdfs = ns;
+  if (n_models) *n_models = nm;
   if (n_lights) *n_lights = (int)l.size();
   return RT0_OK;
 }
 
-int rt0_get_scene(const rt0_ctx *c, rt0_mesh *meshes, int max_meshes, int *n_meshes, int *n_sdfs,
+int rt0_get_scene(const rt0_ctx *c, rt0_mesh *meshes, int max_meshes, int *n_meshes, int *n_sdfs, int *n_models,
                   int32_t *light_index, int max_lights, int *n_lights) {
   if (!c) return RT0_E_ARG;
   if (!c->has_scene) return RT0_E_STATE;
-  int n = c->n_meshes + c->n_sdfs;
+  int n = c->n_meshes + c->n_sdfs + c->n_models;
   if (n_meshes) *n_meshes = c->n_meshes;
   if (n_sdfs) *n_sdfs = c->n_sdfs;
+  if (n_models) *n_models = c->n_models;
   if (n_lights) *n_lights = (int)c->lights.size();
   if (meshes)
     for (int i = 0; i < n && i < max_meshes; i++) meshes[i] = c->meshes[i];
@@ -357,6 +335,86 @@ int rt0_set_cubemap(rt0_ctx *c, int size, const uint8_t *const faces[6]) {
   HIPCHK(c, hipMemcpyAsync(c->d_cube, host.data(), host.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->cube_size = size;
+  return RT0_OK;
+}
+
+int rt0_set_model(rt0_ctx *c, int model, const float *positions, int n_vertices, const int32_t *indices,
+                  int n_triangles) {
+  if (!c || model < 0 || model >= RT0_MAX_MESH || n_vertices < 0 || n_triangles < 0) return RT0_E_ARG;
+  if ((n_vertices && !positions) || (n_triangles && !indices)) return RT0_E_ARG;
+  for (long k = 0; k < 3L * n_triangles; k++)
+    if (indices[k] < 0 || indices[k] >= n_vertices) return fail(c, RT0_E_ARG, "triangle index out of range");
+  if ((int)c->models.size() <= model) c->models.resize(model + 1);
+  c->models[model].pos.assign(positions, positions + 3L * n_vertices);
+  c->models[model].tri.assign(indices, indices + 3L * n_triangles);
+  c->bvh_dirty = true;
+  return RT0_OK;
+}
+
+// World-space triangles of every TRIANGLE entry (instance k uses model k) ->
+// device LBVH (rt0_bvh.hip).  Runs at the first render after a scene/model
+// change.
+static int build_bvh(rt0_ctx *c) {
+  c->bvh_dirty = false;
+  std::vector<float> v;
+  std::vector<int32_t> owner;
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int k = 0; k < c->n_models; k++) {
+    const rt0_mesh &m = c->meshes[c->n_meshes + c->n_sdfs + k];
+    if (m.joker[0] == 0.0f || k >= (int)c->models.size()) continue;  // skipped like intersection()'s joker.x == 0
+    const auto &M = c->models[k];
+    const int32_t tag = k | ((m.mat_opts & 8u) ? RT0_TRI_CULL_BIT : 0);
+    for (size_t t = 0; t + 2 < M.tri.size(); t += 3) {
+      for (int j = 0; j < 3; j++) {
+        const float *p = &M.pos[3 * (size_t)M.tri[t + j]];
+        for (int a = 0; a < 3; a++) {
+          const float w = m.pos[a] + m.joker[0] * p[a];
+          v.push_back(w);
+          lo[a] = std::min(lo[a], w);
+          hi[a] = std::max(hi[a], w);
+        }
+      }
+      owner.push_back(tag);
+    }
+  }
+  const int n = (int)owner.size();
+  if (c->d_bvh) HIPCHK(c, hipFree(c->d_bvh));
+  if (c->d_tris) HIPCHK(c, hipFree(c->d_tris));
+  c->d_bvh = nullptr;
+  c->d_tris = nullptr;
+  c->n_tris = 0;
+  c->bvh_depth = 0;
+  if (n == 0) return RT0_OK;
+  float *d_v = nullptr;
+  int32_t *d_owner = nullptr;
+  HIPCHK(c, hipMalloc(&d_v, v.size() * sizeof(float)));
+  HIPCHK(c, hipMalloc(&d_owner, owner.size() * sizeof(int32_t)));
+  HIPCHK(c, hipMalloc(&c->d_bvh, (size_t)std::max(1, n - 1) * sizeof(BvhNode)));
+  HIPCHK(c, hipMalloc(&c->d_tris, (size_t)n * sizeof(TriDev)));
+  HIPCHK(c, hipMemcpyAsync(d_v, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_owner, owner.data(), owner.size() * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  int depth = 0;
+  hipError_t e = rt0_bvh_build(n, d_v, d_owner, make_float3(lo[0], lo[1], lo[2]), make_float3(hi[0], hi[1], hi[2]),
+                               c->d_bvh, c->d_tris, &depth, c->stream);
+  (void)hipFree(d_v);
+  (void)hipFree(d_owner);
+  if (e != hipSuccess) return fail(c, RT0_E_HIP, std::string("BVH build: ") + hipGetErrorString(e));
+  if (depth >= RT0_BVH_STACK)
+    return fail(c, RT0_E_UNSUPPORTED, "BVH depth " + std::to_string(depth) + " exceeds the traversal stack");
+  c->n_tris = n;
+  c->bvh_depth = depth;
+  return RT0_OK;
+}
+
+int rt0_model_info(rt0_ctx *c, int *n_triangles, int *bvh_depth) {
+  if (!c) return RT0_E_ARG;
+  if (c->has_scene && c->bvh_dirty) {
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = build_bvh(c);
+    if (rc != RT0_OK) return rc;
+  }
+  if (n_triangles) *n_triangles = c->n_tris;
+  if (bvh_depth) *bvh_depth = c->bvh_depth;
   return RT0_OK;
 }
 
@@ -442,6 +500,9 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   }
   p.cube = c->d_cube;
   p.cube_size = c->cube_size;
+  p.bvh = c->d_bvh;
+  p.tris = c->d_tris;
+  p.n_tris = c->n_tris;
   p.accum = c->acc();
   p.counters = c->d_counters;
   if (c->n_shards > 1) {  // one contiguous block per shard (checked for ReSTIR in render_impl)
@@ -478,6 +539,10 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
   if (restir && c->n_shards > 1 && n > 1)
     return fail(c, RT0_E_ARG, "sharded ReSTIR renders one pass per call (halo exchange between passes)");
   HIPCHK(c, hipSetDevice(c->device));
+  if (c->bvh_dirty) {
+    int rc = build_bvh(c);
+    if (rc != RT0_OK) return rc;
+  }
   LaunchParams p;
   fill_params(c, p);
   if (p.n_band_rows == 0 || n == 0) {

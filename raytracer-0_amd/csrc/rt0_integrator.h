@@ -26,6 +26,7 @@ namespace rt0 {
 
 constexpr float EPSILON = 0.001f;
 constexpr float INF_T = 1e4f;
+constexpr float F_INF = __builtin_huge_valf();  // (hipRTC has no INFINITY macro)
 constexpr float PI_F = 3.14159265f;
 constexpr float ONE_OVER_PI = 0.31830989f;
 constexpr float TWO_PI = 6.28318531f;
@@ -34,7 +35,7 @@ constexpr float VOL_SIGMA_T = 0.15f;
 constexpr float VOL_SIGMA_S = 0.13f;
 constexpr float VOL_G = 0.5f;
 
-enum { T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_SDF = 3 };
+enum { T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_SDF = 3, T_TRIANGLE = 5 };
 enum { M_LIGHT = 0, M_DIR_LIGHT = 1, M_DIFF = 2, M_SPEC = 3, M_REFR_FRESNEL = 4, M_REFR_SCHLICK = 5, M_COAT = 6 };
 
 // ------------------------------------------------------------------ math
@@ -139,9 +140,11 @@ DEV void hash2(float sx, float sy, float &ox, float &oy) {
 struct DynScene {
   static constexpr bool kStatic = false;
   static constexpr int kMeshes = 0, kSdfs = 0, kLights = 0;
+  static constexpr bool kMayHaveModels = true;  // runtime check of n_models()
   const SceneDev *__restrict__ S;
   DEV int n_meshes() const { return S->n_meshes; }
   DEV int n_sdfs() const { return S->n_sdfs; }
+  DEV int n_models() const { return S->n_models; }
   DEV int n_lights() const { return S->n_lights; }
   DEV GeomRec geom(int i) const { return S->geom[i]; }
   DEV MatRec mat(int i) const { return S->mat[i]; }
@@ -267,6 +270,88 @@ DEV int axis_of(v3 n) {
   return -1;
 }
 
+
+// --------------------------------------------------- triangles + LBVH
+// iTriangle (the reference's commented-out Moller-Trumbore, raytracer.glsl:
+// 864-892) over the device-built LBVH of all TRIANGLE models (rt0_bvh.hip).
+// Same EPSILON tests as the reference: |a| < EPSILON rejects (a < EPSILON
+// with back-face culling, opts[3]), t must lie in (EPSILON, tmin).
+DEV bool tri_test(const TriDev &T, v3 o, v3 d, float tmin, float &t) {
+  const v3 e0 = mk(T.e0x, T.e0y, T.e0z), e1 = mk(T.e1x, T.e1y, T.e1z);
+  const v3 h = mk(d.y * e1.z - d.z * e1.y, d.z * e1.x - d.x * e1.z, d.x * e1.y - d.y * e1.x);
+  const float a = dot(e0, h);
+  if (T.cull ? a < EPSILON : (a > -EPSILON && a < EPSILON)) return false;
+  const float f = 1.0f / a;
+  const v3 s = o - mk(T.v0x, T.v0y, T.v0z);
+  const float u = f * dot(s, h);
+  if (u < 0.0f || u > 1.0f) return false;
+  const v3 q = mk(s.y * e0.z - s.z * e0.y, s.z * e0.x - s.x * e0.z, s.x * e0.y - s.y * e0.x);
+  const float v = f * dot(d, q);
+  if (v < 0.0f || u + v > 1.0f) return false;
+  t = f * dot(e1, q);
+  return t > EPSILON && t < tmin;
+}
+// slab test of a child box: entry distance, or +inf when the ray misses it or
+// enters beyond tmin
+DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, v3 o, v3 inv, float tmin) {
+  const float tx0 = (x0 - o.x) * inv.x, tx1 = (x1 - o.x) * inv.x;
+  const float ty0 = (y0 - o.y) * inv.y, ty1 = (y1 - o.y) * inv.y;
+  const float tz0 = (z0 - o.z) * inv.z, tz1 = (z1 - o.z) * inv.z;
+  const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  return (tn <= tf && tn < tmin) ? tn : F_INF;
+}
+// closest triangle hit along (o, d) before tmin: depth-first, nearer child
+// first, the far child on a per-lane stack in LDS (stride = block size so the
+// 64 lanes of a wave hit 64 different banks).  Returns the leaf-order triangle
+// index or -1; tmin is updated.
+DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
+  __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
+  int32_t *stk = stk_base + threadIdx.x;
+  int sp = 0, node = 0, best = -1;
+  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
+  const TriDev *__restrict__ tris = P.tris;
+  // a ray visits each of the n-1 nodes at most once: the cap only guarantees
+  // that every wave exits even on a corrupt tree
+  for (int guard = 2 * P.n_tris + 8; guard > 0; --guard) {
+    const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
+    const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+    float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
+    float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
+    int cl = lk.x, cr = lk.y;
+    if (tl != F_INF && cl < 0) {  // leaves are tested in place
+      float t;
+      if (tri_test(tris[~cl], o, d, tmin, t)) {
+        tmin = t;
+        best = ~cl;
+      }
+      tl = F_INF;
+    }
+    if (tr != F_INF && cr < 0) {
+      float t;
+      if (tri_test(tris[~cr], o, d, tmin, t)) {
+        tmin = t;
+        best = ~cr;
+      }
+      tr = F_INF;
+    }
+    if (tl != F_INF && tr != F_INF) {
+      const bool lfirst = tl <= tr;
+      stk[256 * sp] = lfirst ? cr : cl;
+      sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
+      node = lfirst ? cl : cr;
+    } else if (tl != F_INF) {
+      node = cl;
+    } else if (tr != F_INF) {
+      node = cr;
+    } else {
+      if (sp == 0) break;
+      node = stk[256 * --sp];
+    }
+  }
+  return best;
+}
+
 template <class Scene>
 struct Geometry {
   // map(), raytracer.glsl:700-712 + the #sdf_meshes statements of index.html:702-717
@@ -322,7 +407,8 @@ struct Geometry {
   // hit.index = 0 as HIT_MISS).  uv/texel parsing is omitted: only NULL_TEX
   // materials are accepted, so they never reach an output.
   template <bool SDF, class Cfg>
-  static DEV float intersect(const Scene &sc, const Cfg &C, v3 o, v3 d, Hit &hit, unsigned long long &nmap) {
+  static DEV float intersect(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, Hit &hit,
+                             unsigned long long &nmap) {
     hit.n = mk(0.f, 0.f, 0.f);
     hit.index = 0;
     int type = -1;
@@ -382,6 +468,18 @@ struct Geometry {
         hit.index = ok ? i : hit.index;
       }
     });
+    if constexpr (Scene::kMayHaveModels) {  // TRIANGLE models (after the quadrics, before the SDF march)
+      if (sc.n_models() > 0 && P.n_tris > 0) {
+        const int ti = bvh_closest(P, o, d, m, tmin);
+        if (ti >= 0) {
+          const TriDev T = P.tris[ti];
+          const v3 e0 = mk(T.e0x, T.e0y, T.e0z), e1 = mk(T.e1x, T.e1y, T.e1z);
+          hit.n = normalize(mk(e0.y * e1.z - e0.z * e1.y, e0.z * e1.x - e0.x * e1.z, e0.x * e1.y - e0.y * e1.x));
+          hit.index = sc.n_meshes() + sc.n_sdfs() + T.model;
+          type = T_TRIANGLE;
+        }
+      }
+    }
     if (type == T_BOX) {  // iBox's normal for the winning box, 853-856
       const GeomRec g = sc.geom(hit.index);
       v3 hp = (o + d * tmin) - mk(g.px, g.py, g.pz);
@@ -822,7 +920,7 @@ struct Integrator {
 
   DEV float isect(v3 o, v3 d, Hit &h) {
     if (COUNT) ++n_isect;
-    return G::template intersect<SDF>(sc, C, o, d, h, n_map);
+    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map);
   }
 
   // mix(mesh.mat.c, hit.texel.rgb, hit.texel.a) of a shadow ray's light hit

@@ -10,7 +10,10 @@
 namespace rt0h {
 int lookup_material(const std::string &name, rt0_mesh &m);
 int parse_scene_glsl(const char *text, const char *const *sdf, int n_sdf, std::vector<rt0_mesh> &meshes,
-                     int &n_euclid, int &n_sdfs, std::vector<int32_t> &lights, std::string &err);
+                     int &n_euclid, int &n_sdfs, int &n_models, std::vector<int32_t> &lights, std::string &err);
+// OBJ text -> positions (3 floats each) + triangles (3 indices each); polygons
+// are fan-triangulated, negative (relative) indices resolved
+int parse_obj(const char *text, size_t len, std::vector<float> &pos, std::vector<int32_t> &tris, std::string &err);
 void default_config(rt0_config &c);
 int parse_config(const char *const *defines, int nd, const char *const *constants, int nc, rt0_config &c,
                  std::string &err);

@@ -61,7 +61,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   o << "#define RT0_JIT 1\n"
        "using __hip_internal::int32_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
   o << strip_includes(rt0_jit_source_text);
-  const int nt = s.n_meshes + s.n_sdfs;
+  const int nt = s.n_total;
   o << "namespace rt0 {\n";
   o << "__constant__ const GeomRec kJitGeom[" << (nt > 0 ? nt : 1) << "] = {";
   for (int i = 0; i < nt; i++) {
@@ -93,10 +93,12 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   o << "struct JitScene {\n"
        "  static constexpr bool kStatic = true;\n"
        "  static constexpr int kMeshes = "
-    << s.n_meshes << ", kSdfs = " << s.n_sdfs << ", kLights = " << s.n_lights
+    << s.n_meshes << ", kSdfs = " << s.n_sdfs << ", kLights = " << s.n_lights << ", kModels = " << s.n_models
     << ";\n"
+       "  static constexpr bool kMayHaveModels = kModels > 0;\n"
        "  __device__ static constexpr int n_meshes() { return kMeshes; }\n"
        "  __device__ static constexpr int n_sdfs() { return kSdfs; }\n"
+       "  __device__ static constexpr int n_models() { return kModels; }\n"
        "  __device__ static constexpr int n_lights() { return kLights; }\n"
        "  __device__ static GeomRec geom(int i) { return kJitGeom[i]; }\n"
        "  __device__ static MatRec mat(int i) { return kJitMat[i]; }\n"
@@ -307,13 +309,14 @@ JitKey make_jit_key(const rt0_config &g, int n_sdfs) {
   return k;
 }
 
-SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, const int32_t *li, int nl) {
+SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, int nm, const int32_t *li, int nl) {
   SceneDev s;
   memset(&s, 0, sizeof s);
   s.n_meshes = ne;
   s.n_sdfs = ns;
+  s.n_models = nm;
   s.n_lights = nl;
-  s.n_total = ne + ns;
+  s.n_total = ne + ns + nm;
   for (int i = 0; i < s.n_total; i++) {
     GeomRec &g = s.geom[i];
     g.px = m[i].pos[0];
@@ -336,6 +339,20 @@ SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, const int32_t *li, in
     r.eb = m[i].e[2];
     r.nt = m[i].nt;
     r.type = m[i].mat_type;
+    TexRec &t = s.tex[i];
+    t.type = m[i].tex_type;
+    t.cmr = m[i].tex_c_mask[0];
+    t.cmg = m[i].tex_c_mask[1];
+    t.cmb = m[i].tex_c_mask[2];
+    t.emr = m[i].tex_e_mask[0];
+    t.emg = m[i].tex_e_mask[1];
+    t.emb = m[i].tex_e_mask[2];
+    t.opts = m[i].mat_opts;
+    t.p0 = m[i].tex_params[0];
+    t.p1 = m[i].tex_params[1];
+    t.p2 = m[i].tex_params[2];
+    t.p3 = m[i].tex_params[3];
+    if (m[i].tex_type != -1) s.any_tex = 1;
   }
   for (int i = 0; i < nl; i++) s.light_index[i] = li[i];
   return s;
@@ -350,18 +367,18 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
   if (!scene_text || !cfg) return RT0_E_ARG;
   std::vector<rt0_mesh> m;
   std::vector<int32_t> l;
-  int ne = 0, ns = 0;
+  int ne = 0, ns = 0, nm = 0;
   std::string e;
-  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, l, e);
+  int rc = rt0h::parse_scene_glsl(scene_text, sdf_meshes, n_sdf, m, ne, ns, nm, l, e);
   if (rc == RT0_OK) {
-    if (ne + ns > RT0_MAX_MESH || (int)l.size() > RT0_MAX_LIGHTS) {
+    if (ne + ns + nm > RT0_MAX_MESH || (int)l.size() > RT0_MAX_LIGHTS) {
       rc = RT0_E_UNSUPPORTED;
       e = "scene too large";
     }
   }
   std::vector<char> code;
   if (rc == RT0_OK) {
-    SceneDev s = rt0h::make_scene_dev(m.data(), ne, ns, l.data(), (int)l.size());
+    SceneDev s = rt0h::make_scene_dev(m.data(), ne, ns, nm, l.data(), (int)l.size());
     rc = rt0h::jit_compile(rt0h::jit_source(s, rt0h::make_jit_key(*cfg, ns)), code, e);
   }
   if (code_size) *code_size = code.size();

@@ -25,7 +25,7 @@ int jit_compile(const std::string &src, std::vector<char> &code, std::string &er
 uint32_t flags_from_config(const rt0_config &c);
 JitKey make_jit_key(const rt0_config &c, int n_sdfs);
 // flatten validated mesh records into the device scene layout
-SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, const int32_t *li, int nl);
+SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, int nm, const int32_t *li, int nl);
 // Compile (or fetch from the process cache) the kernel for this scene/config on
 // `device`; *fn receives a hipFunction_t.
 int jit_get(const SceneDev &s, const JitKey &k, int device, void **fn, std::string &err);

@@ -6,6 +6,7 @@
 // .sdf_meshes at `#sdf_meshes`, and the GLSL compiler does the rest.  This file
 // accepts exactly those strings (the grammar produced by index.js:11-85 and
 // index.html:610-717) and produces rt0_config / rt0_mesh records.
+#include <algorithm>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -170,7 +171,7 @@ int lookup_material(const std::string &name, rt0_mesh &m) {
 }
 
 int parse_scene_glsl(const char *text, const char *const *sdf, int n_sdf, std::vector<rt0_mesh> &meshes,
-                     int &n_euclid, int &n_sdfs, std::vector<int32_t> &lights, std::string &err) {
+                     int &n_euclid, int &n_sdfs, int &n_models, std::vector<int32_t> &lights, std::string &err) {
   if (!text) {
     err = "scene text is NULL";
     return RT0_E_ARG;
@@ -204,7 +205,8 @@ int parse_scene_glsl(const char *text, const char *const *sdf, int n_sdf, std::v
     else if (type == "PLANE") m.type = 1;
     else if (type == "BOX") m.type = 2;
     else if (type == "SDF") m.type = 3;
-    else if (type == "GRID_SDF" || type == "TRIANGLE") {
+    else if (type == "TRIANGLE") m.type = 5;  // a triangle model (rt0_set_model), index.html:648-649
+    else if (type == "GRID_SDF") {
       err = "mesh type " + type + " has no implementation in the reference integrator";
       return RT0_E_UNSUPPORTED;
     } else {
@@ -243,14 +245,23 @@ int parse_scene_glsl(const char *text, const char *const *sdf, int n_sdf, std::v
     if (*b == ',') b++;
   }
   // meshes[0..NUM_MESHES) Euclidean, then SDFs (index.html:702-717 addresses
-  // meshes[NUM_MESHES + i])
+  // meshes[NUM_MESHES + i]), then the models (meshes[NUM_MESHES + NUM_SDFS +
+  // NUM_MODELS], index.html:669)
   n_euclid = 0;
   n_sdfs = 0;
+  n_models = 0;
   for (const rt0_mesh &m : meshes) {
-    if (m.type == 3) n_sdfs++;
-    else {
-      if (n_sdfs) {
-        err = "SDF meshes must follow the Euclidean meshes";
+    if (m.type == 5) {
+      n_models++;
+    } else if (m.type == 3) {
+      if (n_models) {
+        err = "TRIANGLE models must follow the SDF meshes";
+        return RT0_E_ARG;
+      }
+      n_sdfs++;
+    } else {
+      if (n_sdfs || n_models) {
+        err = "SDF meshes and TRIANGLE models must follow the Euclidean meshes";
         return RT0_E_ARG;
       }
       n_euclid++;
@@ -402,3 +413,94 @@ int parse_config(const char *const *defines, int nd, const char *const *constant
 }
 
 }  // namespace rt0h
+
+// ---------------------------------------------------------------- OBJ models
+// The reference's triangle path loaded a Wavefront OBJ (models/Stanford/Happy
+// Buddha.obj, .gitignore) through its unshipped mesh.js.  Vertices (`v x y z`)
+// and faces (`f a b c ...`, each a `v`, `v/vt`, `v//vn` or `v/vt/vn` token,
+// 1-based or negative = relative); polygons are fan-triangulated; other
+// records are ignored.
+namespace rt0h {
+int parse_obj(const char *text, size_t len, std::vector<float> &pos, std::vector<int32_t> &tris, std::string &err) {
+  pos.clear();
+  tris.clear();
+  const char *p = text, *end = text + len;
+  long line = 0;
+  while (p < end) {
+    const char *eol = (const char *)memchr(p, '\n', (size_t)(end - p));
+    if (!eol) eol = end;
+    ++line;
+    std::string ln(p, (size_t)(eol - p));
+    p = eol + 1;
+    const char *q = ln.c_str();
+    while (*q == ' ' || *q == '\t') ++q;
+    if (q[0] == 'v' && (q[1] == ' ' || q[1] == '\t')) {
+      char *e;
+      float xyz[3];
+      const char *r = q + 2;
+      for (int k = 0; k < 3; ++k) {
+        xyz[k] = strtof(r, &e);
+        if (e == r) {
+          err = "OBJ line " + std::to_string(line) + ": bad vertex";
+          return RT0_E_ARG;
+        }
+        r = e;
+      }
+      pos.insert(pos.end(), xyz, xyz + 3);
+    } else if (q[0] == 'f' && (q[1] == ' ' || q[1] == '\t')) {
+      std::vector<int32_t> f;
+      const char *r = q + 2;
+      const long nv = (long)(pos.size() / 3);
+      for (;;) {
+        while (*r == ' ' || *r == '\t' || *r == '\r') ++r;
+        if (!*r) break;
+        char *e;
+        long v = strtol(r, &e, 10);
+        if (e == r) {
+          err = "OBJ line " + std::to_string(line) + ": bad face";
+          return RT0_E_ARG;
+        }
+        v = v < 0 ? nv + v : v - 1;
+        if (v < 0 || v >= nv) {
+          err = "OBJ line " + std::to_string(line) + ": face index out of range";
+          return RT0_E_ARG;
+        }
+        f.push_back((int32_t)v);
+        r = e;
+        while (*r && *r != ' ' && *r != '\t') ++r;  // skip /vt/vn
+      }
+      for (size_t k = 2; k < f.size(); ++k) {
+        tris.push_back(f[0]);
+        tris.push_back(f[k - 1]);
+        tris.push_back(f[k]);
+      }
+    }
+  }
+  return RT0_OK;
+}
+}  // namespace rt0h
+
+extern "C" int rt0_obj_read(const char *path, float **positions, int *n_vertices, int32_t **indices,
+                            int *n_triangles) {
+  if (!path || !positions || !n_vertices || !indices || !n_triangles) return RT0_E_ARG;
+  FILE *f = fopen(path, "rb");
+  if (!f) return RT0_E_ARG;
+  std::string text;
+  char buf[1 << 16];
+  size_t k;
+  while ((k = fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, k);
+  fclose(f);
+  std::vector<float> pos;
+  std::vector<int32_t> tri;
+  std::string err;
+  int rc = rt0h::parse_obj(text.data(), text.size(), pos, tri, err);
+  if (rc != RT0_OK) return rc;
+  *positions = (float *)malloc(std::max<size_t>(1, pos.size()) * sizeof(float));
+  *indices = (int32_t *)malloc(std::max<size_t>(1, tri.size()) * sizeof(int32_t));
+  if (!*positions || !*indices) return RT0_E_ARG;
+  memcpy(*positions, pos.data(), pos.size() * sizeof(float));
+  memcpy(*indices, tri.data(), tri.size() * sizeof(int32_t));
+  *n_vertices = (int)(pos.size() / 3);
+  *n_triangles = (int)(tri.size() / 3);
+  return RT0_OK;
+}

@@ -132,13 +132,14 @@ static napi_value ParseScene(napi_env env, napi_callback_info info) {
   auto sp = c_strs(s);
   std::vector<rt0_mesh> m(256);
   std::vector<int32_t> l(256);
-  int ne = 0, ns = 0, nl = 0;
-  int rc = rt0_parse_scene_glsl(scene.c_str(), sp.data(), (int)sp.size(), m.data(), 256, &ne, &ns, l.data(), 256, &nl);
+  int ne = 0, ns = 0, nm = 0, nl = 0;
+  int rc = rt0_parse_scene_glsl(scene.c_str(), sp.data(), (int)sp.size(), m.data(), 256, &ne, &ns, &nm, l.data(), 256,
+                                &nl);
   if (rc != RT0_OK) return throw_rt0(env, rc, "cannot parse scene");
   napi_value o, arr, li;
   napi_create_object(env, &o);
-  napi_create_array_with_length(env, ne + ns, &arr);
-  for (int i = 0; i < ne + ns; i++) {
+  napi_create_array_with_length(env, ne + ns + nm, &arr);
+  for (int i = 0; i < ne + ns + nm; i++) {
     napi_value e;
     napi_create_object(env, &e);
     set(env, e, "type", num(env, m[i].type));
@@ -158,6 +159,7 @@ static napi_value ParseScene(napi_env env, napi_callback_info info) {
   set(env, o, "meshes", arr);
   set(env, o, "nMeshes", num(env, ne));
   set(env, o, "nSdfs", num(env, ns));
+  set(env, o, "nModels", num(env, nm));
   set(env, o, "lightIndex", li);
   return o;
 }
@@ -351,6 +353,56 @@ static napi_value SetCubemap(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+// setModel(h, k, positions: Float32Array (3/vertex), indices: Int32Array (3/triangle))
+static napi_value SetModel(napi_env env, napi_callback_info info) {
+  napi_value argv[4];
+  if (!get_args(env, info, 4, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  int32_t k = 0;
+  napi_get_value_int32(env, argv[1], &k);
+  void *pd = nullptr, *id = nullptr;
+  size_t pl = 0, il = 0, off = 0;
+  napi_typedarray_type pt, it;
+  napi_value ab;
+  bool ta = false;
+  napi_is_typedarray(env, argv[2], &ta);
+  if (!ta) return throw_rt0(env, RT0_E_ARG, "positions must be a Float32Array");
+  NAPI_OK(env, napi_get_typedarray_info(env, argv[2], &pt, &pl, &pd, &ab, &off));
+  napi_is_typedarray(env, argv[3], &ta);
+  if (!ta) return throw_rt0(env, RT0_E_ARG, "indices must be an Int32Array");
+  NAPI_OK(env, napi_get_typedarray_info(env, argv[3], &it, &il, &id, &ab, &off));
+  if (pt != napi_float32_array || it != napi_int32_array || pl % 3 || il % 3)
+    return throw_rt0(env, RT0_E_ARG, "positions: Float32Array of xyz, indices: Int32Array of triangles");
+  RC_OR_THROW(rt0_set_model(c, k, (const float *)pd, (int)(pl / 3), (const int32_t *)id, (int)(il / 3)));
+  return nullptr;
+}
+
+// readObj(path) -> {positions: Float32Array, indices: Int32Array}
+static napi_value ReadObj(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return nullptr;
+  std::string path = get_string(env, argv[0]);
+  float *pos = nullptr;
+  int32_t *idx = nullptr;
+  int nv = 0, nt = 0;
+  int rc = rt0_obj_read(path.c_str(), &pos, &nv, &idx, &nt);
+  if (rc != RT0_OK) return throw_rt0(env, rc, ("cannot read OBJ " + path).c_str());
+  void *a = nullptr, *b = nullptr;
+  napi_value ab1, ab2, ta1, ta2, o;
+  napi_create_arraybuffer(env, (size_t)nv * 12, &a, &ab1);
+  napi_create_arraybuffer(env, (size_t)nt * 12, &b, &ab2);
+  memcpy(a, pos, (size_t)nv * 12);
+  memcpy(b, idx, (size_t)nt * 12);
+  rt0_free(pos);
+  rt0_free(idx);
+  napi_create_typedarray(env, napi_float32_array, (size_t)nv * 3, ab1, 0, &ta1);
+  napi_create_typedarray(env, napi_int32_array, (size_t)nt * 3, ab2, 0, &ta2);
+  napi_create_object(env, &o);
+  set(env, o, "positions", ta1);
+  set(env, o, "indices", ta2);
+  return o;
+}
+
 // readPng(path) / readImage(path) -> {width, height, data: Uint8Array (RGBA8,
 // first row = top)}; PNG or baseline JPEG
 static napi_value ReadPng(napi_env env, napi_callback_info info) {
@@ -420,6 +472,8 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"readPng", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readImage", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setCubemap", nullptr, SetCubemap, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setModel", nullptr, SetModel, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"readObj", nullptr, ReadObj, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
   return exports;

@@ -30,7 +30,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
-           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read"]
+           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read"]
 
 TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
@@ -82,10 +82,14 @@ def lib():
         "rt0_set_config": (c_int, [c_void_p, P(Config)]),
         "rt0_get_config": (c_int, [c_void_p, P(Config)]),
         "rt0_set_scene_glsl": (c_int, [c_void_p, ctypes.c_char_p, P(ctypes.c_char_p), c_int]),
-        "rt0_set_scene": (c_int, [c_void_p, P(Mesh), c_int, c_int, P(ctypes.c_int32), c_int]),
+        "rt0_set_scene": (c_int, [c_void_p, P(Mesh), c_int, c_int, c_int, P(ctypes.c_int32), c_int]),
         "rt0_parse_scene_glsl": (c_int, [ctypes.c_char_p, P(ctypes.c_char_p), c_int, P(Mesh), c_int, P(c_int),
-                                         P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
-        "rt0_get_scene": (c_int, [c_void_p, P(Mesh), c_int, P(c_int), P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
+                                         P(c_int), P(c_int), P(ctypes.c_int32), c_int, P(c_int)]),
+        "rt0_get_scene": (c_int, [c_void_p, P(Mesh), c_int, P(c_int), P(c_int), P(c_int), P(ctypes.c_int32), c_int,
+                                  P(c_int)]),
+        "rt0_set_model": (c_int, [c_void_p, c_int, fp, c_int, P(ctypes.c_int32), c_int]),
+        "rt0_model_info": (c_int, [c_void_p, P(c_int), P(c_int)]),
+        "rt0_obj_read": (c_int, [ctypes.c_char_p, P(fp), P(c_int), P(P(ctypes.c_int32)), P(c_int)]),
         "rt0_set_camera": (c_int, [c_void_p, fp, fp, fp]),
         "rt0_set_texture": (c_int, [c_void_p, c_int, c_int, c_int, P(ctypes.c_uint8)]),
         "rt0_set_cubemap": (c_int, [c_void_p, c_int, P(P(ctypes.c_uint8))]),
@@ -154,16 +158,17 @@ def parse_config(defines, constants):
 
 # ----------------------------------------------------------------- scene text
 def parse_scene(scene_text, sdf_meshes=()):
-    """Pure parse of GlslViewport.scene + .sdf_meshes -> (meshes, n_meshes, n_sdfs, light_index)."""
+    """Pure parse of GlslViewport.scene + .sdf_meshes -> (meshes, n_meshes, n_sdfs, light_index);
+    meshes also holds the TRIANGLE entries after the SDFs (len(meshes) - n_meshes - n_sdfs models)."""
     meshes = (Mesh * 128)()
     lights = (ctypes.c_int32 * 128)()
-    ne, ns, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    ne, ns, nm, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     sdf = list(sdf_meshes)
     rc = lib().rt0_parse_scene_glsl(scene_text.encode(), _strarr(sdf), len(sdf), meshes, 128, ctypes.byref(ne),
-                                    ctypes.byref(ns), lights, 128, ctypes.byref(nl))
+                                    ctypes.byref(ns), ctypes.byref(nm), lights, 128, ctypes.byref(nl))
     if rc != RT0_OK:
         raise Rt0Error(rc, "cannot parse scene")
-    return list(meshes[:ne.value + ns.value]), ne.value, ns.value, list(lights[:nl.value])
+    return list(meshes[:ne.value + ns.value + nm.value]), ne.value, ns.value, list(lights[:nl.value])
 
 
 def _check_io(rc, what):
@@ -190,6 +195,21 @@ def png_read(path):
         return np.ctypeslib.as_array(p, shape=(h.value, w.value, 4)).copy()
     finally:
         lib().rt0_free(p)
+
+
+def obj_read(path):
+    """Wavefront OBJ -> (positions float32 [nv, 3], triangles int32 [nt, 3])."""
+    pp, ip = ctypes.POINTER(ctypes.c_float)(), ctypes.POINTER(ctypes.c_int32)()
+    nv, nt = ctypes.c_int(), ctypes.c_int()
+    _check_io(lib().rt0_obj_read(str(path).encode(), ctypes.byref(pp), ctypes.byref(nv), ctypes.byref(ip),
+                                 ctypes.byref(nt)), "obj_read %s" % path)
+    try:
+        v = np.ctypeslib.as_array(pp, shape=(max(1, nv.value) * 3,))[:nv.value * 3].reshape(-1, 3).copy()
+        t = np.ctypeslib.as_array(ip, shape=(max(1, nt.value) * 3,))[:nt.value * 3].reshape(-1, 3).copy()
+        return v, t
+    finally:
+        lib().rt0_free(pp)
+        lib().rt0_free(ip)
 
 
 def jpeg_decode(data):
@@ -330,10 +350,24 @@ class Renderer:
     def get_scene(self):
         meshes = (Mesh * 128)()
         lights = (ctypes.c_int32 * 128)()
-        ne, ns, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        self._chk(lib().rt0_get_scene(self.h, meshes, 128, ctypes.byref(ne), ctypes.byref(ns), lights, 128,
-                                      ctypes.byref(nl)))
-        return list(meshes[:ne.value + ns.value]), ne.value, ns.value, list(lights[:nl.value])
+        ne, ns, nm, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._chk(lib().rt0_get_scene(self.h, meshes, 128, ctypes.byref(ne), ctypes.byref(ns), ctypes.byref(nm),
+                                      lights, 128, ctypes.byref(nl)))
+        return list(meshes[:ne.value + ns.value + nm.value]), ne.value, ns.value, list(lights[:nl.value])
+
+    def set_model(self, k, positions, triangles):
+        """Triangle model k of the k-th TRIANGLE entry: float [nv, 3] object-space
+        positions, int [nt, 3] vertex indices."""
+        v = np.ascontiguousarray(positions, np.float32).reshape(-1, 3)
+        t = np.ascontiguousarray(triangles, np.int32).reshape(-1, 3)
+        self._chk(lib().rt0_set_model(self.h, k, v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), v.shape[0],
+                                      t.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), t.shape[0]))
+
+    def model_info(self):
+        """(triangles, BVH depth); builds the LBVH now if the scene/models changed."""
+        n, d = ctypes.c_int(), ctypes.c_int()
+        self._chk(lib().rt0_model_info(self.h, ctypes.byref(n), ctypes.byref(d)))
+        return n.value, d.value
 
     def set_texture(self, unit, rgba8):
         """loadTexture (index.js:699-728): unit 0..3 = u_tex0..3, TEX_NOISE = u_rnd_tex.

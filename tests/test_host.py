@@ -99,9 +99,11 @@ def test_scene_parser_sdf_statements(cfgs):
 def test_scene_parser_errors():
     with pytest.raises(rt0.Rt0Error):
         rt0.parse_scene("Mesh(MAT_NOPE, PLANE, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);")
-    with pytest.raises(rt0.Rt0Error) as e:
-        rt0.parse_scene("Mesh(MAT_WHITE, TRIANGLE, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);")
+    with pytest.raises(rt0.Rt0Error) as e:  # GRID_SDF has no implementation in the reference integrator
+        rt0.parse_scene("Mesh(MAT_WHITE, GRID_SDF, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);")
     assert e.value.code == -3
+    # TRIANGLE entries are models (tests/test_models.py)
+    assert rt0.parse_scene("Mesh(MAT_WHITE, TRIANGLE, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);")[0][0].type == 5
     # SDF mesh without a #sdf_meshes statement
     with pytest.raises(rt0.Rt0Error):
         rt0.parse_scene("Mesh(MAT_WHITE, SDF, vec3(0.0), vec4(1.0)) light_index[1] = int[](-1);", [])

@@ -1,0 +1,183 @@
+"""TRIANGLE models + the device LBVH (BASELINE config 5).
+
+PARITY UNPINNED: the reference ships no triangle path -- its Moller-Trumbore
+`iTriangle` is commented out (raytracer.glsl:864-892) and the mesh.js/bvh.js it
+belonged to are git-ignored.  The oracle is the restatement of that
+`iTriangle` run over EVERY triangle (oracle/rt0_oracle.c, brute force): the
+GPU's LBVH traversal must find the same closest hit, so the rendered images
+agree within the usual per-pixel tolerance.
+
+CPU: scene grammar with TRIANGLE entries, OBJ reading, mesh generators, the
+oracle's brute-force path.  GPU: BVH build (counts, depth bound), render parity
+vs the brute-force oracle, JIT == AOT, rebuild on model/scene change.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import rt0
+from rt0 import meshes as M
+
+REL_TOL = 1e-3
+
+
+def cfg_by_name(cfgs, name):
+    return [c for c in cfgs["configs"] if c["name"] == name][0]
+
+
+def model_data(cfg):
+    """[(positions, triangles)] per TRIANGLE entry of a config."""
+    out = []
+    for m in cfg.get("models", []):
+        gen = {"icosphere": M.icosphere, "wavy_icosphere": M.wavy_icosphere}[m["kind"]]
+        out.append(gen(m["level"]))
+    return out
+
+
+def world_soup(cfg, cfgs):
+    """All instances' world triangles [n, 9] + owner model ids, as librt0 builds them."""
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    meshes, ne, ns, _ = rt0.parse_scene(scene, sdf)
+    inst = meshes[ne + ns:]
+    vs, owners = [], []
+    for k, ((v, t), m) in enumerate(zip(model_data(cfg), inst)):
+        if m.joker[0] == 0.0:
+            continue
+        w = M.world_triangles(v, t, list(m.pos), m.joker[0])
+        vs.append(w)
+        owners.append(np.full(len(w), k, np.int32))
+    return np.concatenate(vs), np.concatenate(owners)
+
+
+def oracle_for(cfg, cfgs, w, h):
+    o = O.Oracle(cfg, cfgs, width=w, height=h)
+    v, own = world_soup(cfg, cfgs)
+    o.set_triangles(v, own)
+    return o
+
+
+def pixel_match(got, ref):
+    return (np.abs(got - ref) <= REL_TOL * np.maximum(1.0, np.abs(ref))).all(-1)
+
+
+# ------------------------------------------------------------------- CPU
+
+def test_scene_grammar_accepts_triangle_entries(cfgs):
+    cfg = cfg_by_name(cfgs, "tri_models")
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    assert "NUM_MODELS = 2" in scene  # index.html:648-649, 667
+    meshes, ne, ns, lights = rt0.parse_scene(scene, sdf)
+    assert (ne, ns, len(meshes)) == (6, 0, 8)
+    assert [m.type for m in meshes[6:]] == [5, 5]
+    assert meshes[6].joker[0] == pytest.approx(0.5) and list(meshes[6].pos) == pytest.approx([0.45, -1.0, -1.7])
+    assert lights == [5]
+    bad = rt0.scene_from_lines(["MAT_WHITE, TRIANGLE, vec3(0.0), vec4(1.0)",
+                                "MAT_WHITE, SDF, vec3(0.0), vec4(1.0)"])[0]
+    with pytest.raises(rt0.Rt0Error):
+        rt0.parse_scene(bad, [rt0.sdf_statement(0, 0)])
+
+
+def test_obj_reader(tmp_path):
+    """v / f records, v/vt/vn tokens, negative indices, quads fan-triangulated."""
+    p = tmp_path / "quad.obj"
+    p.write_text("# comment\nv 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvt 0 0\nvn 0 0 1\n"
+                 "f 1/1/1 2/1/1 3/1/1 4/1/1\nf -4//1 -2//1 -1//1\ng ignored\n")
+    v, t = rt0.obj_read(p)
+    assert v.shape == (4, 3) and v[2].tolist() == [1.0, 1.0, 0.0]
+    assert t.tolist() == [[0, 1, 2], [0, 2, 3], [0, 2, 3]]
+    p.write_text("v 0 0 0\nf 1 2 3\n")
+    with pytest.raises(rt0.Rt0Error):
+        rt0.obj_read(p)
+
+
+def test_icosphere_generators():
+    for lvl in range(4):
+        v, t = M.icosphere(lvl)
+        assert t.shape == (20 * 4 ** lvl, 3) and t.max() < len(v)
+        assert np.allclose(np.linalg.norm(v, axis=1), 1.0, atol=1e-6)
+        a, b, c = v[t[:, 0]], v[t[:, 1]], v[t[:, 2]]
+        n = np.cross(b - a, c - a)
+        assert (np.einsum("ij,ij->i", n, a + b + c) > 0).all()  # counter-clockwise from outside
+    v, t = M.wavy_icosphere(3)
+    r = np.linalg.norm(v, axis=1)
+    assert r.min() < 0.97 and r.max() > 1.03
+
+
+def test_oracle_bruteforce_models_render(cfgs):
+    """The restatement sees the models: finite image that changes when the
+    models are scaled to 0 (skipped like any joker.x == 0 mesh)."""
+    cfg = cfg_by_name(cfgs, "tri_models")
+    a = oracle_for(cfg, cfgs, 32, 32).frame(1)[0]
+    assert np.isfinite(a).all()
+    cfg0 = dict(cfg, scene_lines=[l.replace("vec4(0.5)", "vec4(0.0)").replace("vec4(0.45)", "vec4(0.0)")
+                                  for l in cfg["scene_lines"]])
+    b = O.Oracle(cfg0, cfgs, width=32, height=32).frame(1)[0]
+    assert not pixel_match(a[..., :3], b[..., :3]).all()
+
+
+# ------------------------------------------------------------------- GPU
+
+def make(cfg, cfgs, w, h, jit=True):
+    r = rt0.Renderer(w, h)
+    r.set_jit(jit)
+    rt0.configure(r, cfg, cfgs)
+    for k, (v, t) in enumerate(model_data(cfg)):
+        r.set_model(k, v, t)
+    return r
+
+
+@pytest.mark.gpu
+def test_bvh_build_counts_and_depth(cfgs, gpu_required):
+    cfg = cfg_by_name(cfgs, "tri_models")
+    r = make(cfg, cfgs, 16, 16)
+    n, depth = r.model_info()
+    assert n == 1280 * 2 and 0 < depth < 48
+    # the BASELINE config-5 size: 81,920 triangles (and the displaced variant)
+    for gen in (M.icosphere, M.wavy_icosphere):
+        v, t = gen(6)
+        r.set_model(0, v, t)
+        r.set_model(1, v, t)
+        n, depth = r.model_info()
+        assert n == 2 * 81920 and depth < 48, depth
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [True, False])
+def test_models_match_bruteforce_oracle(cfgs, gpu_required, jit):
+    cfg = cfg_by_name(cfgs, "tri_models")
+    o = oracle_for(cfg, cfgs, 64, 64)
+    r = make(cfg, cfgs, 64, 64, jit)
+    for k in (1, 2):
+        ref = o.frame(k)[0]
+        r.clear()
+        r.render(k, 1)
+        got = r.read_accum()
+        ok = pixel_match(got[..., :3], ref[..., :3])
+        assert ok.mean() >= 0.98, (k, ok.mean())
+        assert abs(got[..., :3].mean() - ref[..., :3].mean()) <= 5e-3 * max(1.0, ref[..., :3].mean())
+
+
+@pytest.mark.gpu
+def test_model_changes_rebuild(cfgs, gpu_required):
+    cfg = cfg_by_name(cfgs, "tri_models")
+    r = make(cfg, cfgs, 48, 48)
+    r.render(1, 1)
+    a = r.read_accum()
+    v, t = M.icosphere(2)
+    r.set_model(0, v * 0.5, t)  # a smaller glass ball
+    r.clear()
+    r.render(1, 1)
+    b = r.read_accum()
+    assert not np.array_equal(a, b)
+    assert r.model_info()[0] == 320 + 1280
+    # scale 0 hides every instance: same image as the scene without models (up to FMA placement)
+    cfg0 = dict(cfg, scene_lines=cfg["scene_lines"][:6], models=[])
+    r0 = make(cfg0, cfgs, 48, 48)
+    r0.render(1, 1)
+    lines = [l.replace("vec4(0.5)", "vec4(0.0)").replace("vec4(0.45)", "vec4(0.0)") for l in cfg["scene_lines"]]
+    r2 = make(dict(cfg, scene_lines=lines), cfgs, 48, 48)
+    assert r2.model_info()[0] == 0
+    r2.render(1, 1)
+    assert pixel_match(r2.read_accum()[..., :3], r0.read_accum()[..., :3]).mean() >= 0.99
