@@ -53,7 +53,7 @@ typedef struct rt0_config {
   int32_t use_restir;          /* use_restir */
   int32_t light_path_length;   /* LIGHT_PATH_LENGTH (unused by the integrator) */
   int32_t restir_samples;      /* RESTIR_SAMPLES */
-  int32_t render_mode;         /* RENDER_MODE (0 = progressive; 1 unsupported) */
+  int32_t render_mode;         /* RENDER_MODE: 0 progressive sum, 1 animated (EMA + getAnimatedPosition) */
 } rt0_config;
 
 /* Mesh record = the reference's `Mesh` struct (raytracer.glsl:239-244) with its
@@ -165,11 +165,18 @@ int rt0_set_camera(rt0_ctx *ctx, const float pos[3], const float lookat[3], cons
 /* Replaces n_passes consecutive GlslViewport.render() calls (index.js:986-1105)
  * with u_frame = first_frame .. first_frame+n_passes-1: each pass adds one
  * sample per pixel to the accumulator (raytracer.glsl:2168) and, with ReSTIR,
- * rotates the reservoir swap chain (index.js:795-820).  Synchronous. */
+ * rotates the reservoir swap chain (index.js:795-820).  Synchronous.
+ * time_ms is u_time (index.js:1011), read only by RENDER_MODE 1: every pass of
+ * the call sees the scene at that time (getAnimatedPosition,
+ * raytracer.glsl:263-298) and the accumulator becomes the running average
+ * mix(prev, sample, 1/temporal_frames) (2159-2165). */
 int rt0_render(rt0_ctx *ctx, uint32_t first_frame, int n_passes, float time_ms);
 /* Asynchronous variant on the context's stream; rt0_sync() waits. */
 int rt0_render_async(rt0_ctx *ctx, uint32_t first_frame, int n_passes, float time_ms);
 int rt0_sync(rt0_ctx *ctx);
+/* u_temporalFrames (GlslViewport.temporalFrames, index.js:236; default 5):
+ * the RENDER_MODE 1 running-average length. */
+int rt0_set_temporal_frames(rt0_ctx *ctx, int n);
 
 /* Host copy of the accumulator (W*H*4 floats). */
 int rt0_read_accum(rt0_ctx *ctx, float *rgba_out);

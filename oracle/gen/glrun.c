@@ -279,6 +279,7 @@ int main(int argc, char **argv) {
   int w = 64, h = 64, frames = 4, single = 0, restir_out = 0;
   float cam[9] = {0, 0, 2.8f, 0, 0, -1, 50, 0, 3.5f};
   float time_ms = 0.0f;
+  float dtime_ms = 0.0f;
   const char *tex_file[6] = {0};
   int tex_w[6] = {0}, tex_h[6] = {0};
   const char *cube_file = NULL;
@@ -293,6 +294,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "--single")) single = 1;
     else if (!strcmp(argv[i], "--restir-out")) restir_out = 1;
     else if (!strcmp(argv[i], "--time")) time_ms = (float)atof(argv[++i]);
+    else if (!strcmp(argv[i], "--dtime")) dtime_ms = (float)atof(argv[++i]); /* u_time step per pass */
     else if (!strcmp(argv[i], "--tex")) { /* --tex UNIT(1..5) W H file.rgba8 */
       int u = atoi(argv[++i]);
       if (u < 1 || u > 5) die("--tex unit must be 1..5 (u_tex0..3, u_rnd_tex)");
@@ -394,7 +396,7 @@ int main(int argc, char **argv) {
   for (int pass = 1; pass <= frames; pass++) {
     p_glUseProgram(prog);
     if (frame_loc >= 0) p_glUniform1ui(frame_loc, (GLuint)pass);
-    if (time_loc >= 0) p_glUniform1f(time_loc, time_ms);
+    if (time_loc >= 0) p_glUniform1f(time_loc, time_ms + (float)(pass - 1) * dtime_ms);
     if (tf_loc >= 0) p_glUniform1i(tf_loc, temporal_frames);
     p_glActiveTexture(GL_TEXTURE0 + 0);
     p_glBindTexture(GL_TEXTURE_2D, single ? zero : back);

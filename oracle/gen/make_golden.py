@@ -79,6 +79,8 @@ def run_config(glrun, cfgs, cfg):
            "--single", "--out", prefix] + cam_args(cfg, cfgs)
     if restir:
         cmd.append("--restir-out")
+    if cfg.get("time_ms"):  # u_time of pass k = t0 + (k-1)*dt (RENDER_MODE 1 configs)
+        cmd += ["--time", repr(float(cfg["time_ms"][0])), "--dtime", repr(float(cfg["time_ms"][1]))]
     # asset textures (u_tex0..3 = GL units 1..4, u_rnd_tex = unit 5; index.js:149-163)
     sys.path.insert(0, os.path.dirname(HERE))
     from textures import cubemap_for, textures_for

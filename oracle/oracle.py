@@ -44,6 +44,7 @@ def lib():
         L.or_set_triangles.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int),
                                        ctypes.c_int]
         L.or_set_cubemap.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8))]
+        L.or_set_time.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_int]
         L.or_pixel_seed.restype = ctypes.c_float
         L.or_pixel_seed.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_uint]
         _lib = L
@@ -91,6 +92,10 @@ class Oracle:
         faces = cubemap_for(cfg)
         if faces is not None:
             self.set_cubemap(faces)
+
+    def set_time(self, time_ms, temporal_frames=5):
+        """u_time / u_temporalFrames (read by RENDER_MODE 1 only)."""
+        lib().or_set_time(self.h, float(time_ms), int(temporal_frames))
 
     def set_triangles(self, v9, model):
         """World-space triangles float32 [n, 9] and their owner model index
@@ -172,6 +177,12 @@ class Oracle:
         if counters is not None:
             counters += np.array(list(c), np.uint64)
         return acc
+
+
+def pass_time(cfg, k):
+    """u_time of pass k (1-based) of a RENDER_MODE 1 config: t0 + (k-1)*dt."""
+    t0, dt = cfg.get("time_ms") or (0.0, 0.0)
+    return float(t0) + float(k - 1) * float(dt)
 
 
 def hash_(x):

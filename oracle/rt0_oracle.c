@@ -179,6 +179,9 @@ typedef struct {
   int max_bounces, max_diff, max_spec, max_trans, max_scatter, marching_steps;
   float fudge;
   int sample_lights, use_mis, use_restir, restir_samples, render_mode;
+  /* uniforms u_time (ms) and u_temporalFrames, read by RENDER_MODE 1 only */
+  float time_ms;
+  int temporal_frames;
   /* 1 = model SwiftShader 4.1's masked-execution quirk (see radiance()) */
   int ghost;
   /* camera uniforms (index.js:421-423) */
@@ -331,13 +334,35 @@ static v3 calcNormal(Frag *F, v3 pos) {
 #define RAD 0.01745329f
 
 /* raytracer.glsl:812-815 */
+/* getAnimatedPosition, raytracer.glsl:263-298 (identity unless RENDER_MODE 1) */
+static v3 anim_pos(const Oracle *o, v3 base, int idx) {
+  if (o->render_mode != 1) return base;
+  v3 p = base;
+  float t = o->time_ms * 0.001f;
+  if (idx >= 6 && idx <= 14) {
+    float radius = 0.6f;
+    float speed = 1.0f + (float)(idx - 6) * 0.2f;
+    float phase = (float)(idx - 6) * 0.7f;
+    p.x = base.x + cosf(t * speed + phase) * radius * 0.3f;
+    p.z = base.z + sinf(t * speed + phase) * radius * 0.3f;
+    p.y = base.y + sinf(t * speed * 2.0f + phase) * 0.1f;
+  }
+  if (idx >= o->n_meshes && o->n_sdfs > 0) {
+    float angle = t * 0.5f;
+    float ca = cosf(angle), sa = sinf(angle);
+    v3 r = V(p.x * ca - p.z * sa, p.y, p.x * sa + p.z * ca);
+    r.y += sinf(t * 1.5f) * 0.05f;
+    return r;
+  }
+  return p;
+}
 static int iPlane(const Mesh *pl, v3 o, v3 d, float tmin, float *t) {
   *t = (-pl->joker[0] - dot3(pl->pos, o)) / dot3(pl->pos, d);
   return (*t > EPSILON) && (*t < tmin);
 }
 /* raytracer.glsl:818-833 */
-static int iSphere(const Mesh *s, v3 o, v3 d, float tmin, float *t) {
-  v3 oc = sub(o, s->pos);
+static int iSphere(const Oracle *op, const Mesh *s, v3 o, v3 d, float tmin, float *t, int idx) {
+  v3 oc = sub(o, anim_pos(op, s->pos, idx));
   float b = dot3(oc, d);
   float c = dot3(oc, oc) - s->joker[0] * s->joker[0];
   float disc = b * b - c;
@@ -590,7 +615,7 @@ static float intersection(Frag *F, v3 o, v3 d, Hit *hit) {
       const Mesh *m = &op->meshes[i];
       if (m->joker[0] == 0.0f) continue;
       if (m->t == T_SPHERE) {
-        if (iSphere(m, o, d, tmin, &tt)) { tmin = tt; type = T_SPHERE; hit->index = i; }
+        if (iSphere(op, m, o, d, tmin, &tt, i)) { tmin = tt; type = T_SPHERE; hit->index = i; }
       } else if (m->t == T_PLANE) {
         if (iPlane(m, o, d, tmin, &tt)) { tmin = tt; type = T_PLANE; hit->index = i; }
       } else if (m->t == T_BOX) {
@@ -619,7 +644,7 @@ static float intersection(Frag *F, v3 o, v3 d, Hit *hit) {
       /* cartesianToSpherical of the world position (467-471, 1057-1059) */
       float rho = sqrtf(hit->pos.x * hit->pos.x + hit->pos.y * hit->pos.y + hit->pos.z * hit->pos.z);
       hit->uv = (v2){asinf(hit->pos.y / rho) / PI_F, atan2f(hit->pos.z, hit->pos.x) / TWO_PI};
-      hit->n = normalize(sub(hit->pos, op->meshes[hit->index].pos));
+      hit->n = normalize(sub(hit->pos, anim_pos(op, op->meshes[hit->index].pos, hit->index)));
     } else if (type == T_PLANE) hit->n = normalize(op->meshes[hit->index].pos);
     if (hit->uv.x < 0.0f) { /* 1069-1076 */
       v3 nl = vabs(hit->n);
@@ -704,10 +729,11 @@ static v3 calcDirectLighting(Frag *F, const Mesh *light, v3 x, v3 nl, float seed
   const Oracle *o = F->o;
   Hit hit;
   v3 dl = V(0, 0, 0);
+  const int li = (int)(light - o->meshes); /* lightIndex (the light's scene entry) */
   F->n_nee++;
   if (light->mat.t == M_LIGHT) {
     if (light->t == T_SPHERE) {
-      v3 sw = sub(light->pos, x);
+      v3 sw = sub(anim_pos(o, light->pos, li), x);
       float r2 = light->joker[0] * light->joker[0];
       float d2 = dot3(sw, sw);
       float cos_a_max = sqrtf(1.0f - gclamp(r2 / d2, 0.0f, 1.0f));
@@ -721,7 +747,7 @@ static v3 calcDirectLighting(Frag *F, const Mesh *light, v3 x, v3 nl, float seed
         dl = add(dl, muls(muls(muls(mul(c, mh->mat.e), weight), gmax(0.001f, dot3(sr, nl))), T_fog));
       }
     } else if (light->t == T_SDF) {
-      v3 ld = add(light->pos, mul(randomSphereDirection(seed + 78.2358f), V(light->joker[0], light->joker[1], light->joker[2])));
+      v3 ld = add(anim_pos(o, light->pos, li), mul(randomSphereDirection(seed + 78.2358f), V(light->joker[0], light->joker[1], light->joker[2])));
       v3 sr = normalize(sub(ld, x));
       intersection(F, add(x, muls(nl, EPSILON)), sr, &hit);
       const Mesh *mh = &o->meshes[hit.index];
@@ -898,7 +924,7 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
     if (ai > o->n_lights - 1) ai = o->n_lights - 1;
     int li = o->light_index[ai];
     if (li < 0 || li >= o->n_meshes + o->n_sdfs) continue;
-    v3 lp = o->meshes[li].pos;
+    v3 lp = anim_pos(o, o->meshes[li].pos, li);
     v3 lc = mul(o->meshes[li].mat.c, o->meshes[li].mat.e);
     float tv = evaluateTargetFunction(lp, lc, hp, hn, mat);
     if (tv > 0.0f) updateReservoir(&init, lp, lc, li, tv, rv.y);
@@ -925,9 +951,17 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
         }
       }
       if (isValidReservoir(o, &h) && h.M > 0.0f && h.age < 30.0f) {
+        if (o->render_mode == 1 && h.idx >= 0 && h.idx < o->n_lights) { /* 1669-1676 */
+          int act = o->light_index[h.idx];
+          if (act >= 0 && act < o->n_meshes + o->n_sdfs) {
+            h.pos = anim_pos(o, o->meshes[act].pos, act);
+            h.col = mul(o->meshes[act].mat.c, o->meshes[act].mat.e);
+          }
+        }
         h.age += (float)(lvl + 1);
         float ta = 0.95f;
         if (lvl == 1) ta *= 0.80f;
+        if (o->render_mode == 1) ta *= 0.85f;
         h.M *= ta;
         h.ws *= ta;
         float trand = or_hash(sx + 789.123f + (float)lvl * 456.789f);
@@ -959,7 +993,7 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
         v3 ldf = sub(nb.pos, hp);
         if (dot3(ldf, ldf) > 225.0f) continue;
       }
-      float thr = 30.0f * 0.8f;
+      float thr = o->render_mode == 1 ? 2.0f : 30.0f * 0.8f;
       if (nb.age > thr || sr.x < 0.03f) continue;
       combineReservoirs(o, &fr, &nb, hp, hn, mat, sr.y);
     }
@@ -992,6 +1026,8 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
     int ai = fr.idx;
     int act = o->light_index[ai];
     if (act >= 0 && act < o->n_meshes + o->n_sdfs) {
+      /* RENDER_MODE 1: current light position must be visible (1767-1776) */
+      if (o->render_mode == 1 && !isVisible(F, hp, anim_pos(o, o->meshes[act].pos, act))) return V(0, 0, 0);
       v3 lc = calcDirectLighting(F, &o->meshes[act], hp, hn, sx + 456.789f);
       float ew = gclamp(fr.W, 0.0f, 8.0f);
       if (fr.M > 30.0f) ew *= sqrtf(30.0f / fr.M);
@@ -1136,7 +1172,7 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
         if (L->mat.t != M_LIGHT) continue;
         v3 ls = calcDirectLighting(F, L, x, nl, base + 5681.123f + bounce * 7895.13f + (float)i * 123.456f);
         if (dot3(ls, ls) > 0.000001f) {
-          v3 ld = normalize(sub(L->pos, x));
+          v3 ld = normalize(sub(anim_pos(o, L->pos, (int)(L - o->meshes)), x)); /* 1959 */
           float lp = lightSamplingPdf(L, x);
           float bp = cosineHemispherePdf(ld, nl);
           mc = add(mc, muls(ls, powerHeuristic(1.0f, lp, 1.0f, bp)));
@@ -1396,6 +1432,7 @@ void *or_create(void) {
   o->max_bounces = 12; o->max_diff = 4; o->max_spec = 4; o->max_trans = 12; o->max_scatter = 12;
   o->marching_steps = 128; o->fudge = 0.9f;
   o->sample_lights = 1; o->use_mis = 0; o->use_restir = 0; o->restir_samples = 16; o->render_mode = 0;
+  o->time_ms = 0.0f; o->temporal_frames = 5;
   o->cam_pos = V(0, 0, 2.8f); o->cam_look = V(0, 0, -1); o->cam_params = V(50, 0, 3.5f);
   return o;
 }
@@ -1504,7 +1541,7 @@ int or_set_constant(void *h, const char *name, double v) {
   else if (!strcmp(name, "SWIFTSHADER_GHOST")) o->ghost = iv;
   else if (!strcmp(name, "RENDER_MODE")) {
     o->render_mode = iv;
-    if (iv != 0) { snprintf(o->err, sizeof o->err, "RENDER_MODE 1 (animated) not supported"); return -1; }
+    if (iv != 0 && iv != 1) { snprintf(o->err, sizeof o->err, "RENDER_MODE must be 0 or 1"); return -1; }
   } else { snprintf(o->err, sizeof o->err, "unknown constant %s", name); return -1; }
   return 0;
 }
@@ -1540,6 +1577,11 @@ int or_set_cubemap(void *h, int size, const unsigned char *const *faces) {
   for (int i = 0; i < 6; i++) o->cube[i] = faces ? faces[i] : NULL;
   o->cube_size = faces ? size : 0;
   return 0;
+}
+/* u_time (ms) and u_temporalFrames for RENDER_MODE 1 */
+void or_set_time(void *h, float time_ms, int temporal_frames) {
+  ((Oracle *)h)->time_ms = time_ms;
+  ((Oracle *)h)->temporal_frames = temporal_frames > 0 ? temporal_frames : 5;
 }
 void or_set_resolution(void *h, int w, int hh) { ((Oracle *)h)->w = w; ((Oracle *)h)->h = hh; }
 
@@ -1605,7 +1647,12 @@ int or_render_accum(void *h, unsigned first, int n, float *acc, int row0, int ro
     for (int y = row0 < 0 ? 0 : row0; y < (row1 > o->h ? o->h : row1); y++)
       for (int x = 0; x < o->w; x++) {
         size_t p = ((size_t)y * o->w + x) * 4;
-        acc[p] += tmp[p]; acc[p + 1] += tmp[p + 1]; acc[p + 2] += tmp[p + 2];
+        if (o->render_mode == 1) { /* mix(previousFrame, currentFrame, 1/u_temporalFrames), 2159-2165 */
+          float a = 1.0f / (float)o->temporal_frames;
+          for (int k = 0; k < 3; k++) acc[p + k] = mixf(acc[p + k], tmp[p + k], a);
+        } else {
+          acc[p] += tmp[p]; acc[p + 1] += tmp[p + 1]; acc[p + 2] += tmp[p + 2];
+        }
       }
   }
   free(tmp);

@@ -96,6 +96,7 @@ enum : uint32_t {
   F_SPECTRAL = 1u << 6,
   F_VOL = 1u << 7,
   F_CUBEMAP = 1u << 8,  // #define USE_CUBEMAP
+  F_ANIM = 1u << 9,     // RENDER_MODE 1 (animated: getAnimatedPosition + EMA accumulator)
 };
 
 struct LaunchParams {
@@ -141,4 +142,10 @@ struct LaunchParams {
   const BvhNode *bvh;
   const TriDev *tris;
   int32_t n_tris;
+  // RENDER_MODE 1 (F_ANIM): the accumulator is an EMA with weight ema_alpha =
+  // 1/u_temporalFrames (raytracer.glsl:2159-2165), and apos[i] is
+  // getAnimatedPosition(meshes[i].pos, i, u_time) (263-298), evaluated once
+  // per launch on the host (it is uniform over the image).  Unused otherwise.
+  float ema_alpha;
+  float4 apos[RT0_MAX_MESH];
 };

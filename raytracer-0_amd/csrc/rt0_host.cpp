@@ -65,6 +65,7 @@ struct rt0_ctx {
   uchar4 *d_tonemap = nullptr;
   unsigned long long *d_counters = nullptr;
   bool counting = false;
+  int temporal_frames = 5;  // GlslViewport.temporalFrames (index.js:236) -> u_temporalFrames
   uint64_t counters[5] = {};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
@@ -189,7 +190,7 @@ int rt0_parse_config(const char *const *defines, int nd, const char *const *cons
 
 int rt0_set_config(rt0_ctx *c, const rt0_config *cfg) {
   if (!c || !cfg) return RT0_E_ARG;
-  if (cfg->render_mode != 0) return fail(c, RT0_E_UNSUPPORTED, "RENDER_MODE 1 (animated) is not supported");
+  if (cfg->render_mode != 0 && cfg->render_mode != 1) return fail(c, RT0_E_ARG, "RENDER_MODE must be 0 or 1");
   if (cfg->max_bounces < 0 || cfg->marching_steps < 0) return fail(c, RT0_E_ARG, "negative loop bound");
   c->cfg = *cfg;
   return RT0_OK;
@@ -435,6 +436,36 @@ int rt0_set_shard(rt0_ctx *c, int shard, int n_shards, int band_rows) {
   return RT0_OK;
 }
 
+// getAnimatedPosition (raytracer.glsl:263-298) for every scene entry at
+// u_time = time_ms: uniform over the image, so it is evaluated once per launch
+// here (fp32, the shader's operation order) instead of per lane.
+static void animated_positions(const rt0_ctx *c, float time_ms, float4 *out) {
+  const SceneDev &s = c->host_scene;
+  const float t = time_ms * 0.001f;
+  for (int i = 0; i < s.n_total && i < RT0_MAX_MESH; i++) {
+    const GeomRec &g = s.geom[i];
+    float x = g.px, y = g.py, z = g.pz;
+    if (i >= 6 && i <= 14) {
+      const float radius = 0.6f;
+      const float speed = 1.0f + (float)(i - 6) * 0.2f;
+      const float phase = (float)(i - 6) * 0.7f;
+      const float a = t * speed + phase;
+      x = g.px + (cosf(a) * radius) * 0.3f;
+      z = g.pz + (sinf(a) * radius) * 0.3f;
+      y = g.py + sinf((t * speed) * 2.0f + phase) * 0.1f;
+    }
+    if (i >= s.n_meshes && s.n_sdfs > 0) {  // SDF entries rotate about y
+      const float ang = t * 0.5f;
+      const float ca = cosf(ang), sa = sinf(ang);
+      const float rx = x * ca - z * sa, rz = x * sa + z * ca;
+      x = rx;
+      z = rz;
+      y = y + sinf(t * 1.5f) * 0.05f;
+    }
+    out[i] = make_float4(x, y, z, 0.f);
+  }
+}
+
 static void fill_params(rt0_ctx *c, LaunchParams &p) {
   memset(&p, 0, sizeof p);
   const rt0_config &g = c->cfg;
@@ -467,17 +498,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.uULen = p.aspect * p.uVLen;
   p.aperture = c->cam_params[1];
   p.focal = c->cam_params[2];
-  uint32_t f = 0;
-  if (g.defines & RT0_USE_PROCEDURAL_SKY) f |= F_SKY;
-  if (g.defines & RT0_USE_BIASED_SAMPLING) f |= F_BIASED;
-  if (g.sample_lights) f |= F_SAMPLE_LIGHTS;
-  if (g.use_mis) f |= F_MIS;
-  if (g.use_restir) f |= F_RESTIR;
-  if (g.defines & RT0_USE_RESTIR) f |= F_RESTIR_DEF;
-  if (g.defines & RT0_USE_SPECTRAL) f |= F_SPECTRAL;
-  if (g.defines & RT0_USE_VOLUMETRICS) f |= F_VOL;
-  if (g.defines & RT0_USE_CUBEMAP) f |= F_CUBEMAP;
-  p.flags = f;
+  p.flags = rt0h::flags_from_config(g);
   p.max_bounces = g.max_bounces;
   p.max_diff = g.max_diff_bounces;
   p.max_spec = g.max_spec_bounces;
@@ -505,6 +526,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.n_tris = c->n_tris;
   p.accum = c->acc();
   p.counters = c->d_counters;
+  p.ema_alpha = 1.0f / (float)c->temporal_frames;  // raytracer.glsl:2164
   if (c->n_shards > 1) {  // one contiguous block per shard (checked for ReSTIR in render_impl)
     const int lo = c->shard * c->band, hi = std::min(c->H, lo + c->band);
     p.valid_lo = std::max(0, lo - c->halo);
@@ -526,7 +548,7 @@ static int choose_variant(const rt0_ctx *c) {
   return 0;
 }
 
-static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
+static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sync) {
   if (!c || n < 0) return RT0_E_ARG;
   if (!c->has_scene) return fail(c, RT0_E_STATE, "rt0_render before rt0_set_scene*");
   const bool restir = (c->cfg.defines & RT0_USE_RESTIR) != 0;
@@ -545,6 +567,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
   }
   LaunchParams p;
   fill_params(c, p);
+  if (p.flags & F_ANIM) animated_positions(c, time_ms, p.apos);
   if (p.n_band_rows == 0 || n == 0) {
     c->last_ms = 0.f;
     c->last_launches = 0;
@@ -651,14 +674,16 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, bool sync) {
   return RT0_OK;
 }
 
-int rt0_render(rt0_ctx *c, uint32_t first, int n, float time_ms) {
-  (void)time_ms;  // u_time only feeds RENDER_MODE 1 (getAnimatedPosition, raytracer.glsl:263-298)
-  return render_impl(c, first, n, true);
-}
+int rt0_render(rt0_ctx *c, uint32_t first, int n, float time_ms) { return render_impl(c, first, n, time_ms, true); }
 
 int rt0_render_async(rt0_ctx *c, uint32_t first, int n, float time_ms) {
-  (void)time_ms;
-  return render_impl(c, first, n, false);
+  return render_impl(c, first, n, time_ms, false);
+}
+
+int rt0_set_temporal_frames(rt0_ctx *c, int n) {
+  if (!c || n <= 0) return RT0_E_ARG;
+  c->temporal_frames = n;
+  return RT0_OK;
 }
 
 int rt0_sync(rt0_ctx *c) {

@@ -352,6 +352,13 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
   return best;
 }
 
+// getAnimatedPosition(meshes[i].pos, i, u_time) (raytracer.glsl:263-298),
+// precomputed per launch (LaunchParams::apos); only read under F_ANIM.
+DEV v3 anim_pos(const LaunchParams &P, int i) {
+  const float4 a = P.apos[i];
+  return mk(a.x, a.y, a.z);
+}
+
 template <class Scene>
 struct Geometry {
   // map(), raytracer.glsl:700-712 + the #sdf_meshes statements of index.html:702-717
@@ -422,8 +429,8 @@ struct Geometry {
       const GeomRec g = sc.geom(i);
       if (g.j0 == 0.0f) return;  // raytracer.glsl:1009
       const v3 gp = mk(g.px, g.py, g.pz);
-      if (g.type == T_SPHERE) {  // iSphere, 818-833
-        v3 oc = o - gp;
+      if (g.type == T_SPHERE) {  // iSphere, 818-833 (centre animated in RENDER_MODE 1, 819)
+        v3 oc = o - ((C.flags() & F_ANIM) ? anim_pos(P, i) : gp);
         float b = dot(oc, d);
         float c = dot(oc, oc) - g.d0;
         float disc = b * b - c;
@@ -510,9 +517,9 @@ struct Geometry {
     hit.type = type;
     if (type >= 0) {
       hit.pos = d * tmin + o;
-      if (type == T_SPHERE) {
+      if (type == T_SPHERE) {  // 1060
         const GeomRec g = sc.geom(hit.index);
-        hit.n = normalize(hit.pos - mk(g.px, g.py, g.pz));
+        hit.n = normalize(hit.pos - ((C.flags() & F_ANIM) ? anim_pos(P, hit.index) : mk(g.px, g.py, g.pz)));
       } else if (type == T_PLANE) {
         const GeomRec g = sc.geom(hit.index);
         hit.n = normalize(mk(g.px, g.py, g.pz));
@@ -917,6 +924,9 @@ struct Integrator {
       : P(p), sc(s), C(c), n_isect(0), n_iter(0), n_nee(0), n_map(0) {}
 
   DEV bool flag(uint32_t f) const { return (C.flags() & f) != 0; }
+  // a light/sphere position as the reference reads it where it calls
+  // getAnimatedPosition (RENDER_MODE 1); the static position otherwise
+  DEV v3 lpos(int i, const GeomRec &g) const { return flag(F_ANIM) ? anim_pos(P, i) : mk(g.px, g.py, g.pz); }
 
   DEV float isect(v3 o, v3 d, Hit &h) {
     if (COUNT) ++n_isect;
@@ -946,7 +956,7 @@ struct Integrator {
     v3 dl = mk(0.f, 0.f, 0.f);
     if (lm.type == M_LIGHT) {
       if (g.type == T_SPHERE) {
-        v3 sw = mk(g.px, g.py, g.pz) - x;
+        v3 sw = lpos(li, g) - x;  // 1185
         float d2 = dot(sw, sw);
         float cos_a_max = fsqrt(1.0f - fminf(fmaxf(fdiv(g.d0, d2), 0.0f), 1.0f));
         v3 sr = sample_cone(normalize(sw), 1.0f - cos_a_max, seed + 23.1656f);
@@ -965,7 +975,7 @@ struct Integrator {
           dl = (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
         }
       } else if (SDF && g.type == T_SDF) {
-        v3 ld = mk(g.px, g.py, g.pz) + random_sphere_dir(seed + 78.2358f) * mk(g.j0, g.j1, g.j2);
+        v3 ld = lpos(li, g) + random_sphere_dir(seed + 78.2358f) * mk(g.j0, g.j1, g.j2);  // 1207
         v3 sr = normalize(ld - x);
         isect(x + nl * EPSILON, sr, hit);
         const MatRec mh = sc.mat(hit.index);
@@ -1100,7 +1110,7 @@ struct Integrator {
       if (li < 0 || li >= sc.n_meshes() + sc.n_sdfs()) continue;
       const GeomRec lg = sc.geom(li);
       const MatRec lmt = sc.mat(li);
-      v3 lp = mk(lg.px, lg.py, lg.pz);
+      v3 lp = lpos(li, lg);  // 1645
       v3 lc = mk(lmt.cr, lmt.cg, lmt.cb) * mk(lmt.er, lmt.eg, lmt.eb);
       float tv = target_fn(lp, lc, hp, hn, mat);
       if (tv > 0.0f) {  // updateReservoir, 1305-1326
@@ -1139,8 +1149,17 @@ struct Integrator {
           }
         }
         if (valid_res(h) && h.M > 0.0f && h.age < 30.0f) {
+          if (flag(F_ANIM) && h.idx >= 0 && h.idx < nl) {  // history follows the moving light, 1669-1676
+            const int act = sc.light(h.idx);
+            if (act >= 0 && act < sc.n_meshes() + sc.n_sdfs()) {
+              const MatRec am = sc.mat(act);
+              h.pos = lpos(act, sc.geom(act));
+              h.col = mk(am.cr, am.cg, am.cb) * mk(am.er, am.eg, am.eb);
+            }
+          }
           h.age += (float)(lvl + 1);
           float ta = lvl == 1 ? 0.95f * 0.80f : 0.95f;
+          if (flag(F_ANIM)) ta *= 0.85f;  // 1688-1690
           h.M *= ta;
           h.ws *= ta;
           float trand = hash(nc_addmul(sx + 789.123f, (float)lvl, 456.789f));
@@ -1168,7 +1187,7 @@ struct Integrator {
           v3 ldf = nb.pos - hp;
           if (dot(ldf, ldf) > 225.0f) continue;
         }
-        if (nb.age > 30.0f * 0.8f || srx < 0.03f) continue;
+        if (nb.age > (flag(F_ANIM) ? 2.0f : 30.0f * 0.8f) || srx < 0.03f) continue;  // 1743
         combine(fr, nb, hp, hn, mat, sry);
       }
     }
@@ -1197,6 +1216,9 @@ struct Integrator {
     if (fr.W > 0.0f && fr.idx >= 0 && fr.idx < nl) {
       int act = sc.light(fr.idx);
       if (act >= 0 && act < sc.n_meshes() + sc.n_sdfs()) {
+        // RENDER_MODE 1 re-checks visibility of the light's current position
+        // (1767-1776); g_final_reservoir was stored before that update
+        if (flag(F_ANIM) && !visible(hp, lpos(act, sc.geom(act)))) return mk(0.f, 0.f, 0.f);
         v3 lc = direct_light(act, hp, hn, sx + 456.789f);
         float ew = fminf(fmaxf(fr.W, 0.0f), 8.0f);
         if (fr.M > 30.0f) ew *= fsqrt(30.0f / fr.M);
@@ -1255,7 +1277,7 @@ struct Integrator {
         if (lmt.type != M_LIGHT) return;
         v3 ls = direct_light(idx, x, nl, nc_addmul(base, (float)i, 123.456f));
         if (dot(ls, ls) > 0.000001f) {
-          v3 ld = normalize(mk(lg.px, lg.py, lg.pz) - x);
+          v3 ld = normalize(lpos(idx, lg) - x);  // 1959 (lightSamplingPdf keeps light.pos)
           acc = acc + ls * power_heuristic(light_pdf(lg, lmt, x), cos_pdf(ld, nl));
         }
       });
@@ -1524,7 +1546,11 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     for (int f = 0; f < P.nframes; ++f) {
       it.frame = P.frame0 + (uint32_t)f;
       v3 s = it.sample(px, py);
-      {
+      if (it.flag(F_ANIM)) {  // RENDER_MODE 1: mix(previousFrame, currentFrame, alpha), 2159-2165
+        a.x = mixf(a.x, s.x, P.ema_alpha);
+        a.y = mixf(a.y, s.y, P.ema_alpha);
+        a.z = mixf(a.z, s.z, P.ema_alpha);
+      } else {
 #pragma clang fp contract(off)
         a.x += opq(s.x);
         a.y += opq(s.y);
@@ -1567,9 +1593,15 @@ DEV void sum_body(const LaunchParams &P) {
   float4 a = P.accum[pix];
   for (int f = 0; f < P.nframes; ++f) {
     const float4 s = P.samples[(size_t)f * plane + lp];
-    a.x += s.x;
-    a.y += s.y;
-    a.z += s.z;
+    if (P.flags & F_ANIM) {
+      a.x = mixf(a.x, s.x, P.ema_alpha);
+      a.y = mixf(a.y, s.y, P.ema_alpha);
+      a.z = mixf(a.z, s.z, P.ema_alpha);
+    } else {
+      a.x += s.x;
+      a.y += s.y;
+      a.z += s.z;
+    }
   }
   P.accum[pix] = a;
 }

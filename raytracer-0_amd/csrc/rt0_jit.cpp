@@ -288,6 +288,7 @@ uint32_t flags_from_config(const rt0_config &g) {
   if (g.defines & RT0_USE_SPECTRAL) f |= F_SPECTRAL;
   if (g.defines & RT0_USE_VOLUMETRICS) f |= F_VOL;
   if (g.defines & RT0_USE_CUBEMAP) f |= F_CUBEMAP;
+  if (g.render_mode == 1) f |= F_ANIM;
   return f;
 }
 

@@ -180,12 +180,24 @@ class GlslViewport {
       [c.fov, c.aperture, c.focalLength]);
   }
 
-  // index.js:986-1105: one pass, u_frame = ++passes (n > 1 batches passes)
-  render(n) {
+  // index.js:986-1105: one pass, u_frame = ++passes (n > 1 batches passes).
+  // Animated mode (index.js:990-1005): the pass counter cycles
+  // (passes > 2*temporalFrames -> temporalFrames) and the accumulator is the
+  // RENDER_MODE 1 running average over u_temporalFrames.
+  render(n, timeMs) {
     n = n || 1;
     this.updateFrontTarget();
-    addon.render(this._h, this.passes + 1, n, Date.now() - this.loadTime);
-    this.passes += n;
+    const t = timeMs === undefined ? Date.now() - this.loadTime : timeMs;
+    if (!this.animatedScene) {
+      addon.render(this._h, this.passes + 1, n, t);
+      this.passes += n;
+      return;
+    }
+    addon.setTemporalFrames(this._h, this.temporalFrames);
+    for (let k = 0; k < n; k++) {
+      if (this.passes > this.temporalFrames * 2) this.passes = this.temporalFrames;
+      addon.render(this._h, ++this.passes, 1, t);
+    }
   }
 
   // index.js:822-880
@@ -209,8 +221,8 @@ class GlslViewport {
 
   accumulator() { return addon.readAccum(this._h); }
 
-  // display pass (tonemapper.glsl:28-33) with u_cont = 1/passes (index.js:1089)
-  image() { return addon.tonemap(this._h, 1.0 / Math.max(1, this.passes)); }
+  // display pass (tonemapper.glsl:28-33) with u_cont = 1/passes, 1 when animated (index.js:1080-1090)
+  image() { return addon.tonemap(this._h, this.animatedScene ? 1.0 : 1.0 / Math.max(1, this.passes)); }
 
   lastKernelMs() { return addon.lastKernelMs(this._h); }
 }

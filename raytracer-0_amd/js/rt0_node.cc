@@ -243,6 +243,16 @@ static napi_value Render(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+static napi_value SetTemporalFrames(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  int32_t n = 5;
+  napi_get_value_int32(env, argv[1], &n);
+  RC_OR_THROW(rt0_set_temporal_frames(c, n));
+  return nullptr;
+}
+
 static napi_value ReadAccum(napi_env env, napi_callback_info info) {
   napi_value argv[1];
   if (!get_args(env, info, 1, argv)) return nullptr;
@@ -463,6 +473,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"setScene", nullptr, SetScene, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setCamera", nullptr, SetCamera, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"render", nullptr, Render, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setTemporalFrames", nullptr, SetTemporalFrames, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readAccum", nullptr, ReadAccum, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"tonemap", nullptr, Tonemap, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"clear", nullptr, Clear, nullptr, nullptr, nullptr, napi_default, nullptr},

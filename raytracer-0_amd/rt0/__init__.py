@@ -10,6 +10,7 @@ fallback, and every entry point raises if the library or a GPU is missing.
 """
 import ctypes
 import os
+import time
 
 import numpy as np
 
@@ -30,7 +31,8 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
-           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read"]
+           "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read",
+           "rt0_set_temporal_frames"]
 
 TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
@@ -95,6 +97,7 @@ def lib():
         "rt0_set_cubemap": (c_int, [c_void_p, c_int, P(P(ctypes.c_uint8))]),
         "rt0_render": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
         "rt0_render_async": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
+        "rt0_set_temporal_frames": (c_int, [c_void_p, c_int]),
         "rt0_sync": (c_int, [c_void_p]),
         "rt0_read_accum": (c_int, [c_void_p, fp]),
         "rt0_write_accum": (c_int, [c_void_p, fp]),
@@ -402,6 +405,10 @@ class Renderer:
     def render(self, first_frame, n_passes, time_ms=0.0):
         self._chk(lib().rt0_render(self.h, first_frame, n_passes, time_ms))
 
+    def set_temporal_frames(self, n):
+        """u_temporalFrames: RENDER_MODE 1 running-average length (index.js:236)."""
+        self._chk(lib().rt0_set_temporal_frames(self.h, int(n)))
+
     def render_async(self, first_frame, n_passes, time_ms=0.0):
         self._chk(lib().rt0_render_async(self.h, first_frame, n_passes, time_ms))
 
@@ -543,6 +550,7 @@ class GlslViewport:
         self.max_passes = opts.get("max_passes", float("inf"))
         self.animatedScene = False
         self.temporalFrames = 5
+        self.loadTime = time.monotonic() * 1000.0  # u_time origin (index.js:986)
         self.renderer = Renderer(self.width, self.height, device)
         self._compiled = None
         self.images = {}
@@ -585,12 +593,26 @@ class GlslViewport:
         self.renderer.set_camera(c["origin"].tolist(), c["lookat"].tolist(),
                                  [c["fov"], c["aperture"], c["focalLength"]])
 
-    def render(self, n_passes=1):
-        """index.js:986-1105: u_frame = ++passes per pass; accumulate."""
+    def render(self, n_passes=1, time_ms=None):
+        """index.js:986-1105: u_frame = ++passes per pass; accumulate.
+
+        Animated mode (index.js:990-1005) keeps the pass counter cycling
+        (passes > 2*temporalFrames -> temporalFrames) so the ReSTIR history
+        stays valid, and every pass sees u_time = ms since construction (or
+        `time_ms`)."""
         self.updateFrontTarget()
-        first = self.passes + 1
-        self.renderer.render(first, n_passes, 0.0)
-        self.passes += n_passes
+        t = (time.monotonic() * 1000.0 - self.loadTime) if time_ms is None else float(time_ms)
+        if not self.animatedScene:
+            first = self.passes + 1
+            self.renderer.render(first, n_passes, t)
+            self.passes += n_passes
+            return
+        self.renderer.set_temporal_frames(self.temporalFrames)
+        for _ in range(n_passes):
+            if self.passes > self.temporalFrames * 2:
+                self.passes = self.temporalFrames
+            self.passes += 1
+            self.renderer.render(self.passes, 1, t)
 
     def clear(self):
         """index.js:822-880."""
@@ -604,7 +626,7 @@ class GlslViewport:
         self.passes = 0
 
     def setAnimatedMode(self, is_animated):
-        """index.js:940-983 (animated mode itself is RENDER_MODE 1: unsupported)."""
+        """index.js:940-983: animated constants (RENDER_MODE 1, ReSTIR) or the static ones."""
         self.animatedScene = bool(is_animated)
         if is_animated:
             self.constants = list(self.animatedConstants)
@@ -618,8 +640,9 @@ class GlslViewport:
         return self.renderer.read_accum()
 
     def image(self):
-        """Display pass, tonemapper.glsl:28-33 with u_cont = 1/passes (index.js:1089)."""
-        return self.renderer.tonemap(1.0 / max(1, self.passes))
+        """Display pass, tonemapper.glsl:28-33 with u_cont = 1/passes, or 1 for the
+        animated running average (index.js:1080-1090)."""
+        return self.renderer.tonemap(1.0 if self.animatedScene else 1.0 / max(1, self.passes))
 
 
 STATIC_CONSTANTS = ["const lowp int MAX_BOUNCES = 12;", "const lowp int MAX_DIFF_BOUNCES = 4;",

@@ -1,0 +1,174 @@
+"""Animated mode: RENDER_MODE 1 (index.js:37-51 animatedConstants, 940-958
+setAnimatedMode, 990-1005 the cycling pass counter).
+
+The shader moves the meshes 6..14 and the SDF entries with u_time
+(getAnimatedPosition, raytracer.glsl:263-298) wherever it calls that function
+(iSphere 819, the sphere normal 1060, calcDirectLighting 1185/1207, the ReSTIR
+candidates / history / final light 1645, 1669-1676, 1767-1776, the MIS light
+direction 1959), damps the ReSTIR history (1688-1690, 1743) and replaces the
+progressive sum by the running average mix(prev, sample, 1/u_temporalFrames)
+(2159-2165).
+
+Fixtures (tests/golden/anim_*.npz) are the reference shader run by SwiftShader
+with u_bufferA = 0, so each pass is mix(0, sample, 1/5) = sample/5.  These
+scenes are dim (tiny lights), so on top of the usual absolute tolerance the
+checks here are relative: a pixel matches when every channel satisfies
+|d| <= REL * max(|ref|, FLOOR), and the image's relative L2 error is bounded.
+Restatement vs reference (measured): >= 99.88% of pixels, L2 <= 1.6e-4.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REL, FLOOR = 1e-3, 1e-5
+ALPHA = np.float32(1.0 / 5.0)  # 1/u_temporalFrames, temporalFrames = 5 (index.js:236)
+NAMES = ["anim_mis_sdflight", "anim_restir_demo"]
+
+
+def cfg_by_name(cfgs, name):
+    return [c for c in cfgs["configs"] if c["name"] == name][0]
+
+
+def rel_match(got, ref):
+    ok = (np.abs(got - ref) <= REL * np.maximum(np.abs(ref), FLOOR)).all(-1)
+    l2 = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+    return ok.mean(), l2
+
+
+def restir_inputs(G, k):
+    def out(j, key):
+        return G[key][j - 1] if j >= 1 else np.zeros_like(G["restir_main"][0])
+    return [out(k - 1, "restir_main"), out(k - 1, "restir_aux"), out(k - 2, "restir_main"),
+            out(k - 2, "restir_aux"), out(k - 3, "restir_main"), out(k - 3, "restir_aux")]
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_animated_matches_reference(name, cfgs):
+    """The restatement's RENDER_MODE 1 against the reference (ReSTIR: with the
+    reference's own reservoirs of passes k-1..k-3 as input)."""
+    cfg = cfg_by_name(cfgs, name)
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    F, H, W = G["samples"].shape[:3]
+    o = O.Oracle(cfg, cfgs, width=W, height=H)
+    restir = "restir_main" in G
+    for k in range(1, F + 1):
+        o.set_time(O.pass_time(cfg, k), cfg.get("temporal_frames", 5))
+        s = o.frame(k, restir_inputs(G, k) if restir else None)[0][..., :3] * ALPHA
+        frac, l2 = rel_match(s, G["samples"][k - 1][..., :3])
+        assert frac >= 0.995 and l2 <= 1e-3, (name, k, frac, l2)
+
+
+def test_oracle_animated_positions_move(cfgs):
+    """u_time matters in RENDER_MODE 1 and is ignored in RENDER_MODE 0."""
+    cfg = cfg_by_name(cfgs, "anim_mis_sdflight")
+    o = O.Oracle(cfg, cfgs, width=32, height=32)
+    o.set_time(1000.0)
+    a = o.frame(1)[0]
+    o.set_time(4000.0)
+    b = o.frame(1)[0]
+    assert not np.array_equal(a, b)
+    s = O.Oracle(cfg, cfgs, width=32, height=32, overrides={"RENDER_MODE": 0})
+    s.set_time(1000.0)
+    c = s.frame(1)[0]
+    s.set_time(4000.0)
+    assert np.array_equal(c, s.frame(1)[0])
+
+
+def test_oracle_ema_accumulator(cfgs):
+    """or_render_accum in RENDER_MODE 1 is the running average of the passes."""
+    cfg = cfg_by_name(cfgs, "anim_mis_sdflight")
+    o = O.Oracle(cfg, cfgs, width=16, height=16)
+    o.set_time(2500.0)
+    acc = o.accumulate(1, 3)
+    ref = np.zeros_like(acc)
+    for k in range(1, 4):
+        s = o.frame(k)[0]
+        ref[..., :3] = ALPHA * (s[..., :3] - ref[..., :3]) + ref[..., :3]
+    assert np.allclose(acc[..., :3], ref[..., :3], rtol=1e-6, atol=1e-9)
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_gpu_animated_matches_reference(name, cfgs, gpu_required):
+    import rt0
+    cfg = cfg_by_name(cfgs, name)
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    F, H, W = G["samples"].shape[:3]
+    r = rt0.Renderer(W, H)
+    rt0.configure(r, cfg, cfgs)
+    r.set_temporal_frames(cfg.get("temporal_frames", 5))
+    restir = "restir_main" in G
+    for k in range(1, F + 1):
+        r.clear()
+        if restir:
+            r.write_restir_inputs(*restir_inputs(G, k))
+        r.render(k, 1, O.pass_time(cfg, k))
+        got = r.read_accum()[..., :3]
+        assert np.isfinite(got).all()
+        frac, l2 = rel_match(got, G["samples"][k - 1][..., :3])
+        assert frac >= 0.98 and l2 <= 5e-3, (name, k, frac, l2)
+
+
+@pytest.mark.gpu
+def test_gpu_animated_matches_oracle_larger(cfgs, gpu_required):
+    """96^2, beyond the fixtures: GPU RENDER_MODE 1 vs the restatement."""
+    import rt0
+    cfg = cfg_by_name(cfgs, "anim_mis_sdflight")
+    o = O.Oracle(cfg, cfgs, width=96, height=96)
+    r = rt0.Renderer(96, 96)
+    rt0.configure(r, cfg, cfgs)
+    for k, t in ((1, 800.0), (7, 12345.0)):
+        o.set_time(t)
+        ref = o.frame(k)[0][..., :3] * ALPHA
+        r.clear()
+        r.render(k, 1, t)
+        frac, l2 = rel_match(r.read_accum()[..., :3], ref)
+        assert frac >= 0.98 and l2 <= 5e-3, (k, frac, l2)
+
+
+@pytest.mark.gpu
+def test_gpu_ema_chain(cfgs, gpu_required):
+    """n passes in one call = the running average of the single passes, and
+    the frame-chunked launch (a 1-shard-of-8 grid) gives the same result."""
+    import rt0
+    cfg = cfg_by_name(cfgs, "anim_mis_sdflight")
+    r = rt0.Renderer(64, 64)
+    rt0.configure(r, cfg, cfgs)
+    r.set_temporal_frames(4)
+    alpha = np.float32(0.25)
+    ref = np.zeros((64, 64, 3), np.float32)
+    for k in range(1, 6):
+        r.clear()
+        r.render(k, 1, 3000.0)
+        s = r.read_accum()[..., :3] / alpha
+        ref = alpha * (s - ref) + ref
+    r.clear()
+    r.render(1, 5, 3000.0)
+    got = r.read_accum()[..., :3]
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_gpu_viewport_animated_pass_cycle(gpu_required):
+    """GlslViewport.setAnimatedMode(true) + render(): u_frame cycles
+    1..2T+1, then T+1..2T+1 (index.js:1002-1004), and the display uses
+    contribution 1."""
+    import rt0
+    vp = rt0.GlslViewport(opts={"width": 32, "height": 32})
+    vp.setAnimatedMode(True)
+    seen = []
+    for _ in range(16):
+        vp.render(1, time_ms=500.0)
+        seen.append(vp.passes)
+    T = vp.temporalFrames
+    assert seen[:2 * T + 1] == list(range(1, 2 * T + 2))
+    assert seen[2 * T + 1] == T + 1
+    img = vp.image()
+    assert img.shape[:2] == (32, 32)
+    acc = vp.accumulator()
+    assert np.isfinite(acc).all()
