@@ -1291,186 +1291,207 @@ struct Integrator {
     return acc;
   }
 
-  // radiance() + brdf(), raytracer.glsl:1986-2105 and 1804-1980
-  DEV v3 radiance(v3 ro, v3 rd, float seed) {
-    v3 acc = mk(0.f, 0.f, 0.f), mask = mk(1.f, 1.f, 1.f);
-    bool spec = true;
-    v3 prev_nl = mk(0.f, 1.f, 0.f);
+  // radiance() + brdf(), raytracer.glsl:1986-2105 and 1804-1980, as a step
+  // function: one iteration of the bounce loop per call, so that a lane whose
+  // path ended can start its next sample while the rest of its wave is still
+  // bouncing (path regeneration in pass_body).  The path state is what the
+  // shader keeps across iterations.
+  struct Path {
+    v3 ro, rd, acc, mask, prev_nl;
+    float seed;
+    int depth;
+    bool spec;
+  };
+  // false = the path ended (a `break` of the reference loop, or depth reached MAX_BOUNCES)
+  DEV bool step(Path &ps) {
+    v3 &ro = ps.ro, &rd = ps.rd, &acc = ps.acc, &mask = ps.mask, &prev_nl = ps.prev_nl;
+    bool &spec = ps.spec;
+    const float seed = ps.seed;
+    const int depth = ps.depth;
     const float fr = (float)frame;
-    for (int depth = 0; depth < C.max_bounces(); ++depth) {
-      if (COUNT) ++n_iter;
-      Hit hit;
-      float t = isect(ro, rd, hit);
-      if constexpr (VOL) {
-        if (flag(F_VOL)) {
-          float sd = -flog(fmaxf(hash(nc_addmul(seed + 4729.3f, (float)depth, 991.1f)), 1e-6f)) / VOL_SIGMA_T;
-          if (sd < fminf(INF_T, t)) {
-            v3 sp = ro + rd * sd;
-            mask = mask * (VOL_SIGMA_S / VOL_SIGMA_T);
-            if (flag(F_SAMPLE_LIGHTS)) {
-              for_lights(sc, [&](int li) {
-                int lidx = sc.light(li);
-                if (lidx < 0) return;
-                const GeomRec lg = sc.geom(lidx);
-                const MatRec lmt = sc.mat(lidx);
-                if (lmt.type != M_LIGHT || lg.type != T_SPHERE) return;
-                v3 dlc = mk(lg.px, lg.py, lg.pz) - sp;
-                float dc = length(dlc);
-                float cam = fsqrt(1.0f - fminf(fmaxf(fdiv(lg.d0, dc * dc), 0.0f), 1.0f));
-                float idc = frcp(dc);
-                v3 dir = sample_cone(mk(dlc.x * idc, dlc.y * idc, dlc.z * idc), 1.0f - cam,
-                                     nc_addmul(nc_addmul(seed + 2341.7f, (float)li, 917.3f), (float)depth, 199.1f));
-                if (COUNT) ++n_nee;
-                Hit sh;
-                float ts = isect(sp + dir * (EPSILON * 20.0f), dir, sh);
-                if (sh.index != lidx) return;
-                float omega = 2.0f * (1.0f - cam);
-                float ct = dot(rd, dir);
-                constexpr float g2 = VOL_G * VOL_G;
-                float den = 1.0f + g2 - 2.0f * VOL_G * ct;
-                float phase = fdiv(1.0f - g2, FOUR_PI * den * fsqrt(den));
-                float Tf = fexp(-VOL_SIGMA_T * ts);
-                acc = acc + ((((mask * mk(lmt.cr, lmt.cg, lmt.cb)) * mk(lmt.er, lmt.eg, lmt.eb)) * phase) * Tf) *
-                                (PI_F * omega);
-              });
-            }
-            rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
-            ro = sp;
-            spec = false;
-            ++scat_ev;
-            if (scat_ev >= C.max_scatter() || vmaxc(mask) < 0.01f) break;
-            continue;
+    {
+    if (COUNT) ++n_iter;
+    Hit hit;
+    float t = isect(ro, rd, hit);
+    if constexpr (VOL) {
+      if (flag(F_VOL)) {
+        float sd = -flog(fmaxf(hash(nc_addmul(seed + 4729.3f, (float)depth, 991.1f)), 1e-6f)) / VOL_SIGMA_T;
+        if (sd < fminf(INF_T, t)) {
+          v3 sp = ro + rd * sd;
+          mask = mask * (VOL_SIGMA_S / VOL_SIGMA_T);
+          if (flag(F_SAMPLE_LIGHTS)) {
+            for_lights(sc, [&](int li) {
+              int lidx = sc.light(li);
+              if (lidx < 0) return;
+              const GeomRec lg = sc.geom(lidx);
+              const MatRec lmt = sc.mat(lidx);
+              if (lmt.type != M_LIGHT || lg.type != T_SPHERE) return;
+              v3 dlc = mk(lg.px, lg.py, lg.pz) - sp;
+              float dc = length(dlc);
+              float cam = fsqrt(1.0f - fminf(fmaxf(fdiv(lg.d0, dc * dc), 0.0f), 1.0f));
+              float idc = frcp(dc);
+              v3 dir = sample_cone(mk(dlc.x * idc, dlc.y * idc, dlc.z * idc), 1.0f - cam,
+                                   nc_addmul(nc_addmul(seed + 2341.7f, (float)li, 917.3f), (float)depth, 199.1f));
+              if (COUNT) ++n_nee;
+              Hit sh;
+              float ts = isect(sp + dir * (EPSILON * 20.0f), dir, sh);
+              if (sh.index != lidx) return;
+              float omega = 2.0f * (1.0f - cam);
+              float ct = dot(rd, dir);
+              constexpr float g2 = VOL_G * VOL_G;
+              float den = 1.0f + g2 - 2.0f * VOL_G * ct;
+              float phase = fdiv(1.0f - g2, FOUR_PI * den * fsqrt(den));
+              float Tf = fexp(-VOL_SIGMA_T * ts);
+              acc = acc + ((((mask * mk(lmt.cr, lmt.cg, lmt.cb)) * mk(lmt.er, lmt.eg, lmt.eb)) * phase) * Tf) *
+                              (PI_F * omega);
+            });
           }
+          rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
+          ro = sp;
+          spec = false;
+          ++scat_ev;
+          if (scat_ev >= C.max_scatter() || vmaxc(mask) < 0.01f) return false;
+          return ++ps.depth < C.max_bounces();
         }
       }
-      if (t == INF_T) {
-        if (!spec && flag(F_SAMPLE_LIGHTS)) break;
-        if (flag(F_CUBEMAP)) {  // 2059-2060 (USE_CUBEMAP wins over the procedural sky)
-          const T4 cm = cube_sample(P, rd);
-          acc = acc + mask * mk(cm.r, cm.g, cm.b);
-        } else if (flag(F_SKY)) {
-          float k = fminf(fmaxf(rd.y * 0.6f + 0.5f, 0.3f), 1.0f);
-          v3 sky = mk(0.5f + 0.5f * fcos(TWO_PI * (0.525f + 0.9f * k)), 0.5f + 0.5f * fcos(TWO_PI * (0.408f + 0.97f * k)),
-                      0.5f + 0.5f * fcos(TWO_PI * (0.409f + 0.8f * k)));
-          acc = acc + mask * sky;
-        }
-        break;
+    }
+    if (t == INF_T) {
+      if (!spec && flag(F_SAMPLE_LIGHTS)) return false;
+      if (flag(F_CUBEMAP)) {  // 2059-2060 (USE_CUBEMAP wins over the procedural sky)
+        const T4 cm = cube_sample(P, rd);
+        acc = acc + mask * mk(cm.r, cm.g, cm.b);
+      } else if (flag(F_SKY)) {
+        float k = fminf(fmaxf(rd.y * 0.6f + 0.5f, 0.3f), 1.0f);
+        v3 sky = mk(0.5f + 0.5f * fcos(TWO_PI * (0.525f + 0.9f * k)), 0.5f + 0.5f * fcos(TWO_PI * (0.408f + 0.97f * k)),
+                    0.5f + 0.5f * fcos(TWO_PI * (0.409f + 0.8f * k)));
+        acc = acc + mask * sky;
       }
-      const GeomRec g = sc.geom(hit.index);
-      const MatRec mt = sc.mat(hit.index);
-      v3 c = mk(mt.cr, mt.cg, mt.cb), e = mk(mt.er, mt.eg, mt.eb);
-      if (sc.any_tex()) {  // raytracer.glsl:2071, 2077
-        const TexRec tr = sc.tex(hit.index);
-        if (tr.type >= 0 && (tr.opts & 3u)) {
-          const T4 tx = hit_texel(P, tr, hit);
-          if (tr.opts & 1u) {
-            const float a = tx.a;
-            c = mk(mixf(c.x, tx.r * tr.cmr, a), mixf(c.y, tx.g * tr.cmg, a), mixf(c.z, tx.b * tr.cmb, a));
-          }
-          if (tr.opts & 2u) {
-            const float a = tx.a;
-            e = mk(mixf(e.x, tx.r * tr.emr, a), mixf(e.y, tx.g * tr.emg, a), mixf(e.z, tx.b * tr.emb, a));
-          }
+      return false;
+    }
+    const GeomRec g = sc.geom(hit.index);
+    const MatRec mt = sc.mat(hit.index);
+    v3 c = mk(mt.cr, mt.cg, mt.cb), e = mk(mt.er, mt.eg, mt.eb);
+    if (sc.any_tex()) {  // raytracer.glsl:2071, 2077
+      const TexRec tr = sc.tex(hit.index);
+      if (tr.type >= 0 && (tr.opts & 3u)) {
+        const T4 tx = hit_texel(P, tr, hit);
+        if (tr.opts & 1u) {
+          const float a = tx.a;
+          c = mk(mixf(c.x, tx.r * tr.cmr, a), mixf(c.y, tx.g * tr.cmg, a), mixf(c.z, tx.b * tr.cmb, a));
+        }
+        if (tr.opts & 2u) {
+          const float a = tx.a;
+          e = mk(mixf(e.x, tx.r * tr.emr, a), mixf(e.y, tx.g * tr.emg, a), mixf(e.z, tx.b * tr.emb, a));
         }
       }
-      c = vmaxs(c, 0.001f);
-      float inside = -sgn(dot(rd, hit.n));
-      e = vmaxs(e, 0.001f);
-      if (mt.type == M_LIGHT) {
-        mask = mask * c;
-        float w = 1.0f;
-        if (flag(F_MIS) && !spec && flag(F_SAMPLE_LIGHTS) && depth > 0) {
-          v3 ld = normalize(hit.pos - ro);
-          w = power_heuristic(cos_pdf(ld, prev_nl), light_pdf(g, mt, ro));
-        }
-        acc = acc + (mask * e) * w;
-        break;
+    }
+    c = vmaxs(c, 0.001f);
+    float inside = -sgn(dot(rd, hit.n));
+    e = vmaxs(e, 0.001f);
+    if (mt.type == M_LIGHT) {
+      mask = mask * c;
+      float w = 1.0f;
+      if (flag(F_MIS) && !spec && flag(F_SAMPLE_LIGHTS) && depth > 0) {
+        v3 ld = normalize(hit.pos - ro);
+        w = power_heuristic(cos_pdf(ld, prev_nl), light_pdf(g, mt, ro));
       }
-      prev_nl = hit.n * inside;
+      acc = acc + (mask * e) * w;
+      return false;
+    }
+    prev_nl = hit.n * inside;
 
-      // ---- brdf(), 1804-1980
-      const v3 x = hit.pos;
-      const v3 nl = hit.n * inside;
-      const float bounce = (float)depth;
-      v3 rdir;
-      {
-        float s = nc_seed4(seed, 7.1f, fr, 5681.123f, bounce, 92.13f);
-        rdir = flag(F_BIASED) ? sample_cosine(nl, s) : sample_cone(nl, 1.0f, s);
-      }
-      const float ncr = 1.00029f;
-      float nt_eff = fabsf(mt.nt);
-      if constexpr (SPECTRAL) {
-        if (flag(F_SPECTRAL) && mt.nt < 0.0f) nt_eff = spectral_ior(hero, fabsf(mt.nt));
-      }
-      const int mtype = mt.type;
-      if (mtype == M_DIFF) {
+    // ---- brdf(), 1804-1980
+    const v3 x = hit.pos;
+    const v3 nl = hit.n * inside;
+    const float bounce = (float)depth;
+    v3 rdir;
+    {
+      float s = nc_seed4(seed, 7.1f, fr, 5681.123f, bounce, 92.13f);
+      rdir = flag(F_BIASED) ? sample_cosine(nl, s) : sample_cone(nl, 1.0f, s);
+    }
+    const float ncr = 1.00029f;
+    float nt_eff = fabsf(mt.nt);
+    if constexpr (SPECTRAL) {
+      if (flag(F_SPECTRAL) && mt.nt < 0.0f) nt_eff = spectral_ior(hero, fabsf(mt.nt));
+    }
+    const int mtype = mt.type;
+    if (mtype == M_DIFF) {
+      ro = x + nl * EPSILON;
+      rd = rdir;
+      mask = mask * c;
+      ++diff_b;
+      spec = false;
+    } else if (mtype == M_SPEC) {
+      ro = x + nl * EPSILON;
+      rd = normalize(e * rdir + reflect(rd, nl));
+      mask = mask * c;
+      ++spec_b;
+      spec = true;
+    } else if (mtype == M_REFR_FRESNEL || mtype == M_REFR_SCHLICK) {
+      float nnt = inside < 0.0f ? fdiv(nt_eff, ncr) : fdiv(ncr, nt_eff);
+      v3 tdir = refract(rd, nl, nnt);
+      if (length(tdir) == 0.0f) {  // total internal reflection
         ro = x + nl * EPSILON;
+        rd = normalize(e * rdir + reflect(rd, nl));
+        ++spec_b;
+        spec = true;
+      } else {
+        tdir = normalize(e * rdir + tdir);
+        float Re = mtype == M_REFR_FRESNEL ? fresnel(rd, nl, ncr, nt_eff, tdir) : schlick(rd, nl, ncr, nt_eff);
+        if (hash(seed) < Re) {
+          ro = x + nl * EPSILON;
+          rd = normalize(e * rdir + reflect(rd, nl));
+          ++spec_b;
+        } else {
+          ro = x - nl * EPSILON;
+          mask = mask * c;
+          rd = tdir;
+          ++scat_ev;
+        }
+        spec = true;
+      }
+    } else if (mtype == M_COAT) {
+      ro = x + nl * EPSILON;
+      if (hash(seed) < schlick(rd, nl, ncr, nt_eff)) {
+        rd = normalize(e * rdir + reflect(rd, nl));
+        ++spec_b;
+        spec = true;
+      } else {
         rd = rdir;
         mask = mask * c;
         ++diff_b;
         spec = false;
-      } else if (mtype == M_SPEC) {
-        ro = x + nl * EPSILON;
-        rd = normalize(e * rdir + reflect(rd, nl));
-        mask = mask * c;
-        ++spec_b;
-        spec = true;
-      } else if (mtype == M_REFR_FRESNEL || mtype == M_REFR_SCHLICK) {
-        float nnt = inside < 0.0f ? fdiv(nt_eff, ncr) : fdiv(ncr, nt_eff);
-        v3 tdir = refract(rd, nl, nnt);
-        if (length(tdir) == 0.0f) {  // total internal reflection
-          ro = x + nl * EPSILON;
-          rd = normalize(e * rdir + reflect(rd, nl));
-          ++spec_b;
-          spec = true;
-        } else {
-          tdir = normalize(e * rdir + tdir);
-          float Re = mtype == M_REFR_FRESNEL ? fresnel(rd, nl, ncr, nt_eff, tdir) : schlick(rd, nl, ncr, nt_eff);
-          if (hash(seed) < Re) {
-            ro = x + nl * EPSILON;
-            rd = normalize(e * rdir + reflect(rd, nl));
-            ++spec_b;
-          } else {
-            ro = x - nl * EPSILON;
-            mask = mask * c;
-            rd = tdir;
-            ++scat_ev;
-          }
-          spec = true;
-        }
-      } else if (mtype == M_COAT) {
-        ro = x + nl * EPSILON;
-        if (hash(seed) < schlick(rd, nl, ncr, nt_eff)) {
-          rd = normalize(e * rdir + reflect(rd, nl));
-          ++spec_b;
-          spec = true;
-        } else {
-          rd = rdir;
-          mask = mask * c;
-          ++diff_b;
-          spec = false;
-        }
       }
-      if (!spec && flag(F_CUBEMAP)) {  // environment NEE, 1887-1897
-        const float s = nc_addmul(seed, bounce, 965.325f);
-        const v3 sr = flag(F_BIASED) ? sample_cosine(nl, s) : sample_cone(nl, 1.0f, s);
-        Hit eh;
-        if (isect(x + nl * EPSILON, sr, eh) == INF_T) {
-          const T4 cm = cube_sample(P, sr);
-          acc = acc + mask * mk(cm.r, cm.g, cm.b);
-        }
-      }
-      if (!spec && flag(F_SAMPLE_LIGHTS)) acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;
-      // ---- end brdf
-
-      if (vmaxc(mask) < 0.01f) break;
-      if (diff_b >= C.max_diff() || spec_b >= C.max_spec() || 0 >= C.max_trans() || scat_ev >= C.max_scatter()) break;
     }
-    return acc;
+    if (!spec && flag(F_CUBEMAP)) {  // environment NEE, 1887-1897
+      const float s = nc_addmul(seed, bounce, 965.325f);
+      const v3 sr = flag(F_BIASED) ? sample_cosine(nl, s) : sample_cone(nl, 1.0f, s);
+      Hit eh;
+      if (isect(x + nl * EPSILON, sr, eh) == INF_T) {
+        const T4 cm = cube_sample(P, sr);
+        acc = acc + mask * mk(cm.r, cm.g, cm.b);
+      }
+    }
+    if (!spec && flag(F_SAMPLE_LIGHTS)) acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;
+    // ---- end brdf
+
+    if (vmaxc(mask) < 0.01f) return false;
+    if (diff_b >= C.max_diff() || spec_b >= C.max_spec() || 0 >= C.max_trans() || scat_ev >= C.max_scatter()) return false;
+    }
+    return ++ps.depth < C.max_bounces();
   }
 
-  // main(), raytracer.glsl:2111-2180: one sample of pixel (px, py) at `frame`
-  DEV v3 sample(int px, int py) {
+  DEV v3 radiance(v3 ro, v3 rd, float seed) {
+    Path ps{ro, rd, mk(0.f, 0.f, 0.f), mk(1.f, 1.f, 1.f), mk(0.f, 1.f, 0.f), seed, 0, true};
+    if (C.max_bounces() > 0)
+      while (step(ps)) {
+      }
+    return ps.acc;
+  }
+
+  // main() up to radiance(), raytracer.glsl:2111-2150: seed, hero wavelength
+  // and the camera ray of pixel (px, py) at `frame`
+  DEV void begin(Path &ps, int px, int py) {
     fcx = (float)px + 0.5f;
     fcy = (float)py + 0.5f;
     diff_b = spec_b = scat_ev = 0;
@@ -1503,11 +1524,24 @@ struct Integrator {
       rd = normalize(fp);  // aperture 0: randomAperturePos == 0 exactly
     }
     if (RESTIR) fin = empty_res();
-    v3 col = radiance(ro, rd, seed);
+    ps = Path{ro, rd, mk(0.f, 0.f, 0.f), mk(1.f, 1.f, 1.f), mk(0.f, 1.f, 0.f), seed, 0, true};
+  }
+  // main() after radiance(): the spectral weighting (2152-2155)
+  DEV v3 finish(const Path &ps) {
+    v3 col = ps.acc;
     if constexpr (SPECTRAL) {
       if (flag(F_SPECTRAL)) col = col * wavelength_to_rgb(hero);
     }
     return col;
+  }
+  // main(), raytracer.glsl:2111-2180: one sample of pixel (px, py) at `frame`
+  DEV v3 sample(int px, int py) {
+    Path ps;
+    begin(ps, px, py);
+    if (C.max_bounces() > 0)
+      while (step(ps)) {
+      }
+    return finish(ps);
   }
 };
 
@@ -1516,6 +1550,22 @@ struct Integrator {
 DEV int image_row(const LaunchParams &P, int r) {
   const int b = r / P.band;
   return (b * P.n_shards + P.shard) * P.band + (r - b * P.band);
+}
+
+// accumulator update of one sample: prev + sample (raytracer.glsl:2168) or, in
+// RENDER_MODE 1, mix(previousFrame, currentFrame, 1/u_temporalFrames) (2159-2165)
+template <class It>
+DEV void accumulate(const It &it, const LaunchParams &P, float4 &a, v3 s) {
+  if (it.flag(F_ANIM)) {
+    a.x = mixf(a.x, s.x, P.ema_alpha);
+    a.y = mixf(a.y, s.y, P.ema_alpha);
+    a.z = mixf(a.z, s.z, P.ema_alpha);
+  } else {
+#pragma clang fp contract(off)
+    a.x += opq(s.x);
+    a.y += opq(s.y);
+    a.z += opq(s.z);
+  }
 }
 
 // The pass kernel body: 16x16 pixel tile per 256-thread workgroup (four 8x8
@@ -1541,21 +1591,36 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       v3 s = it.sample(px, py);
       P.samples[(size_t)f * plane + lp] = make_float4(s.x, s.y, s.z, 0.f);
     }
+  } else if constexpr (!RESTIR && !COUNT) {
+    // Path regeneration: the lane runs its pixel's passes back to back as ONE
+    // loop of bounce steps; when its path ends it accumulates the sample and
+    // starts the next pass at once instead of idling until the longest path
+    // of its wave has finished.  Each pixel's samples are still produced and
+    // summed in pass order, so the result is bit-identical to the plain loop.
+    float4 a = P.accum[pix];
+    if (P.nframes > 0) {
+      typename Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::Path ps;
+      int f = 0;
+      it.frame = P.frame0;
+      it.begin(ps, px, py);
+      bool alive = cfg.max_bounces() > 0;
+      while (true) {
+        if (alive) alive = it.step(ps);
+        if (!alive) {
+          accumulate(it, P, a, it.finish(ps));
+          if (++f >= P.nframes) break;
+          it.frame = P.frame0 + (uint32_t)f;
+          it.begin(ps, px, py);
+          alive = cfg.max_bounces() > 0;
+        }
+      }
+    }
+    P.accum[pix] = a;
   } else {
     float4 a = P.accum[pix];
     for (int f = 0; f < P.nframes; ++f) {
       it.frame = P.frame0 + (uint32_t)f;
-      v3 s = it.sample(px, py);
-      if (it.flag(F_ANIM)) {  // RENDER_MODE 1: mix(previousFrame, currentFrame, alpha), 2159-2165
-        a.x = mixf(a.x, s.x, P.ema_alpha);
-        a.y = mixf(a.y, s.y, P.ema_alpha);
-        a.z = mixf(a.z, s.z, P.ema_alpha);
-      } else {
-#pragma clang fp contract(off)
-        a.x += opq(s.x);
-        a.y += opq(s.y);
-        a.z += opq(s.z);
-      }
+      accumulate(it, P, a, it.sample(px, py));
     }
     P.accum[pix] = a;
   }
