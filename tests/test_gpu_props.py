@@ -66,10 +66,10 @@ def test_state_errors(cfgs, gpu_required):
     with pytest.raises(rt0.Rt0Error) as e:
         r.render(1, 1)
     assert e.value.code == -4
-    cfg = rt0.parse_config([], ["const lowp int RENDER_MODE = 1;"])  # animated mode
+    cfg = rt0.parse_config([], ["const lowp int RENDER_MODE = 2;"])  # the shader knows modes 0 and 1
     with pytest.raises(rt0.Rt0Error) as e:
         r.set_config(cfg)
-    assert e.value.code == -3
+    assert e.value.code == -1
     with pytest.raises(ValueError):  # six square RGB faces
         r.set_cubemap([np.zeros((4, 4, 3), np.uint8)] * 5)
     with pytest.raises(ValueError):
