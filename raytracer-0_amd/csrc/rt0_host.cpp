@@ -83,6 +83,10 @@ struct rt0_ctx {
   int cube_size = 0;
   SceneDev host_scene;   // what d_scene holds (also the JIT's scene data)
   bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
+  // the scene-specialised kernel of the current (scene, config): looked up once
+  // per change instead of regenerating and hashing its source on every render
+  void *jit_fn = nullptr;
+  bool jit_dirty = true;
   std::string jit_err;
   std::string err;
 };
@@ -193,6 +197,7 @@ int rt0_set_config(rt0_ctx *c, const rt0_config *cfg) {
   if (cfg->render_mode != 0 && cfg->render_mode != 1) return fail(c, RT0_E_ARG, "RENDER_MODE must be 0 or 1");
   if (cfg->max_bounces < 0 || cfg->marching_steps < 0) return fail(c, RT0_E_ARG, "negative loop bound");
   c->cfg = *cfg;
+  c->jit_dirty = true;
   return RT0_OK;
 }
 
@@ -207,6 +212,7 @@ static int upload_scene(rt0_ctx *c) {
                                     (int)c->lights.size());
   HIPCHK(c, hipSetDevice(c->device));
   c->host_scene = s;
+  c->jit_dirty = true;
   HIPCHK(c, hipMemcpyAsync(c->d_scene, &s, sizeof s, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->has_scene = true;
@@ -579,8 +585,12 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   // counting instance is always the ahead-of-time one
   void *jit_fn = nullptr;
   if (c->use_jit && !c->counting) {
-    int rc = rt0h::jit_get(c->host_scene, rt0h::make_jit_key(c->cfg, c->n_sdfs), c->device, &jit_fn, c->jit_err);
-    if (rc != RT0_OK) return fail(c, rc, c->jit_err);
+    if (c->jit_dirty || !c->jit_fn) {
+      int rc = rt0h::jit_get(c->host_scene, rt0h::make_jit_key(c->cfg, c->n_sdfs), c->device, &c->jit_fn, c->jit_err);
+      if (rc != RT0_OK) return fail(c, rc, c->jit_err);
+      c->jit_dirty = false;
+    }
+    jit_fn = c->jit_fn;
   }
   auto launch = [&](const LaunchParams &lp, unsigned gz) -> hipError_t {
     if (jit_fn)
@@ -630,7 +640,8 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     // rt0_sum_kernel adds them in frame order (bit-identical accumulation).
     const long waves = (long)grid.x * grid.y * 4;
     static const long target = getenv("RT0_TARGET_WAVES") ? atol(getenv("RT0_TARGET_WAVES")) : kChunkWaves;
-    const int want = (c->counting || waves >= kTargetWaves)
+    static const long min_waves = getenv("RT0_MIN_WAVES") ? atol(getenv("RT0_MIN_WAVES")) : kTargetWaves;
+    const int want = (c->counting || waves >= min_waves)
                          ? 1
                          : (int)std::min<long>(c->max_frames_per_launch, (target + waves - 1) / waves);
     for (int k = 0; k < n; k += c->max_frames_per_launch) {

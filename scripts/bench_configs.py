@@ -48,7 +48,7 @@ def main():
             gen = {"icosphere": M.icosphere, "wavy_icosphere": M.wavy_icosphere}[m["kind"]]
             r.set_model(k, *gen(m["level"]))
         tris, depth = r.model_info()
-        r.render(1, 1)  # JIT compile + BVH build + first touch
+        r.render(1, spp)  # JIT compile + BVH build + scratch planes + first touch
         r.clear()
         kms = []
         t0 = time.perf_counter()
