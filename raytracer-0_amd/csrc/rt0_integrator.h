@@ -1572,6 +1572,7 @@ DEV void accumulate(const It &it, const LaunchParams &P, float4 &a, v3 s) {
 // wave tiles); each lane accumulates its pixel's passes in registers.
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  if constexpr (Scene::kStatic) Scene::stage();  // LDS copy of the scene records (before any early exit)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
   const int ly = (lane >> 3) + ((wave >> 1) << 3);
