@@ -98,7 +98,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // measured on the bench scene: 5.86 ms with the LDS copies vs 5.75 ms without
   // (more code, 65 VGPRs = one wave less per SIMD), so off by default
   static const bool lds = getenv("RT0_JIT_LDS") ? atoi(getenv("RT0_JIT_LDS")) != 0 : false;  // A/B knob
-  if (!lds) o << "#define __builtin_constant_p(x) 1\n";  // every lookup reads the constant segment
+  // RT0_LDS_IDX(i): this lookup goes to the LDS copy (never when staging is off)
+  o << (lds ? "#define RT0_LDS_IDX(i) (!__builtin_constant_p(i))\n" : "#define RT0_LDS_IDX(i) false\n");
   o << "__shared__ GeomRec sJitGeom[" << ntl << "];\n__shared__ MatRec sJitMat[" << ntl << "];\n";
   if (s.any_tex) o << "__shared__ TexRec sJitTex[" << ntl << "];\n";
   o << "struct JitScene {\n"
@@ -111,21 +112,22 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
        "  __device__ static constexpr int n_sdfs() { return kSdfs; }\n"
        "  __device__ static constexpr int n_models() { return kModels; }\n"
        "  __device__ static constexpr int n_lights() { return kLights; }\n"
-       "  __device__ static GeomRec geom(int i) { return __builtin_constant_p(i) ? kJitGeom[i] : sJitGeom[i]; }\n"
-       "  __device__ static MatRec mat(int i) { return __builtin_constant_p(i) ? kJitMat[i] : sJitMat[i]; }\n"
+       "  __device__ static GeomRec geom(int i) { return RT0_LDS_IDX(i) ? sJitGeom[i] : kJitGeom[i]; }\n"
+       "  __device__ static MatRec mat(int i) { return RT0_LDS_IDX(i) ? sJitMat[i] : kJitMat[i]; }\n"
        "  __device__ static float j3(int i) { return kJitJ3[i]; }\n"
        "  __device__ static int sdf_kind(int i) { return kJitSdfKind[i]; }\n"
        "  __device__ static int light(int i) { return kJitLights[i]; }\n"
-    << (s.any_tex ? "  __device__ static TexRec tex(int i) { return __builtin_constant_p(i) ? kJitTex[i] : sJitTex[i]; }\n"
+    << (s.any_tex ? "  __device__ static TexRec tex(int i) { return RT0_LDS_IDX(i) ? sJitTex[i] : kJitTex[i]; }\n"
                   : "  __device__ static TexRec tex(int i) { return kJitTex[i]; }\n")
-    << "  __device__ static void stage() {\n"
-       "    for (int k = threadIdx.x; k < " << ntl << "; k += blockDim.x) {\n"
-       "      sJitGeom[k] = kJitGeom[k];\n"
-       "      sJitMat[k] = kJitMat[k];\n"
-    << (s.any_tex ? "      sJitTex[k] = kJitTex[k];\n" : "")
-    << "    }\n"
-       "    __syncthreads();\n"
-       "  }\n"
+    << "  __device__ static void stage() {\n";
+  if (lds)
+    o << "    for (int k = threadIdx.x; k < " << ntl << "; k += blockDim.x) {\n"
+         "      sJitGeom[k] = kJitGeom[k];\n"
+         "      sJitMat[k] = kJitMat[k];\n"
+      << (s.any_tex ? "      sJitTex[k] = kJitTex[k];\n" : "")
+      << "    }\n"
+         "    __syncthreads();\n";
+  o << "  }\n"
        "  __device__ static constexpr bool any_tex() { return "
     << (s.any_tex ? "true" : "false") << "; }\n"
        "};\n";
