@@ -168,3 +168,40 @@ console.log(vp.passes);
     r.clear()
     r.render(1, 2)
     assert not np.array_equal(r.read_accum(), b)
+
+
+@pytest.mark.gpu
+def test_js_animated_mode_matches_python(cfgs, gpu_required, tmp_path):
+    """setAnimatedMode(true) (index.js:940-958) + render(n, timeMs) in JS: the
+    cycling pass counter (1..2T+1, then T+1..) and the RENDER_MODE 1 running
+    average equal the Python host's, bit for bit."""
+    cfg = [c for c in cfgs["configs"] if c["name"] == "anim_restir_demo"][0]
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    cam = cfg["camera"]
+    out = tmp_path / "acc.bin"
+    src = """
+const fs = require('fs');
+const v = require(%r);
+const vp = new v.GlslViewport(null, {width: 48, height: 48});
+vp.setAnimatedMode(true);
+vp.scene = %s; vp.sdf_meshes = %s; vp.defines[1] = '//#define USE_PROCEDURAL_SKY';
+vp.camera.origin = new v.Vector3(%r, %r, %r); vp.camera.lookat = new v.Vector3(%r, %r, %r); vp.camera.fov = %r;
+const seen = [];
+for (let k = 0; k < 14; k++) { vp.render(1, 1000 + 50 * k); seen.push(vp.passes); }
+fs.writeFileSync(%r, Buffer.from(vp.accumulator().buffer));
+console.log(JSON.stringify(seen));
+""" % (VIEWPORT, json.dumps(scene), json.dumps(sdf), *cam["origin"], *cam["lookat"], cam["fov"], str(out))
+    seen = json.loads(run_node(src))
+    assert seen == list(range(1, 12)) + [6, 7, 8]
+    a = np.fromfile(str(out), np.float32).reshape(48, 48, 4)
+    vp = rt0.GlslViewport(opts={"width": 48, "height": 48})
+    vp.setAnimatedMode(True)
+    vp.scene, vp.sdf_meshes = scene, sdf
+    vp.defines[1] = "//#define USE_PROCEDURAL_SKY"
+    vp.camera["origin"], vp.camera["lookat"] = rt0.Vector3(*cam["origin"]), rt0.Vector3(*cam["lookat"])
+    vp.camera["fov"] = cam["fov"]
+    for k in range(14):
+        vp.render(1, time_ms=1000 + 50 * k)
+    b = vp.accumulator()
+    assert np.isfinite(b).all() and np.abs(b).sum() > 0
+    assert np.array_equal(a, b), (a != b).any(-1).mean()
