@@ -10,8 +10,10 @@ i.e. 64 GlslViewport.render() calls) with scene + accumulator resident in HBM.
 
 N GPUs (one process per GPU, torch.distributed.run): the image is split into
 16-row bands dealt round-robin over ranks (rt0_set_shard); each rank renders
-its bands into a torch-owned accumulator and rank 0 gathers the bands over
-RCCL inside the timed region ("strong" scaling: total work fixed).
+its bands straight into a band-packed torch buffer (rt0_set_accum_buffer_compact:
+the RCCL send buffer as it stands), and rank 0 gathers the bands over RCCL and
+reorders them with one index_copy_ inside the timed region ("strong" scaling:
+total work fixed).
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
 `roofline` (VALU FP32: algorithmic FLOP/sample from SURVEY 8d x counted events,
@@ -128,19 +130,25 @@ def main():
     band = 16
     nb = H // band
     owned = [b for b in range(nb) if b % world == rank]
-    acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
-    r.set_accum_buffer(acc.data_ptr())
     if world > 1:
+        # each rank renders its 16-row bands straight into a band-packed
+        # accumulator (rt0_set_accum_buffer_compact) that is the RCCL send buffer
         import rt0.shard as shard
         r.set_shard(rank, world, band)
-        image = torch.zeros((H, W, 4), device=acc.device) if rank == 0 else None
+        gather = shard.BandGather(H, W, rank, world, band, "cuda:%d" % local)
+        acc = gather.acc
+        rows = r.set_accum_buffer_compact(acc.data_ptr())
+        assert rows <= acc.shape[0], (rows, acc.shape)
+    else:
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
+        r.set_accum_buffer(acc.data_ptr())
 
     def step(frame0):
         acc.zero_()
         torch.cuda.synchronize()
         r.render(frame0, SPP)  # synchronous: returns after the kernels finished
         if world > 1:
-            shard.gather_image(acc, rank, world, band, image=image)  # RCCL gather of the HDR bands
+            gather.gather()  # RCCL gather of the HDR bands + one reorder on rank 0
 
     for i in range(args.warmup):
         step(1)

@@ -243,6 +243,12 @@ int rt0_device_accum(rt0_ctx *ctx, void **dptr, void **stream);
  * torch tensor that RCCL gathers) as the accumulator; NULL restores the
  * context's own buffer.  Contents are not cleared. */
 int rt0_set_accum_buffer(rt0_ctx *ctx, void *dptr);
+/* Same with a band-packed layout for multi-GPU sharding (rt0_set_shard): the
+ * buffer holds only this shard's bands, in band order ((*rows) x W x 4 f32,
+ * *rows = owned bands x band_rows), so it is the send buffer of the gather
+ * as it stands.  Not for ReSTIR (RT0_E_UNSUPPORTED).  rt0_read_accum /
+ * rt0_write_accum / rt0_clear then cover these rows. */
+int rt0_set_accum_buffer_compact(rt0_ctx *ctx, void *dptr, int *rows);
 
 /* Sharded ReSTIR: the reservoir textures of index.js:149-163
  * (units 7-12) and their swap chain (swapReSTIRBuffers, index.js:795-820).

@@ -115,6 +115,7 @@ struct LaunchParams {
   int32_t n_band_rows;            // rows covered by this launch's grid (host-computed)
   const SceneDev *scene;
   float4 *accum;
+  int32_t compact;  // accum holds only this shard's bands: row r of the band-compressed grid
   const float4 *rin[6];  // spatial main/aux, history1 main/aux, history2 main/aux
   float4 *rout_main, *rout_aux;
   unsigned long long *counters;  // 5 x u64 (counting instance only)

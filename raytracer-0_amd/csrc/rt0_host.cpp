@@ -60,7 +60,15 @@ struct rt0_ctx {
   float cam_pos[3] = {0.f, 0.f, 2.8f}, cam_look[3] = {0.f, 0.f, -1.f}, cam_params[3] = {50.f, 0.f, 3.5f};
   float4 *d_accum = nullptr;
   float4 *ext_accum = nullptr;  // caller-owned accumulator (rt0_set_accum_buffer)
+  bool compact = false;         // ext_accum holds only this shard's bands (rt0_set_accum_buffer_compact)
   float4 *acc() const { return ext_accum ? ext_accum : d_accum; }
+  // rows of this shard's bands: the band-compressed grid height
+  int owned_rows() const {
+    const int total = (H + band - 1) / band;
+    return (total / n_shards + (shard < total % n_shards ? 1 : 0)) * band;
+  }
+  // rows the accumulator buffer holds
+  int accum_rows() const { return compact ? owned_rows() : H; }
   float4 *d_restir[R_COUNT] = {};
   uchar4 *d_tonemap = nullptr;
   unsigned long long *d_counters = nullptr;
@@ -126,7 +134,7 @@ static int alloc_buffers(rt0_ctx *c, int w, int h) {
 
 static int clear_buffers(rt0_ctx *c) {
   size_t n = (size_t)c->W * c->H * sizeof(float4);
-  HIPCHK(c, hipMemsetAsync(c->acc(), 0, n, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->acc(), 0, (size_t)c->W * c->accum_rows() * sizeof(float4), c->stream));
   for (auto &p : c->d_restir) HIPCHK(c, hipMemsetAsync(p, 0, n, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return RT0_OK;
@@ -531,6 +539,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.tris = c->d_tris;
   p.n_tris = c->n_tris;
   p.accum = c->acc();
+  p.compact = c->compact ? 1 : 0;
   p.counters = c->d_counters;
   p.ema_alpha = 1.0f / (float)c->temporal_frames;  // raytracer.glsl:2164
   if (c->n_shards > 1) {  // one contiguous block per shard (checked for ReSTIR in render_impl)
@@ -714,7 +723,7 @@ int rt0_read_accum(rt0_ctx *c, float *out) {
   if (!c || !out) return RT0_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(out, c->acc(), (size_t)c->W * c->H * sizeof(float4), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(out, c->acc(), (size_t)c->W * c->accum_rows() * sizeof(float4), hipMemcpyDeviceToHost));
   return RT0_OK;
 }
 
@@ -722,7 +731,7 @@ int rt0_write_accum(rt0_ctx *c, const float *in) {
   if (!c || !in) return RT0_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(c->acc(), in, (size_t)c->W * c->H * sizeof(float4), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(c->acc(), in, (size_t)c->W * c->accum_rows() * sizeof(float4), hipMemcpyHostToDevice));
   return RT0_OK;
 }
 
@@ -738,6 +747,7 @@ int rt0_resize(rt0_ctx *c, int w, int h) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   free_buffers(c);
   c->ext_accum = nullptr;  // a caller buffer has the old size
+  c->compact = false;
   int rc = alloc_buffers(c, w, h);
   if (rc != RT0_OK) return rc;
   return clear_buffers(c);
@@ -805,6 +815,17 @@ int rt0_set_jit(rt0_ctx *c, int enable) {
 int rt0_set_accum_buffer(rt0_ctx *c, void *dptr) {
   if (!c) return RT0_E_ARG;
   c->ext_accum = (float4 *)dptr;
+  c->compact = false;
+  return RT0_OK;
+}
+
+int rt0_set_accum_buffer_compact(rt0_ctx *c, void *dptr, int *rows) {
+  if (!c || !dptr) return RT0_E_ARG;
+  if (c->cfg.defines & RT0_USE_RESTIR)
+    return fail(c, RT0_E_UNSUPPORTED, "ReSTIR shards keep a full-size accumulator (contiguous row blocks)");
+  c->ext_accum = (float4 *)dptr;
+  c->compact = true;
+  if (rows) *rows = c->owned_rows();
   return RT0_OK;
 }
 

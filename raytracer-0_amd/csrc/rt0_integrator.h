@@ -1582,7 +1582,8 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const int py = image_row(P, r);
   if (py >= P.height) return;
   Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT> it(P, sc, cfg);
-  const size_t pix = (size_t)py * P.width + px;
+  const size_t pix = (size_t)py * P.width + px;                        // image pixel (ReSTIR planes)
+  const size_t apix = P.compact ? (size_t)r * P.width + px : pix;      // accumulator pixel
   if (!RESTIR && P.samples) {  // frame-chunked: samples out, rt0_sum_kernel accumulates
     const int f0 = (int)blockIdx.z * P.frame_chunk;
     const int f1 = min(P.nframes, f0 + P.frame_chunk);
@@ -1598,7 +1599,7 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     // starts the next pass at once instead of idling until the longest path
     // of its wave has finished.  Each pixel's samples are still produced and
     // summed in pass order, so the result is bit-identical to the plain loop.
-    float4 a = P.accum[pix];
+    float4 a = P.accum[apix];
     if (P.nframes > 0) {
       typename Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::Path ps;
       int f = 0;
@@ -1616,14 +1617,14 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
         }
       }
     }
-    P.accum[pix] = a;
+    P.accum[apix] = a;
   } else {
-    float4 a = P.accum[pix];
+    float4 a = P.accum[apix];
     for (int f = 0; f < P.nframes; ++f) {
       it.frame = P.frame0 + (uint32_t)f;
       accumulate(it, P, a, it.sample(px, py));
     }
-    P.accum[pix] = a;
+    P.accum[apix] = a;
   }
   if constexpr (RESTIR) {
     if (P.rout_main == nullptr || P.rout_aux == nullptr) return;
@@ -1654,7 +1655,7 @@ DEV void sum_body(const LaunchParams &P) {
   if (px >= P.width || r >= P.n_band_rows) return;
   const int py = image_row(P, r);
   if (py >= P.height) return;
-  const size_t pix = (size_t)py * P.width + px;
+  const size_t pix = P.compact ? (size_t)r * P.width + px : (size_t)py * P.width + px;
   const size_t plane = (size_t)P.n_band_rows * P.width, lp = (size_t)r * P.width + px;
   float4 a = P.accum[pix];
   for (int f = 0; f < P.nframes; ++f) {

@@ -28,7 +28,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_set_scene_glsl", "rt0_set_scene", "rt0_parse_scene_glsl", "rt0_get_scene", "rt0_set_camera", "rt0_render",
            "rt0_render_async", "rt0_sync", "rt0_read_accum", "rt0_write_accum", "rt0_clear", "rt0_resize",
            "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
-           "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_restir_buffers", "rt0_device_restir",
+           "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_accum_buffer_compact", "rt0_set_restir_buffers", "rt0_device_restir",
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
            "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read",
@@ -72,6 +72,15 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("librt0.so not built (run `make -C raytracer-0_amd` or __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7, and
+    # if librt0 bound /opt/rocm's copy first, torch.cuda would later find "No
+    # HIP GPUs" (two runtimes over one device).  Importing torch first (when
+    # it is installed) makes librt0 resolve to the runtime torch loaded, so
+    # torch tensors (sharded accumulators, RCCL buffers) and librt0 share it.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.POINTER
     c_void_p, c_int, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
@@ -110,6 +119,7 @@ def lib():
         "rt0_set_shard": (c_int, [c_void_p, c_int, c_int, c_int]),
         "rt0_device_accum": (c_int, [c_void_p, P(c_void_p), P(c_void_p)]),
         "rt0_set_accum_buffer": (c_int, [c_void_p, c_void_p]),
+        "rt0_set_accum_buffer_compact": (c_int, [c_void_p, c_void_p, P(c_int)]),
         "rt0_set_restir_buffers": (c_int, [c_void_p, P(c_void_p)]),
         "rt0_device_restir": (c_int, [c_void_p, c_int, P(c_void_p), P(c_void_p)]),
         "rt0_set_halo": (c_int, [c_void_p, c_int]),
@@ -468,6 +478,13 @@ class Renderer:
     def set_accum_buffer(self, dptr):
         """Use a caller-owned device buffer (e.g. torch tensor .data_ptr()) as accumulator."""
         self._chk(lib().rt0_set_accum_buffer(self.h, ctypes.c_void_p(dptr) if dptr else None))
+
+    def set_accum_buffer_compact(self, dptr):
+        """Band-packed caller-owned accumulator for a shard (after set_shard):
+        rows x W x 4 f32 holding only the owned bands; returns rows."""
+        rows = ctypes.c_int()
+        self._chk(lib().rt0_set_accum_buffer_compact(self.h, ctypes.c_void_p(dptr), ctypes.byref(rows)))
+        return rows.value
 
     def set_restir_buffers(self, dptrs):
         """Use 8 caller-owned W*H*4 f32 device planes (e.g. torch tensors) as the

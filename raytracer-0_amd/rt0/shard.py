@@ -70,6 +70,46 @@ def gather_image(acc, rank, world, band, image=None, bufs=None):
     return None
 
 
+class BandGather:
+    """The per-step gather for band-packed accumulators (rt0_set_accum_buffer_compact):
+    every rank renders straight into a [rows, W, 4] buffer holding only its
+    bands, which is the send buffer as it stands; rank 0 scatters the gathered
+    bands into the image with one index_copy_ over cached indices.  No packing,
+    no per-step allocation or host->device index upload."""
+
+    def __init__(self, H, W, rank, world, band, device, channels=4):
+        import torch
+        self.H, self.W, self.rank, self.world, self.band = H, W, rank, world, band
+        self.nb = (H + band - 1) // band
+        self.max_owned = (self.nb + world - 1) // world
+        self.rows = self.max_owned * band  # every rank's buffer has this many rows (RCCL needs equal sizes)
+        self.acc = torch.zeros((self.rows, W, channels), dtype=torch.float32, device=device)
+        if rank == 0:
+            self.bufs = [torch.empty_like(self.acc) for _ in range(world)]
+            src_slot, dst_band = [], []
+            for s in range(world):
+                for j, b in enumerate(owned_bands(s, world, self.nb)):
+                    src_slot.append(s * self.max_owned + j)
+                    dst_band.append(b)
+            self.src = torch.tensor(src_slot, device=device)
+            self.dst = torch.tensor(dst_band, device=device)
+            self.image = torch.zeros((self.nb * band, W, channels), dtype=torch.float32, device=device)
+
+    def gather(self):
+        """Collective; rank 0 returns the assembled [H, W, 4] image (a view of a
+        persistent buffer), the other ranks None."""
+        import torch
+        import torch.distributed as dist
+        if self.rank != 0:
+            dist.gather(self.acc, None, dst=0)
+            return None
+        dist.gather(self.acc, self.bufs, dst=0)
+        stacked = torch.stack(self.bufs).view(self.world * self.max_owned, self.band, self.W, -1)
+        img = self.image.view(self.nb, self.band, self.W, -1)
+        img.index_copy_(0, self.dst, stacked.index_select(0, self.src))
+        return self.image[:self.H]
+
+
 # ------------------------------------------------------------- sharded ReSTIR
 # ReSTIR's spatial pass reads the previous pass's reservoirs up to ~16 px away
 # (raytracer.glsl:1726-1760) and the temporal pass reads the history at a

@@ -135,3 +135,39 @@ def test_restir_halo_exchange_over_gloo(world, H, halo):
     assert all(p.exitcode == 0 for p in procs)
     res = dict(q.get(timeout=10) for _ in range(world))
     assert all(res.values()), res
+
+
+def _worker_compact(rank, world, port, H, W, band, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = _expected(H, W, band)
+        g = shard.BandGather(H, W, rank, world, band, "cpu")
+        nb = (H + band - 1) // band
+        # what a shard renders into its band-packed accumulator: its bands in order
+        for j, b in enumerate(shard.owned_bands(rank, world, nb)):
+            rows = full[b * band:(b + 1) * band]
+            g.acc[j * band:j * band + rows.shape[0]] = rows
+        for _ in range(2):  # the buffers are reused step after step
+            img = g.gather()
+        if rank == 0:
+            q.put(bool(torch.equal(img, full)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H", [(2, 64), (3, 80), (4, 64)])
+def test_band_packed_gather_reassembles_image(world, H):
+    """bench.py's multi-GPU step: band-packed accumulators -> one gather -> one
+    index_copy_ on rank 0 == the full image, bitwise (uneven ownership too)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_compact, args=(r, world, port, H, 24, 16, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=10) is True

@@ -38,6 +38,42 @@ def test_determinism_and_sharding_bitwise(cfgs, gpu_required):
     assert np.array_equal(parts, a)
 
 
+def test_band_packed_shards_bitwise(cfgs, gpu_required):
+    """bench.py's multi-GPU layout: each shard renders into a band-packed torch
+    buffer (rt0_set_accum_buffer_compact); BandGather's reorder of those
+    buffers == the single-GPU image, bit for bit (8 shards: the 1024^2 / 8
+    frame-chunked launches included)."""
+    import torch
+    import rt0.shard as shard
+    cfg = cfg_by_name(cfgs, "c2_cornell_mis_8")
+    H = W = 256
+    r = rt0.Renderer(W, H)
+    rt0.configure(r, cfg, cfgs)
+    r.render(1, 3)
+    a = r.read_accum()
+    for world in (3, 8):
+        nb = H // 16
+        max_owned = (nb + world - 1) // world
+        img = np.zeros_like(a)
+        for s in range(world):
+            rs = rt0.Renderer(W, H)
+            rt0.configure(rs, cfg, cfgs)
+            rs.set_shard(s, world, 16)
+            buf = torch.zeros((max_owned * 16, W, 4), dtype=torch.float32, device="cuda:0")
+            rows = rs.set_accum_buffer_compact(buf.data_ptr())
+            own = shard.owned_bands(s, world, nb)
+            assert rows == len(own) * 16
+            rs.render(1, 3)
+            torch.cuda.synchronize()
+            got = buf.cpu().numpy()
+            assert np.array_equal(rs.read_accum()[:rows], got[:rows])  # read_accum covers the packed rows
+            for j, b in enumerate(own):
+                img[b * 16:(b + 1) * 16] = got[j * 16:(j + 1) * 16]
+            assert not got[rows:].any()  # padding rows untouched
+            rs.close()
+        assert np.array_equal(img, a), world
+
+
 def test_odd_sizes_and_edges(cfgs, gpu_required):
     cfg = cfg_by_name(cfgs, "c1_cornell_cos")
     for w, h in ((1, 1), (17, 5), (130, 67)):
