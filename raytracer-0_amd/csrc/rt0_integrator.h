@@ -421,6 +421,9 @@ struct Geometry {
     int type = -1;
     float tmin = INF_T;
     const v3 m = mk(frcp(d.x), frcp(d.y), frcp(d.z));  // iBox's 1/r.d, hoisted (837)
+    // iBox's m*(centre - o) as m*centre - m*o: m*o once per ray, one FMA per
+    // axis and box (ulp-level, like the other contracted geometry)
+    const v3 mo = m * o;
     // Each candidate test is branch-free (v_cndmask selects): a lane never
     // waits on another lane's taken branch inside the mesh loop.  The box
     // normal of iBox (853-856) depends only on the winning box and its t, so
@@ -463,7 +466,7 @@ struct Geometry {
         type = ok ? (int)T_PLANE : type;
         hit.index = ok ? i : hit.index;
       } else if (g.type == T_BOX) {  // iBox, 836-851
-        v3 nv = m * (gp - o);
+        v3 nv = mk(__builtin_fmaf(m.x, gp.x, -mo.x), __builtin_fmaf(m.y, gp.y, -mo.y), __builtin_fmaf(m.z, gp.z, -mo.z));
         v3 k = vabs(m) * g.d0;
         v3 t1 = nv - k, t2 = nv + k;
         float tN = fmaxf(fmaxf(t1.x, t1.y), t1.z);
