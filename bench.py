@@ -219,6 +219,13 @@ def main():
                      "traffic_source": ("profiles/%s/pmc_summary.json" % PROFILE_ROUND) if pmc else None,
                      "valu_lane_utilisation": round(pmc["valu_lane_utilisation"], 4) if pmc and "valu_lane_utilisation"
                      in pmc else None,
+                     # wave64 VALU instruction = 2 SIMD cycles (transcendental 4,
+                     # MI355X_MICROARCH.md constants), over 1024 SIMDs x the live
+                     # kernel time at the nominal 2.4 GHz
+                     "valu_issue_utilisation": round(2.0 * (pmc["valu"]["SQ_INSTS_VALU"]
+                                                           + pmc["valu"]["SQ_INSTS_VALU_TRANS_F32"])
+                                                     / (1024 * kern_s * 2.4e9), 4)
+                     if pmc and "valu" in pmc and world == 1 else None,
                      "flop_per_sample": round(fps, 1),
                      "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3)
                                            for k in ("isect", "iter", "nee")},

@@ -55,6 +55,8 @@ def main():
         res["valu"] = v
         # active lanes per issued VALU instruction (1.0 = no divergence)
         res["valu_lane_utilisation"] = v["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * v["SQ_ACTIVE_INST_VALU"])
+        # (bench.py turns these into the VALU issue utilisation with its own live
+        # kernel time: counter collection itself slows the dispatches ~3x)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
