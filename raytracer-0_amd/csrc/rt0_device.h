@@ -71,7 +71,9 @@ struct BvhNode {
   float rz0, rx1, ry1, rz1;
   int32_t left, right, pad0, pad1;
 };
+#ifndef RT0_BVH_STACK
 #define RT0_BVH_STACK 48  // traversal stack entries per lane (LDS); the build checks the depth
+#endif
 
 struct SceneDev {
   int32_t n_meshes, n_sdfs, n_lights, n_total;

@@ -418,6 +418,7 @@ static int build_bvh(rt0_ctx *c) {
     return fail(c, RT0_E_UNSUPPORTED, "BVH depth " + std::to_string(depth) + " exceeds the traversal stack");
   c->n_tris = n;
   c->bvh_depth = depth;
+  c->jit_dirty = true;  // the scene-specialised kernel's traversal stack follows the depth
   return RT0_OK;
 }
 
@@ -595,7 +596,9 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   void *jit_fn = nullptr;
   if (c->use_jit && !c->counting) {
     if (c->jit_dirty || !c->jit_fn) {
-      int rc = rt0h::jit_get(c->host_scene, rt0h::make_jit_key(c->cfg, c->n_sdfs), c->device, &c->jit_fn, c->jit_err);
+      rt0h::JitKey key = rt0h::make_jit_key(c->cfg, c->n_sdfs);
+      key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
+      int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit_fn, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
       c->jit_dirty = false;
     }

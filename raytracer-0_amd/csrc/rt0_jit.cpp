@@ -58,8 +58,12 @@ static std::string strip_includes(const char *src) {
 std::string jit_source(const SceneDev &s, const JitKey &k) {
   std::ostringstream o;
   if (const char *x = getenv("RT0_JIT_EXTRA")) o << "// options: " << x << "\n";  // part of the cache key
-  o << "#define RT0_JIT 1\n"
-       "using __hip_internal::int32_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
+  o << "#define RT0_JIT 1\n";
+  // the LDS traversal stack sized to this tree (depth + 1 entries, rounded up to
+  // 8) instead of the ahead-of-time kernels' 48: 48 x 256 lanes x 4 B = 48 KiB
+  // per workgroup would cap a CU at three workgroups
+  if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
+  o << "using __hip_internal::int32_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
   o << strip_includes(rt0_jit_source_text);
   const int nt = s.n_total;
   o << "namespace rt0 {\n";
@@ -145,6 +149,15 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
   if (const char *w = getenv("RT0_JIT_WAVES_PER_EU"))  // tuning knob: occupancy target
     o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w) << "))) ";
+  // occupancy targets measured per kernel family (scripts/ab_configs.sh, ab_c5.sh):
+  // BVH traversal is load-latency bound -- C5 4096^2 129.9 ms (3 waves/SIMD:
+  // 131 VGPRs and a 48-entry LDS stack) -> 78.3 ms at 6; the ReSTIR kernel
+  // (C3) 9.71 -> 9.32 ms at 5; the quadric/SDF kernels already sit at <= 64
+  // VGPRs (8 waves) and are left alone
+  else if (s.n_models > 0)
+    o << "__attribute__((amdgpu_waves_per_eu(6))) ";
+  else if (k.restir)
+    o << "__attribute__((amdgpu_waves_per_eu(5))) ";
   o << "void rt0_jit_pass(const LaunchParams P) {\n"
        "  rt0::pass_body<rt0::JitScene, rt0::JitCfg, "
     << (k.restir ? "true" : "false") << ", " << (k.vol ? "true" : "false") << ", " << (k.sdf ? "true" : "false")

@@ -17,6 +17,7 @@ struct JitKey {
   int max_bounces, max_diff, max_spec, max_trans, max_scatter, marching_steps, restir_samples;
   float fudge;
   bool restir, vol, sdf, spectral;
+  int bvh_stack = 0;  // LDS traversal stack entries (BVH depth + 1) when the scene has models
 };
 
 std::string jit_source(const SceneDev &s, const JitKey &k);
