@@ -174,6 +174,11 @@ int rt0_render(rt0_ctx *ctx, uint32_t first_frame, int n_passes, float time_ms);
 /* Asynchronous variant on the context's stream; rt0_sync() waits. */
 int rt0_render_async(rt0_ctx *ctx, uint32_t first_frame, int n_passes, float time_ms);
 int rt0_sync(rt0_ctx *ctx);
+/* gl.viewport of the passes (tile rendering: index.js:379, updateTile
+ * 761-792): only pixels x in [x, x+w), y in [y, y+h) (row 0 = bottom) are
+ * rendered, the rest of the accumulator is left untouched; clipped to the
+ * canvas.  w or h <= 0 restores the whole canvas.  Not with rt0_set_shard. */
+int rt0_set_viewport(rt0_ctx *ctx, int x, int y, int w, int h);
 /* u_temporalFrames (GlslViewport.temporalFrames, index.js:236; default 5):
  * the RENDER_MODE 1 running-average length. */
 int rt0_set_temporal_frames(rt0_ctx *ctx, int n);

@@ -115,6 +115,9 @@ struct LaunchParams {
   int32_t restir_samples;
   int32_t shard, n_shards, band;  // row-band sharding
   int32_t n_band_rows;            // rows covered by this launch's grid (host-computed)
+  // gl.viewport rectangle of the pass (tile rendering, index.js:761-792):
+  // columns [vp_x0, vp_x1) x band rows [vp_y0, vp_y1); the whole canvas by default
+  int32_t vp_x0, vp_y0, vp_x1, vp_y1;
   const SceneDev *scene;
   float4 *accum;
   int32_t compact;  // accum holds only this shard's bands: row r of the band-compressed grid

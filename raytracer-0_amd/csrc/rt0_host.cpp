@@ -73,7 +73,8 @@ struct rt0_ctx {
   uchar4 *d_tonemap = nullptr;
   unsigned long long *d_counters = nullptr;
   bool counting = false;
-  int temporal_frames = 5;  // GlslViewport.temporalFrames (index.js:236) -> u_temporalFrames
+  int temporal_frames = 5;
+  int vp[4] = {0, 0, 0, 0};  // gl.viewport (x, y, w, h); w or h <= 0 = whole canvas  // GlslViewport.temporalFrames (index.js:236) -> u_temporalFrames
   uint64_t counters[5] = {};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
@@ -528,6 +529,16 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   int total_bands = (c->H + c->band - 1) / c->band;
   int owned = total_bands / c->n_shards + (c->shard < total_bands % c->n_shards ? 1 : 0);
   p.n_band_rows = owned * c->band;
+  p.vp_x0 = 0;
+  p.vp_y0 = 0;
+  p.vp_x1 = c->W;
+  p.vp_y1 = p.n_band_rows;
+  if (c->vp[2] > 0 && c->vp[3] > 0) {  // clipped to the canvas like gl.viewport's scissor-free draw
+    p.vp_x0 = std::max(0, std::min(c->W, c->vp[0]));
+    p.vp_y0 = std::max(0, std::min(c->H, c->vp[1]));
+    p.vp_x1 = std::max(p.vp_x0, std::min(c->W, c->vp[0] + c->vp[2]));
+    p.vp_y1 = std::max(p.vp_y0, std::min(c->H, c->vp[1] + c->vp[3]));
+  }
   p.scene = c->d_scene;
   for (int u = 0; u < RT0_TEX_UNITS; u++) {
     p.tex_img[u] = c->d_tex[u];
@@ -590,7 +601,14 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     return RT0_OK;
   }
   const int variant = choose_variant(c);
-  dim3 grid((c->W + 15) / 16, (p.n_band_rows + 15) / 16);
+  if (c->n_shards > 1 && c->vp[2] > 0 && c->vp[3] > 0)
+    return fail(c, RT0_E_UNSUPPORTED, "a viewport (tile rendering) and pixel sharding do not combine");
+  if (p.vp_x1 <= p.vp_x0 || p.vp_y1 <= p.vp_y0) {  // empty viewport: nothing to draw
+    c->last_ms = 0.f;
+    c->last_launches = 0;
+    return RT0_OK;
+  }
+  dim3 grid((p.vp_x1 - p.vp_x0 + 15) / 16, (p.vp_y1 - p.vp_y0 + 15) / 16);
   // scene-specialised kernel (compiled once per scene/config, cached); the
   // counting instance is always the ahead-of-time one
   void *jit_fn = nullptr;
@@ -701,6 +719,15 @@ int rt0_render(rt0_ctx *c, uint32_t first, int n, float time_ms) { return render
 
 int rt0_render_async(rt0_ctx *c, uint32_t first, int n, float time_ms) {
   return render_impl(c, first, n, time_ms, false);
+}
+
+int rt0_set_viewport(rt0_ctx *c, int x, int y, int w, int h) {
+  if (!c) return RT0_E_ARG;
+  c->vp[0] = x;
+  c->vp[1] = y;
+  c->vp[2] = w;
+  c->vp[3] = h;
+  return RT0_OK;
 }
 
 int rt0_set_temporal_frames(rt0_ctx *c, int n) {

@@ -1579,9 +1579,9 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
   const int ly = (lane >> 3) + ((wave >> 1) << 3);
-  const int px = blockIdx.x * 16 + lx;
-  const int r = blockIdx.y * 16 + ly;
-  if (px >= P.width || r >= P.n_band_rows) return;
+  const int px = P.vp_x0 + blockIdx.x * 16 + lx;
+  const int r = P.vp_y0 + blockIdx.y * 16 + ly;
+  if (px >= P.vp_x1 || r >= P.vp_y1) return;
   const int py = image_row(P, r);
   if (py >= P.height) return;
   Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT> it(P, sc, cfg);
@@ -1653,9 +1653,9 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 // order -- the same sequential fp32 sum as the in-register loop above.
 DEV void sum_body(const LaunchParams &P) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int px = blockIdx.x * 16 + (lane & 7) + ((wave & 1) << 3);
-  const int r = blockIdx.y * 16 + (lane >> 3) + ((wave >> 1) << 3);
-  if (px >= P.width || r >= P.n_band_rows) return;
+  const int px = P.vp_x0 + blockIdx.x * 16 + (lane & 7) + ((wave & 1) << 3);
+  const int r = P.vp_y0 + blockIdx.y * 16 + (lane >> 3) + ((wave >> 1) << 3);
+  if (px >= P.vp_x1 || r >= P.vp_y1) return;
   const int py = image_row(P, r);
   if (py >= P.height) return;
   const size_t pix = P.compact ? (size_t)r * P.width + px : (size_t)py * P.width + px;

@@ -117,6 +117,11 @@ class GlslViewport {
     this.animatedScene = false;
     this.temporalFrames = 5;
     this.loadTime = Date.now();
+    // tile rendering (index.js:97-103, 379): 32x32 viewports visited by updateTile()
+    this.tile = [0, 0];
+    this.tile_size = [32, 32];
+    this.total_tiles = [Math.ceil(this.canvas.width / 32) - 1, Math.ceil(this.canvas.height / 32) - 1];
+    this.viewport = this.tile_rendering ? [0, 0, 32, 32] : [0, 0, this.canvas.width, this.canvas.height];
     this._h = addon.create(this.canvas.width, this.canvas.height, this.device);
     this._compiled = null;
     this.images = {};
@@ -188,6 +193,8 @@ class GlslViewport {
     n = n || 1;
     this.updateFrontTarget();
     const t = timeMs === undefined ? Date.now() - this.loadTime : timeMs;
+    const vp = this.tile_rendering ? this.viewport : [0, 0, this.canvas.width, this.canvas.height];
+    addon.setViewport(this._h, vp[0], vp[1], vp[2], vp[3]);
     if (!this.animatedScene) {
       addon.render(this._h, this.passes + 1, n, t);
       this.passes += n;
@@ -209,6 +216,32 @@ class GlslViewport {
     this.canvas.width = this.canvas.height = size;
     addon.resize(this._h, size, size);
     this.passes = 0;
+    this.total_tiles = [Math.ceil(size / this.tile_size[0]) - 1, Math.ceil(size / this.tile_size[1]) - 1];
+  }
+
+  // index.js:761-792: the next 32x32 viewport (row-major, bottom-up); passes
+  // restart at 0 and the viewer pauses after the last tile.  As in the
+  // reference, the edge tile's extent goes through tileMax, which IS
+  // tile_size, so it persists for the tiles that follow.
+  updateTile() {
+    const tileMax = this.tile_size;
+    this.passes = 0;
+    if (this.tile[0] < this.total_tiles[0]) {
+      this.tile[0]++;
+      if (this.tile[0] === this.total_tiles[0] - 1)
+        tileMax[0] = Math.abs(this.canvas.width - this.total_tiles[0] * this.tile_size[0]);
+    } else {
+      this.tile[0] = 0;
+      if (this.tile[1] < this.total_tiles[1]) {
+        this.tile[1]++;
+        if (this.tile[1] === this.total_tiles[1] - 1)
+          tileMax[1] = Math.abs(this.canvas.height - this.total_tiles[1] * this.tile_size[1]);
+      } else {
+        this.paused = true;
+        this.tile[1] = 0;
+      }
+    }
+    this.viewport = [this.tile[0] * this.tile_size[0], this.tile[1] * this.tile_size[1], tileMax[0], tileMax[1]];
   }
 
   // index.js:940-983

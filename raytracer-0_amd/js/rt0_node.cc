@@ -243,6 +243,16 @@ static napi_value Render(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+static napi_value SetViewport(napi_env env, napi_callback_info info) {
+  napi_value argv[5];
+  if (!get_args(env, info, 5, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  int32_t v[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) napi_get_value_int32(env, argv[1 + i], &v[i]);
+  RC_OR_THROW(rt0_set_viewport(c, v[0], v[1], v[2], v[3]));
+  return nullptr;
+}
+
 static napi_value SetTemporalFrames(napi_env env, napi_callback_info info) {
   napi_value argv[2];
   if (!get_args(env, info, 2, argv)) return nullptr;
@@ -474,6 +484,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"setCamera", nullptr, SetCamera, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"render", nullptr, Render, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setTemporalFrames", nullptr, SetTemporalFrames, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setViewport", nullptr, SetViewport, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readAccum", nullptr, ReadAccum, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"tonemap", nullptr, Tonemap, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"clear", nullptr, Clear, nullptr, nullptr, nullptr, napi_default, nullptr},

@@ -32,7 +32,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
            "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read",
-           "rt0_set_temporal_frames"]
+           "rt0_set_temporal_frames", "rt0_set_viewport"]
 
 TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
@@ -107,6 +107,7 @@ def lib():
         "rt0_render": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
         "rt0_render_async": (c_int, [c_void_p, ctypes.c_uint32, c_int, c_float]),
         "rt0_set_temporal_frames": (c_int, [c_void_p, c_int]),
+        "rt0_set_viewport": (c_int, [c_void_p, c_int, c_int, c_int, c_int]),
         "rt0_sync": (c_int, [c_void_p]),
         "rt0_read_accum": (c_int, [c_void_p, fp]),
         "rt0_write_accum": (c_int, [c_void_p, fp]),
@@ -419,6 +420,10 @@ class Renderer:
         """u_temporalFrames: RENDER_MODE 1 running-average length (index.js:236)."""
         self._chk(lib().rt0_set_temporal_frames(self.h, int(n)))
 
+    def set_viewport(self, x, y, w, h):
+        """gl.viewport of the following passes (tile rendering); w or h <= 0 = whole canvas."""
+        self._chk(lib().rt0_set_viewport(self.h, int(x), int(y), int(w), int(h)))
+
     def render_async(self, first_frame, n_passes, time_ms=0.0):
         self._chk(lib().rt0_render_async(self.h, first_frame, n_passes, time_ms))
 
@@ -568,6 +573,12 @@ class GlslViewport:
         self.animatedScene = False
         self.temporalFrames = 5
         self.loadTime = time.monotonic() * 1000.0  # u_time origin (index.js:986)
+        self.paused = opts.get("paused", False)
+        # tile rendering (index.js:97-103, 379): 32x32 viewports visited by updateTile()
+        self.tile = [0, 0]
+        self.tile_size = [32, 32]
+        self.total_tiles = [-(-self.width // 32) - 1, -(-self.height // 32) - 1]
+        self.viewport = [0, 0, 32, 32] if self.tile_rendering else [0, 0, self.width, self.height]
         self.renderer = Renderer(self.width, self.height, device)
         self._compiled = None
         self.images = {}
@@ -618,6 +629,8 @@ class GlslViewport:
         stays valid, and every pass sees u_time = ms since construction (or
         `time_ms`)."""
         self.updateFrontTarget()
+        vp = self.viewport if self.tile_rendering else [0, 0, self.width, self.height]
+        self.renderer.set_viewport(*vp)
         t = (time.monotonic() * 1000.0 - self.loadTime) if time_ms is None else float(time_ms)
         if not self.animatedScene:
             first = self.passes + 1
@@ -635,12 +648,35 @@ class GlslViewport:
         """index.js:822-880."""
         self.renderer.clear()
 
+    def updateTile(self):
+        """index.js:761-792: the next 32x32 viewport (row-major, bottom-up), passes
+        restart at 0, and the viewer pauses after the last tile.  As in the
+        reference, the edge tile's extent is written through `tile_max`, which is
+        the tile_size list itself, so it persists for the following tiles."""
+        tile_max = self.tile_size
+        self.passes = 0
+        if self.tile[0] < self.total_tiles[0]:
+            self.tile[0] += 1
+            if self.tile[0] == self.total_tiles[0] - 1:
+                tile_max[0] = abs(self.width - self.total_tiles[0] * self.tile_size[0])
+        else:
+            self.tile[0] = 0
+            if self.tile[1] < self.total_tiles[1]:
+                self.tile[1] += 1
+                if self.tile[1] == self.total_tiles[1] - 1:
+                    tile_max[1] = abs(self.height - self.total_tiles[1] * self.tile_size[1])
+            else:
+                self.paused = True
+                self.tile[1] = 0
+        self.viewport = [self.tile[0] * self.tile_size[0], self.tile[1] * self.tile_size[1], tile_max[0], tile_max[1]]
+
     def resize(self, v):
         """index.js:471-493: v selects 256..8192 square canvases."""
         size = {0: 256, 1: 512, 2: 1024, 3: 2048, 4: 4096, 5: 8192}.get(v, v)
         self.width = self.height = size
         self.renderer.resize(size, size)
         self.passes = 0
+        self.total_tiles = [-(-size // self.tile_size[0]) - 1, -(-size // self.tile_size[1]) - 1]
 
     def setAnimatedMode(self, is_animated):
         """index.js:940-983: animated constants (RENDER_MODE 1, ReSTIR) or the static ones."""

@@ -258,3 +258,47 @@ def test_texture_api(cfgs, gpu_required):
     r.clear()
     r.render(1, 1)
     assert np.array_equal(r.read_accum(), unbound)
+
+
+def test_viewport_renders_only_its_rectangle(cfgs, gpu_required):
+    """rt0_set_viewport (gl.viewport of tile rendering, index.js:379, 761-792):
+    pixels inside the rectangle equal the whole-canvas render bit for bit, the
+    rest stays zero; rectangles are clipped to the canvas."""
+    cfg = cfg_by_name(cfgs, "c2_cornell_mis_8")
+    W, H = 96, 80
+    r = rt0.Renderer(W, H)
+    rt0.configure(r, cfg, cfgs)
+    r.render(1, 3)
+    full = r.read_accum()
+    for x, y, w, h in ((0, 0, 32, 32), (32, 16, 40, 24), (70, 60, 64, 64), (5, 3, 1, 1)):
+        r.clear()
+        r.set_viewport(x, y, w, h)
+        r.render(1, 3)
+        got = r.read_accum()
+        inside = np.zeros((H, W), bool)
+        inside[y:min(H, y + h), x:min(W, x + w)] = True
+        assert np.array_equal(got[inside], full[inside]), (x, y, w, h)
+        assert not got[~inside].any()
+    r.set_viewport(0, 0, 0, 0)  # whole canvas again
+    r.clear()
+    r.render(1, 3)
+    assert np.array_equal(r.read_accum(), full)
+
+
+def test_glslviewport_tile_rendering(cfgs, gpu_required):
+    """tile_rendering: render() draws the current 32x32 tile, updateTile()
+    walks the tiles (passes restart), and after every tile had its passes the
+    accumulator is the whole-canvas image."""
+    vp = rt0.GlslViewport(None, {"width": 64, "height": 64, "tile_rendering": True})
+    vp.constants[0] = "const lowp int MAX_BOUNCES = 8;"
+    vp.constants[8] = "const bool use_mis = true;"
+    seen = []
+    while not vp.paused:
+        vp.render(2)
+        seen.append(tuple(vp.viewport))
+        vp.updateTile()
+    assert seen == [(0, 0, 32, 32), (32, 0, 32, 32), (0, 32, 32, 32), (32, 32, 32, 32)]
+    r = rt0.Renderer(64, 64)
+    rt0.configure(r, cfg_by_name(cfgs, "c2_cornell_mis_refcaps"), cfgs)
+    r.render(1, 2)
+    assert np.array_equal(vp.accumulator(), r.read_accum())

@@ -205,3 +205,26 @@ console.log(JSON.stringify(seen));
     b = vp.accumulator()
     assert np.isfinite(b).all() and np.abs(b).sum() > 0
     assert np.array_equal(a, b), (a != b).any(-1).mean()
+
+
+@pytest.mark.gpu
+def test_js_tile_walk_matches_python(gpu_required):
+    """updateTile() (index.js:761-792) in both hosts: the same viewport sequence
+    on a 96x80 canvas, including the reference's edge-tile quirk (the edge
+    extent is written through an alias of tile_size and persists)."""
+    src = """
+const v = require(%r);
+const vp = new v.GlslViewport(null, {width: 96, height: 80, tile_rendering: true});
+const seen = [];
+for (let k = 0; k < 12 && !vp.paused; k++) { seen.push(vp.viewport.slice()); vp.updateTile(); }
+console.log(JSON.stringify(seen));
+""" % VIEWPORT
+    js = json.loads(run_node(src))
+    vp = rt0.GlslViewport(None, {"width": 96, "height": 80, "tile_rendering": True})
+    py = []
+    for _ in range(12):
+        if vp.paused:
+            break
+        py.append(list(vp.viewport))
+        vp.updateTile()
+    assert js == py and len(py) > 3
