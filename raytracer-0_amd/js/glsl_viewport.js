@@ -244,6 +244,19 @@ class GlslViewport {
     this.viewport = [this.tile[0] * this.tile_size[0], this.tile[1] * this.tile_size[1], tileMax[0], tileMax[1]];
   }
 
+  // index.js:911-927: force USE_RESTIR, use_restir and sample_lights on (next render())
+  toggleReSTIR() {
+    this.defines[4] = '#define USE_RESTIR';
+    this.constants[9] = 'const bool use_restir = true;';
+    this.constants[7] = 'const bool sample_lights = true;';
+  }
+
+  // index.js:930-938 (the reference reports ReSTIR as active exactly in animated mode)
+  getReSTIRDebugInfo() {
+    return { isReSTIREnabled: this.animatedScene, temporalFrames: this.temporalFrames, passes: this.passes,
+      animatedMode: this.animatedScene, debugViewActive: false };
+  }
+
   // index.js:940-983
   setAnimatedMode(isAnimated) {
     this.animatedScene = !!isAnimated;

@@ -678,6 +678,18 @@ class GlslViewport:
         self.passes = 0
         self.total_tiles = [-(-size // self.tile_size[0]) - 1, -(-size // self.tile_size[1]) - 1]
 
+    def toggleReSTIR(self):
+        """index.js:911-927: force USE_RESTIR, use_restir and sample_lights on
+        (picked up by the next render(); the reference needs a recompile)."""
+        self.defines[4] = "#define USE_RESTIR"
+        self.constants[9] = "const bool use_restir = true;"
+        self.constants[7] = "const bool sample_lights = true;"
+
+    def getReSTIRDebugInfo(self):
+        """index.js:930-938 (the reference reports ReSTIR as active exactly in animated mode)."""
+        return {"isReSTIREnabled": self.animatedScene, "temporalFrames": self.temporalFrames,
+                "passes": self.passes, "animatedMode": self.animatedScene, "debugViewActive": False}
+
     def setAnimatedMode(self, is_animated):
         """index.js:940-983: animated constants (RENDER_MODE 1, ReSTIR) or the static ones."""
         self.animatedScene = bool(is_animated)

@@ -302,3 +302,20 @@ def test_glslviewport_tile_rendering(cfgs, gpu_required):
     rt0.configure(r, cfg_by_name(cfgs, "c2_cornell_mis_refcaps"), cfgs)
     r.render(1, 2)
     assert np.array_equal(vp.accumulator(), r.read_accum())
+
+
+def test_glslviewport_toggle_restir(cfgs, gpu_required):
+    """toggleReSTIR() (index.js:911-927) switches the next render() to the
+    ReSTIR path; getReSTIRDebugInfo() reports as the reference does."""
+    vp = rt0.GlslViewport(None, {"width": 32, "height": 32})
+    vp.render()
+    before = vp.accumulator()
+    vp.toggleReSTIR()
+    assert vp.defines[4] == "#define USE_RESTIR" and "true" in vp.constants[9]
+    vp.clear()
+    vp.passes = 0
+    vp.render(3)
+    after = vp.accumulator()
+    assert np.isfinite(after).all() and not np.array_equal(after, before)
+    info = vp.getReSTIRDebugInfo()
+    assert info["passes"] == 3 and info["isReSTIREnabled"] is False and info["temporalFrames"] == 5
