@@ -311,6 +311,9 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
 #ifndef RT0_LEAF_UNIFIED
 #define RT0_LEAF_UNIFIED 1
 #endif
+#ifndef RT0_LEAF_DEFER  // Aila-Laine style postponed leaf: A/B knob
+#define RT0_LEAF_DEFER 0
+#endif
 // closest triangle hit along (o, d) before tmin: depth-first, nearer child
 // first, the far child on a per-lane stack in LDS (stride = block size so the
 // 64 lanes of a wave hit 64 different banks).  Returns the leaf-order triangle
@@ -323,6 +326,71 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
   const TriDev *__restrict__ tris = P.tris;
   // a ray visits each of the n-1 nodes at most once: the cap only guarantees
   // that every wave exits even on a corrupt tree
+#if RT0_LEAF_DEFER
+  // one leaf per lane may wait while the lane keeps walking inner nodes; the
+  // leaf tests run once every active lane has one (or a lane holds two, or
+  // its walk ends), so the 64 lanes test triangles together.  Same closest
+  // hit: only the order of the tests changes.
+  int pend = -1;
+  for (int guard = 2 * P.n_tris + 8; guard > 0; --guard) {
+    const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
+    const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+    float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
+    float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
+    const int cl = lk.x, cr = lk.y;
+    int l0 = -1, l1 = -1;
+    if (tl != F_INF && cl < 0) {
+      l0 = ~cl;
+      tl = F_INF;
+    }
+    if (tr != F_INF && cr < 0) {
+      if (l0 < 0) l0 = ~cr;
+      else l1 = ~cr;
+      tr = F_INF;
+    }
+    bool done = false;
+    if (tl != F_INF && tr != F_INF) {
+      const bool lfirst = tl <= tr;
+      stk[256 * sp] = lfirst ? cr : cl;
+      sp = min(sp + 1, RT0_BVH_STACK - 1);
+      node = lfirst ? cl : cr;
+    } else if (tl != F_INF) {
+      node = cl;
+    } else if (tr != F_INF) {
+      node = cr;
+    } else if (sp == 0) {
+      done = true;
+    } else {
+      node = stk[256 * --sp];
+    }
+    const int nl = (pend >= 0) + (l0 >= 0) + (l1 >= 0);
+    const bool has = nl > 0;
+    const bool now = has && (done || nl >= 2 || __ballot(has) == __builtin_amdgcn_read_exec());
+    if (now) {
+#pragma unroll 1
+      for (int k = 0; k < 3; ++k) {
+        const int li = k == 0 ? pend : (k == 1 ? l0 : l1);
+        float t;
+        if (li >= 0 && tri_test(tris[li], o, d, tmin, t)) {
+          tmin = t;
+          best = li;
+        }
+      }
+      pend = -1;
+    } else if (has && pend < 0) {
+      pend = l0 >= 0 ? l0 : l1;
+    }
+    if (done) break;
+  }
+  if (pend >= 0) {  // only on a guard exit
+    float t;
+    if (tri_test(tris[pend], o, d, tmin, t)) {
+      tmin = t;
+      best = pend;
+    }
+  }
+  return best;
+#endif
   for (int guard = 2 * P.n_tris + 8; guard > 0; --guard) {
     const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
     const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
