@@ -1,50 +1,101 @@
 #!/usr/bin/env python3
-"""bench.py -- Msamples/s of the rt0 HIP integrator on BASELINE.json's workload.
+"""bench.py -- Msamples/s of the rt0 HIP integrator on BASELINE.json's workloads.
 
-Workload (BASELINE.json configs[1], SURVEY 8d "C2"): 1024x1024 Cornell box
-(index.js:54-85, camera index.js:89-95), MIS power heuristic on, 8 bounces
+Default workload (BASELINE.json configs[1], SURVEY 8d "C2"): 1024x1024 Cornell
+box (index.js:54-85, camera index.js:89-95), MIS power heuristic on, 8 bounces
 (MAX_BOUNCES = MAX_DIFF_BOUNCES = 8: a true 8-bounce path; the reference's
-default MAX_DIFF_BOUNCES=4 variant is reported beside it), 64 spp.
-One step = one 64-pass progressive render of the whole image (u_frame 1..64,
-i.e. 64 GlslViewport.render() calls) with scene + accumulator resident in HBM.
+default MAX_DIFF_BOUNCES=4 variant is reported beside it with --secondary),
+64 spp.  One step = one 64-pass progressive render of the whole image
+(u_frame 1..64, i.e. 64 GlslViewport.render() calls) with scene + accumulator
+resident in HBM.  `--config c1|c3|c4|c5` times the other BASELINE configs
+(rt0/workloads.json); C3/C5 are ReSTIR workloads whose steps continue the
+frame sequence (temporal reuse needs u_frame > 2).
 
-N GPUs (one process per GPU, torch.distributed.run): the image is split into
-16-row bands dealt round-robin over ranks (rt0_set_shard); each rank renders
-its bands straight into a band-packed torch buffer (rt0_set_accum_buffer_compact:
-the RCCL send buffer as it stands), and rank 0 gathers the bands over RCCL and
-reorders them with one index_copy_ inside the timed region ("strong" scaling:
-total work fixed).
+N GPUs: `python bench.py --gpus N` starts `torch.distributed.run` with N
+ranks as a child process (before anything touches a GPU) unless it already
+runs under it; WORLD_SIZE must equal --gpus.  One process per GPU:
+  * progressive workloads (C1, C2, C4): the image is split into 16-row bands
+    dealt round-robin over ranks (rt0_set_shard); each rank renders its bands
+    straight into a band-packed torch buffer (rt0_set_accum_buffer_compact:
+    the RCCL send buffer as it stands), and rank 0 gathers the bands over RCCL
+    into one preallocated buffer and reorders them with one index_copy_;
+  * ReSTIR workloads (C3, C5): one contiguous row block per rank, a halo
+    exchange of the newest reservoir planes after every pass (RCCL
+    point-to-point, rt0/shard.py: RestirShard), the block gather at the end
+    of the step.
+Both gathers are inside the timed region ("strong" scaling: total work fixed);
+rank 0's gather time is reported separately.
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
 `roofline` (VALU FP32: algorithmic FLOP/sample from SURVEY 8d x counted events,
 over the kernel's HIP-event time; HBM traffic from the committed PMC passes)
-and `cpu_baseline` (the JS CPU integrator oracle/js/rt0_cpu.js on
-node worker_threads, bounded sample of the same workload), with the C
-restatement oracle/rt0_oracle.c (OpenMP) beside it as `cpu_baseline_c`.
+and, at N=1, `cpu_baseline` (the JS CPU integrator
+oracle/js/rt0_cpu.js on node worker_threads, bounded sample of the same
+workload) with the C restatement oracle/rt0_oracle.c (OpenMP) beside it as
+`cpu_baseline_c`.  Only those two baseline legs touch oracle/.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "raytracer-0_amd"))
-sys.path.insert(0, os.path.join(HERE, "oracle"))
-
-import numpy as np  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
-W = H = 1024
-SPP = 64
-PROFILE_ROUND = "r01"  # profiles/<round>/ holding the PMC summary of this workload
+PROFILE_ROUND = "r02"  # profiles/<round>/ holding the PMC summary of the default workload
+BAND = 16
 
 
-def flop_per_sample(c, mis=True):
-    """SURVEY 8d algorithmic FLOP model: 140 + 150*isect + 130*iter + (140+54*mis)*nee per sample."""
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch(n):
+    """Run this script under torch.distributed.run with n ranks (a child
+    process: nothing here has touched the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# ---------------------------------------------------------------- FLOP model
+def isect_flop(scene):
+    """SURVEY 8d per-intersection() weights counted from source: iPlane 12,
+    iSphere 20, iBox 23 FLOP per candidate (raytracer.glsl:812-859), plus ~25
+    for the closest-hit parse (1049-1079).  Cornell (5 planes, 1 sphere,
+    2 boxes) = 151, the 150 of SURVEY 8d."""
+    n = {"PLANE": 0, "SPHERE": 0, "BOX": 0}
+    for line in scene:
+        t = [x.strip() for x in line.split(",")]
+        if len(t) > 1 and t[1] in n:
+            n[t[1]] += 1
+    return 12.0 * n["PLANE"] + 20.0 * n["SPHERE"] + 23.0 * n["BOX"] + 25.0
+
+
+# FLOP of one map() evaluation per SDF kind (raytracer.glsl:496-712, counted
+# from source as in SURVEY 8d): sdBox 0, udRoundBox 1, sdSphere 2,
+# sdTriPrism 3, sdCone 4, Menger 5, Mandelbulb 6 (index.html:702-717); + 4 for
+# the p - pos offset and the min() of map().
+MAP_FLOP = {0: 17.0, 1: 16.0, 2: 8.0, 3: 18.0, 4: 16.0, 5: 140.0, 6: 190.0}
+
+
+def flop_per_sample(c, wl):
+    """SURVEY 8d algorithmic FLOP model, per sample:
+    140 + C_isect*isect + 130*iter + (140 + 54*mis)*nee + C_map*map."""
     n = max(1, c["samples"])
-    return 140.0 + 150.0 * c["isect"] / n + 130.0 * c["iter"] / n + (140.0 + 54.0 * mis) * c["nee"] / n
+    mis = bool(wl["constants"].get("use_mis", False))
+    c_map = sum(MAP_FLOP[k] for k in wl.get("sdf_kinds", [])) or 0.0
+    return (140.0 + isect_flop(wl["scene_lines"]) * c["isect"] / n + 130.0 * c["iter"] / n
+            + (140.0 + 54.0 * mis) * c["nee"] / n + c_map * c["map"] / n)
 
 
 def host_threads():
@@ -53,49 +104,161 @@ def host_threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
 
 
-def cpu_baseline_js(cfg_name, budget_s=10.0):
+# ------------------------------------------------------------ CPU baselines
+def cpu_baseline_js(wl, budget_s=10.0):
     """SURVEY 8d's CPU baseline: the JS CPU integrator (oracle/js/rt0_cpu.js,
     fp32 restatement of the same integrator, parity-checked in
     tests/test_cpu_js.py) on node worker_threads, timed on a bounded sample of
-    the same workload: rows 480..543 of the 1024^2 image, successive passes
-    until the time budget."""
+    the same workload: a 64-row band through the image centre, successive
+    passes until the time budget."""
     import shutil
-    import subprocess
     node = shutil.which("node")
     if node is None:
         return None
     threads = host_threads()
+    W, H = wl["width"], wl["height"]
+    r0 = H // 2 - 32
     r = subprocess.run([node, os.path.join(HERE, "oracle", "js", "cpu_bench.js"),
-                        os.path.join(HERE, "tests", "golden", "configs.json"), cfg_name, str(W), str(H), str(threads),
-                        "bench", "480", "544", str(budget_s)], capture_output=True, text=True, timeout=budget_s * 10 + 60)
+                        os.path.join(HERE, "tests", "golden", "configs.json"), wl["fixture"], str(W), str(H),
+                        str(threads), "bench", str(r0), str(r0 + 64), str(budget_s)]
+                       + (["--constants", json.dumps(wl["constants"])]),
+                       capture_output=True, text=True, timeout=budget_s * 10 + 60)
     if r.returncode != 0:
         return {"error": r.stderr[-300:]}
     d = json.loads(r.stdout)
     return {"value": d["msamples_s"], "unit": "Msamples/s", "cores": d["threads"], "kind": "port",
-            "sample": "oracle/js/rt0_cpu.js (JS CPU integrator, node %s worker_threads x%d, %s): rows 480..543 of "
-                      "the 1024^2 bench image, successive passes, %d samples in %.1f s"
-                      % (d["node"], d["threads"], d["cpu"], d["samples"], d["seconds"])}
+            "sample": "oracle/js/rt0_cpu.js (JS CPU integrator, node %s worker_threads x%d, %s): rows %d..%d of "
+                      "the %dx%d bench image, successive passes, %d samples in %.1f s"
+                      % (d["node"], d["threads"], d["cpu"], r0, r0 + 63, W, H, d["samples"], d["seconds"])}
 
 
-def cpu_baseline(cfgs, cfg, budget_s=8.0):
+def cpu_baseline_c(wl, budget_s=8.0):
     """Time the C restatement (OpenMP, all host threads we are allowed) on a
-    bounded sample of the same workload: full-width 1024 rows x a band of rows,
-    8-bounce MIS passes, scaled by samples."""
+    bounded sample of the same workload: a full-width band of 64 rows through
+    the image centre, successive passes, scaled by samples."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as O
     threads = host_threads()
-    rows = 64
-    o = O.Oracle(cfg, cfgs, width=W, height=H)
-    o.frame(1, rows=(480, 480 + 8), threads=threads)  # warm
+    W, H = wl["width"], wl["height"]
+    rows, r0 = 64, H // 2 - 32
+    cfg = {"scene_lines": wl["scene_lines"], "sdf_kinds": wl.get("sdf_kinds", []), "defines": wl["defines"],
+           "constants": wl["constants"], "camera": wl["camera"], "models": wl.get("models", [])}
+    o = O.Oracle(cfg, {"cornell_lines": None, "default_camera": wl["camera"]}, width=W, height=H)
+    o.frame(1, rows=(r0, r0 + 8), threads=threads)  # warm
     n = 0
     t0 = time.time()
     while time.time() - t0 < budget_s:
-        o.frame(1 + n, rows=(480, 480 + rows), threads=threads)
+        o.frame(1 + n, rows=(r0, r0 + rows), threads=threads)
         n += 1
     dt = time.time() - t0
     samples = n * rows * W
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "oracle/rt0_oracle.c (OpenMP x%d), rows 480..%d of the 1024^2 bench image, %d passes "
-                      "(%d samples, %.1f s)" % (threads, 480 + rows, n, samples, dt)}
+            "sample": "oracle/rt0_oracle.c (OpenMP x%d), rows %d..%d of the %dx%d bench image, %d passes "
+                      "(%d samples, %.1f s)" % (threads, r0, r0 + rows - 1, W, H, n, samples, dt)}
+
+
+# ---------------------------------------------------------------- workloads
+class Progressive:
+    """C1/C2/C4: 16-row bands round-robin, band-packed accumulators, one gather."""
+
+    def __init__(self, rt0, torch, wl, rank, world, local):
+        import rt0.shard as shard
+        from rt0 import workloads
+        self.torch, self.world = torch, world
+        W, H = wl["width"], wl["height"]
+        self.r = rt0.Renderer(W, H, device=local)
+        workloads.configure(self.r, wl)
+        self.spp = wl["spp"]
+        self.gather = None
+        if world > 1:
+            self.r.set_shard(rank, world, BAND)
+            self.gather = shard.BandGather(H, W, rank, world, BAND, "cuda:%d" % local)
+            self.acc = self.gather.acc
+            rows = self.r.set_accum_buffer_compact(self.acc.data_ptr())
+            assert rows <= self.acc.shape[0], (rows, self.acc.shape)
+            self.samples_per_step = rows * W * self.spp
+        else:
+            self.acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
+            self.r.set_accum_buffer(self.acc.data_ptr())
+            self.samples_per_step = W * H * self.spp
+        self.kernel_ms, self.gather_s, self.launches = [], [], 0
+
+    def step(self, i):
+        self.acc.zero_()
+        self.torch.cuda.synchronize()
+        self.r.render(1, self.spp)  # synchronous: returns after the kernels finished
+        ms, n = self.r.last_kernel_ms()
+        self.kernel_ms.append(ms)
+        self.launches = n
+        if self.gather is not None:
+            t = time.perf_counter()
+            self.gather.gather()  # RCCL gather of the HDR bands + one reorder on rank 0
+            self.torch.cuda.synchronize()
+            self.gather_s.append(time.perf_counter() - t)
+
+
+class Restir:
+    """C3/C5: one pass per launch (frame-to-frame reservoir dependency); N>1:
+    contiguous row blocks + per-pass halo exchange + block gather."""
+
+    def __init__(self, rt0, torch, wl, rank, world, local):
+        import rt0.shard as shard
+        from rt0 import workloads
+        self.torch, self.world = torch, world
+        W, H = wl["width"], wl["height"]
+        self.r = rt0.Renderer(W, H, device=local)
+        workloads.configure(self.r, wl)
+        self.spp = wl["spp"]
+        self.sh, self.gather = None, None
+        dev = "cuda:%d" % local
+        if world > 1:
+            self.sh = shard.RestirShard(self.r, rank, world, H, W, dev)
+            band = self.sh.band
+            self.gather = shard.BandGather(H, W, rank, world, band, dev)
+            # full-size accumulator padded to world x band rows: the block of this
+            # rank is the gather's send buffer as it stands
+            self.acc = torch.zeros((world * band, W, 4), dtype=torch.float32, device=dev)
+            self.r.set_accum_buffer(self.acc.data_ptr())
+            lo, hi = shard.block_rows(rank, band, H)
+            self.send = self.acc[rank * band:(rank + 1) * band]
+            self.samples_per_step = (hi - lo) * W * self.spp
+        else:
+            self.acc = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
+            self.r.set_accum_buffer(self.acc.data_ptr())
+            self.samples_per_step = W * H * self.spp
+        self.kernel_ms, self.gather_s, self.launches = [], [], 0
+
+    def step(self, i):
+        first = 1 + i * self.spp
+        if self.sh is None:
+            self.r.render(first, self.spp)
+            ms, n = self.r.last_kernel_ms()
+        else:
+            ms, n = 0.0, 0
+            for k in range(first, first + self.spp):
+                self.sh.render(k, 1)
+                m, l = self.r.last_kernel_ms()
+                ms, n = ms + m, n + l
+        self.kernel_ms.append(ms)
+        self.launches = n
+        if self.gather is not None:
+            t = time.perf_counter()
+            self.gather.gather(self.send)
+            self.torch.cuda.synchronize()
+            self.gather_s.append(time.perf_counter() - t)
+
+
+def count_events(rt0, wl, local):
+    """Event counts of the same workload (separate counting kernel instance, a
+    fresh whole-image renderer, outside the timed region)."""
+    from rt0 import workloads
+    r = rt0.Renderer(wl["width"], wl["height"], device=local)
+    workloads.configure(r, wl)
+    r.set_counting(True)
+    r.render(1, min(wl["spp"], 8) if workloads.restir(wl) else wl["spp"])
+    cnt = r.counters()
+    r.close()
+    return cnt
 
 
 def main():
@@ -103,100 +266,97 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c2_cornell_mis_8")
+    ap.add_argument("--config", default="c2", help="workload of rt0/workloads.json: c1 c2 c2_refcaps c3 c4 c5")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--secondary", action="store_true", help="also time the MAX_DIFF_BOUNCES=4 variant")
+    ap.add_argument("--secondary", action="store_true", help="also time the MAX_DIFF_BOUNCES=4 variant of c2")
     ap.add_argument("--jit", type=int, default=1, help="1: scene-specialised kernels (default), 0: ahead-of-time")
     args = ap.parse_args()
 
-    import torch
-    import rt0
-    import oracle as O
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+    import rt0
+    from rt0 import workloads
+
+    wl = workloads.get(args.config)
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")  # RCCL on ROCm
-    cfgs = O.load_configs()
-    cfg = [c for c in cfgs["configs"] if c["name"] == args.config][0]
+    W, H = wl["width"], wl["height"]
 
-    r = rt0.Renderer(W, H, device=local)
-    r.set_jit(bool(args.jit))
-    rt0.configure(r, cfg, cfgs)
-    band = 16
-    nb = H // band
-    owned = [b for b in range(nb) if b % world == rank]
-    if world > 1:
-        # each rank renders its 16-row bands straight into a band-packed
-        # accumulator (rt0_set_accum_buffer_compact) that is the RCCL send buffer
-        import rt0.shard as shard
-        r.set_shard(rank, world, band)
-        gather = shard.BandGather(H, W, rank, world, band, "cuda:%d" % local)
-        acc = gather.acc
-        rows = r.set_accum_buffer_compact(acc.data_ptr())
-        assert rows <= acc.shape[0], (rows, acc.shape)
-    else:
-        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
-        r.set_accum_buffer(acc.data_ptr())
-
-    def step(frame0):
-        acc.zero_()
-        torch.cuda.synchronize()
-        r.render(frame0, SPP)  # synchronous: returns after the kernels finished
-        if world > 1:
-            gather.gather()  # RCCL gather of the HDR bands + one reorder on rank 0
-
+    job = (Restir if workloads.restir(wl) else Progressive)(rt0, torch, wl, rank, world, local)
+    job.r.set_jit(bool(args.jit))
     for i in range(args.warmup):
-        step(1)
-    kernel_ms = []
+        job.step(i)
+    job.kernel_ms.clear()
+    job.gather_s.clear()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(1)
-        kernel_ms.append(r.last_kernel_ms()[0])
+        job.step(args.warmup + i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], device=acc.device)
+        t = torch.tensor([dt], device="cuda:%d" % local)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt * 1000.0 / args.steps
-    total_samples = W * H * SPP * args.steps
+    total_samples = W * H * wl["spp"] * args.steps  # every rank's share: the whole image
     value = total_samples / dt / 1e6
 
     if rank != 0:
         dist.destroy_process_group()
         return
 
-    # algorithmic FLOPs of the dominant kernel: counted events of the same
-    # workload (separate counting kernel instance, outside the timed region)
-    r.set_counting(True)
-    acc.zero_()
-    r.render(1, SPP)
-    cnt = r.counters()
-    r.set_counting(False)
-    fps = flop_per_sample(cnt)
-    owned_samples = len(owned) * band * W * SPP
-    kern_s = float(np.mean(kernel_ms)) / 1000.0
-    achieved_tflops = fps * owned_samples / kern_s / 1e12
+    cnt = count_events(rt0, wl, local)
+    fps = flop_per_sample(cnt, wl)
+    kern_s = float(np.mean(job.kernel_ms)) / 1000.0  # all launches of one step on rank 0
+    achieved_tflops = fps * job.samples_per_step / kern_s / 1e12
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this
-    # workload (scripts/gpu_profile.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2
+    # workload (scripts/gpu_pmc.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2
     # gfx950 correction); counters cannot be read from inside this process
     traffic, pmc = None, None
-    pmc_path = os.path.join(HERE, "profiles", PROFILE_ROUND, "pmc_summary.json")
+    pmc_path = os.path.join(HERE, "profiles", PROFILE_ROUND, "pmc_%s.json" % args.config)
     if world == 1 and os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path))
         traffic = pmc["traffic_bytes_per_launch"]
+    per_launch = max(1, job.launches)
+    kern_launch_s = kern_s / per_launch
+    roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+            "traffic_unit": "bytes/launch",
+            "traffic_source": ("profiles/%s/pmc_%s.json" % (PROFILE_ROUND, args.config)) if pmc else None,
+            "flop_per_sample": round(fps, 1),
+            "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3) for k in ("isect", "iter", "nee", "map")},
+            "kernel_ms_per_step": round(kern_s * 1000.0, 3),
+            "launches_per_step": job.launches,
+            "kernel_ms_per_launch": round(kern_launch_s * 1000.0, 3),
+            "note": "FP32 vector kernel (no MFMA): peak = MI355X FP32 vector 157.3 TF; FLOP model SURVEY 8d x "
+                    "counted events (counting instance, whole image); achieved over rank 0's kernel time"}
+    if pmc and "valu" in pmc:
+        roof["valu_lane_utilisation"] = round(pmc.get("valu_lane_utilisation", 0.0), 4)
+        # wave64 VALU instruction = 2 SIMD cycles (transcendental 4,
+        # MI355X_MICROARCH.md constants), over 1024 SIMDs x the live kernel
+        # time of one launch at the nominal 2.4 GHz
+        roof["valu_issue_utilisation"] = round(2.0 * (pmc["valu"]["SQ_INSTS_VALU"] + pmc["valu"]["SQ_INSTS_VALU_TRANS_F32"])
+                                               / (1024 * kern_launch_s * 2.4e9), 4)
+    mdb = wl["constants"].get("MAX_DIFF_BOUNCES", 4)
     out = {
-        "metric": "Msamples/sec (pixels x spp / s) at 1024^2 Cornell, 8 bounces",
+        "metric": "Msamples/sec (pixels x spp / s) at 1024^2 Cornell, 8 bounces" if args.config == "c2"
+        else "Msamples/sec (pixels x spp / s), BASELINE workload %s" % args.config,
         "value": round(value, 3),
         "unit": "Msamples/s",
         "n_gpus": world,
@@ -207,49 +367,35 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (the reference's own Cornell scene, index.js:54-85; no external data)",
-        "config": {"workload": "%s: 1024x1024 Cornell, MIS power heuristic, MAX_BOUNCES=8, MAX_DIFF_BOUNCES=%d, "
-                               "64 spp per step (u_frame 1..64)" % (args.config, cfg["constants"].get(
-                                   "MAX_DIFF_BOUNCES", 4)),
-                   "width": W, "height": H, "spp": SPP, "parallelism": "row-band x%d (16-row bands)" % world,
+        "data": "synthetic (the reference's own scene grammar and materials; no external data)",
+        "config": {"workload": "%s (%s): %s" % (args.config, wl["fixture"], wl["doc"]),
+                   "width": W, "height": H, "spp": wl["spp"], "max_diff_bounces": mdb,
+                   "parallelism": ("row-band x%d (16-row bands)" % world) if not workloads.restir(wl)
+                   else ("row-block x%d + reservoir halo exchange" % world),
                    "kernel": "scene-specialised (hipRTC JIT)" if args.jit else "ahead-of-time"},
-        "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_FP32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes/launch",
-                     "traffic_source": ("profiles/%s/pmc_summary.json" % PROFILE_ROUND) if pmc else None,
-                     "valu_lane_utilisation": round(pmc["valu_lane_utilisation"], 4) if pmc and "valu_lane_utilisation"
-                     in pmc else None,
-                     # wave64 VALU instruction = 2 SIMD cycles (transcendental 4,
-                     # MI355X_MICROARCH.md constants), over 1024 SIMDs x the live
-                     # kernel time at the nominal 2.4 GHz
-                     "valu_issue_utilisation": round(2.0 * (pmc["valu"]["SQ_INSTS_VALU"]
-                                                           + pmc["valu"]["SQ_INSTS_VALU_TRANS_F32"])
-                                                     / (1024 * kern_s * 2.4e9), 4)
-                     if pmc and "valu" in pmc and world == 1 else None,
-                     "flop_per_sample": round(fps, 1),
-                     "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3)
-                                           for k in ("isect", "iter", "nee")},
-                     "kernel_ms_per_launch": round(kern_s * 1000.0, 3),
-                     "hbm_bytes_per_launch": W * H * 16 * 2 // world,
-                     "note": "FP32 vector kernel (no MFMA): peak = MI355X FP32 vector 157.3 TF; "
-                             "FLOP model SURVEY 8d x counted events"},
+        "roofline": roof,
     }
-    if args.secondary:
-        sec = [c for c in cfgs["configs"] if c["name"] == "c2_cornell_mis_refcaps"][0]
-        rt0.configure(r, sec, cfgs)
-        acc.zero_()
-        r.render(1, SPP)
+    if job.gather_s:
+        out["gather_ms_per_step"] = round(1000.0 * float(np.mean(job.gather_s)), 3)
+    if args.secondary and args.config == "c2":
+        sec = workloads.get("c2_refcaps")
+        workloads.configure(job.r, sec)
+        job.step(0)
         t1 = time.perf_counter()
-        for _ in range(args.steps):
-            acc.zero_()
-            r.render(1, SPP)
-        out["secondary_refcaps_Msamples_s"] = round(W * H * SPP * args.steps / (time.perf_counter() - t1) / 1e6 *
-                                                    (world if world > 1 else 1), 3)
-    if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-        js = cpu_baseline_js(args.config)
-        c_port = cpu_baseline(cfgs, cfg)
+        for i in range(args.steps):
+            job.step(i)
+        torch.cuda.synchronize()
+        out["secondary_refcaps_Msamples_s"] = round(W * H * sec["spp"] * args.steps
+                                                    / (time.perf_counter() - t1) / 1e6, 3)
+    if not args.no_cpu_baseline and world == 1 and wl.get("models"):
+        out["cpu_baseline"] = None  # brute-force triangles in the restatement: minutes per row, no bounded sample
+    elif not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
+        js = cpu_baseline_js(wl)
+        c_port = cpu_baseline_c(wl)
         out["cpu_baseline"] = js if js and "value" in js else c_port
         out["cpu_baseline_c"] = c_port  # the C oracle on the same sample (OpenMP)
+        if js and "error" in js:
+            out["cpu_baseline_js_error"] = js["error"][-160:]
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -194,7 +194,8 @@ int rt0_resize(rt0_ctx *ctx, int width, int height);
 int rt0_get_size(const rt0_ctx *ctx, int *width, int *height);
 
 /* Display epilogue, tonemapper.glsl:28-33: rgba8 = 255*pow(acc*cont, 1/2.2),
- * alpha 255, cont = 1/passes (index.js:1089). */
+ * alpha 255, cont = 1/passes (index.js:1089).  RT0_E_UNSUPPORTED on a
+ * band-packed accumulator (rt0_set_accum_buffer_compact). */
 int rt0_tonemap(rt0_ctx *ctx, float contribution, uint8_t *rgba8_out);
 /* Same with a curve: RT0_TONEMAP_GAMMA (= rt0_tonemap), RT0_TONEMAP_ACES
  * (tonemapper.glsl's unused ACESFilm, 17-26, at its exposure 1.5) or
@@ -252,7 +253,10 @@ int rt0_set_accum_buffer(rt0_ctx *ctx, void *dptr);
  * buffer holds only this shard's bands, in band order ((*rows) x W x 4 f32,
  * *rows = owned bands x band_rows), so it is the send buffer of the gather
  * as it stands.  Not for ReSTIR (RT0_E_UNSUPPORTED).  rt0_read_accum /
- * rt0_write_accum / rt0_clear then cover these rows. */
+ * rt0_write_accum / rt0_clear then cover these rows; rt0_tonemap* return
+ * RT0_E_UNSUPPORTED (gather the bands into an image first), and rt0_render
+ * returns RT0_E_STATE once rt0_set_shard changed the rows this shard owns
+ * (set the buffer again). */
 int rt0_set_accum_buffer_compact(rt0_ctx *ctx, void *dptr, int *rows);
 
 /* Sharded ReSTIR: the reservoir textures of index.js:149-163
@@ -298,6 +302,9 @@ int rt0_read_counters(rt0_ctx *ctx, uint64_t out[5]);
 /* Wall time of the kernels of the last rt0_render (HIP events on the
  * context's stream), milliseconds, and the number of kernel launches. */
 int rt0_last_kernel_ms(const rt0_ctx *ctx, float *ms, int *launches);
+/* Bytes of device scratch the context holds for frame-chunked launches
+ * (per-frame sample planes over the launch rectangle; grows on demand). */
+int rt0_scratch_bytes(const rt0_ctx *ctx, size_t *bytes);
 
 /* Library version string. */
 const char *rt0_version(void);

@@ -30,6 +30,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 typedef void *EGLDisplay, *EGLConfig, *EGLSurface, *EGLContext;
 typedef int32_t EGLint;
@@ -137,6 +138,12 @@ F(GLenum, glGetError, (void))
 
 static const char *SS_DIR =
     "/usr/local/lib/python3.10/dist-packages/kaleido/executable/bin/swiftshader";
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
 
 static void die(const char *m) {
   fprintf(stderr, "glrun: %s\n", m);
@@ -346,6 +353,8 @@ int main(int argc, char **argv) {
     return 3;
   }
   p_glUseProgram(prog);
+  double t0 = now_s();
+  fprintf(stderr, "glrun: linked\n");
 
   GLuint vb;
   static const float quad[12] = {-1, -1, 1, -1, -1, 1, -1, 1, 1, -1, 1, 1};
@@ -421,6 +430,7 @@ int main(int argc, char **argv) {
     p_glDrawArrays(GL_TRIANGLES, 0, 6);
     p_glFinish();
     if (p_glGetError() != 0) die("GL error after draw");
+    fprintf(stderr, "glrun: pass %d done at %.1f s after link\n", pass, now_s() - t0);
 
     dump(prefix, pass, "c", w, h, fb, 0);
     if (restir_out) {

@@ -6,6 +6,7 @@
 //   mode "image" <frame0> <n> <out.f32>  : passes frame0..frame0+n-1 of the whole
 //                                          image, RGBA f32 rows bottom-up -> file
 //   mode "bench" <y0> <y1> <seconds>     : rows [y0,y1) split over the threads,
+//                                          [--constants JSON] overrides constants,
 //                                          successive passes until the deadline;
 //                                          prints {"samples", "seconds", "msamples_s", ...}
 const os = require('os');
@@ -18,6 +19,7 @@ function makeRenderer(d) {
   const cfgs = JSON.parse(fs.readFileSync(d.configs, 'utf8'));
   const cfg = cfgs.configs.find((c) => c.name === d.config);
   if (!cfg) throw new Error('no config ' + d.config);
+  if (d.constants) cfg.constants = Object.assign({}, cfg.constants || {}, d.constants);
   return new CpuRenderer(cfg, cfgs.cornell_lines, cfgs.default_camera, d.W, d.H);
 }
 
@@ -39,6 +41,8 @@ if (!isMainThread) {
 } else {
   const a = process.argv.slice(2);
   const base = { configs: path.resolve(a[0]), config: a[1], W: +a[2], H: +a[3] };
+  const ci = a.indexOf('--constants');  // optional JSON of constant overrides (bench workloads)
+  if (ci >= 0) base.constants = JSON.parse(a[ci + 1]);
   const threads = +a[4] || os.cpus().length;
   const mode = a[5];
   const split = (y0, y1) => {

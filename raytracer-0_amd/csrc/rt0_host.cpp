@@ -61,6 +61,7 @@ struct rt0_ctx {
   float4 *d_accum = nullptr;
   float4 *ext_accum = nullptr;  // caller-owned accumulator (rt0_set_accum_buffer)
   bool compact = false;         // ext_accum holds only this shard's bands (rt0_set_accum_buffer_compact)
+  int compact_rows = 0;         // owned_rows() when the compact buffer was set (its row capacity)
   float4 *acc() const { return ext_accum ? ext_accum : d_accum; }
   // rows of this shard's bands: the band-compressed grid height
   int owned_rows() const {
@@ -587,6 +588,14 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
                                       "(band_rows * n_shards >= height)");
   if (restir && c->n_shards > 1 && n > 1)
     return fail(c, RT0_E_ARG, "sharded ReSTIR renders one pass per call (halo exchange between passes)");
+  // a band-packed caller buffer holds exactly the rows of the shard it was set
+  // for: a later rt0_set_shard / ReSTIR config would index past its end
+  if (c->compact && restir)
+    return fail(c, RT0_E_UNSUPPORTED, "band-packed accumulator (rt0_set_accum_buffer_compact) with ReSTIR on");
+  if (c->compact && c->owned_rows() != c->compact_rows)
+    return fail(c, RT0_E_STATE, "the shard changed after rt0_set_accum_buffer_compact (buffer holds " +
+                                    std::to_string(c->compact_rows) + " rows, shard owns " +
+                                    std::to_string(c->owned_rows()) + "): set the buffer again");
   HIPCHK(c, hipSetDevice(c->device));
   if (c->bvh_dirty) {
     int rc = build_bvh(c);
@@ -681,7 +690,8 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       if (chunks > 1) {
         p.frame_chunk = (p.nframes + chunks - 1) / chunks;
         chunks = (p.nframes + p.frame_chunk - 1) / p.frame_chunk;
-        const size_t need = (size_t)p.nframes * p.n_band_rows * c->W * sizeof(float4);
+        // one plane per frame over the launch rectangle (sample_plane in rt0_integrator.h)
+        const size_t need = (size_t)p.nframes * (p.vp_x1 - p.vp_x0) * (p.vp_y1 - p.vp_y0) * sizeof(float4);
         if (need > c->samples_bytes) {
           if (c->d_samples) HIPCHK(c, hipFree(c->d_samples));
           c->d_samples = nullptr;
@@ -794,6 +804,10 @@ int rt0_tonemap(rt0_ctx *c, float contribution, uint8_t *out) { return rt0_tonem
 
 int rt0_tonemap_ex(rt0_ctx *c, float contribution, int mode, uint8_t *out) {
   if (!c || !out || mode < 0 || mode > 2) return RT0_E_ARG;
+  // a band-packed shard buffer is not an image (rows in band order, H/N of
+  // them): gather it first (rt0/shard.py: BandGather) and tonemap the image
+  if (c->compact)
+    return fail(c, RT0_E_UNSUPPORTED, "rt0_tonemap on a band-packed accumulator (rt0_set_accum_buffer_compact)");
   HIPCHK(c, hipSetDevice(c->device));
   int n = c->W * c->H;
   HIPCHK(c, rt0_launch_tonemap(c->acc(), c->d_tonemap, n, contribution, mode, c->stream));
@@ -855,7 +869,8 @@ int rt0_set_accum_buffer_compact(rt0_ctx *c, void *dptr, int *rows) {
     return fail(c, RT0_E_UNSUPPORTED, "ReSTIR shards keep a full-size accumulator (contiguous row blocks)");
   c->ext_accum = (float4 *)dptr;
   c->compact = true;
-  if (rows) *rows = c->owned_rows();
+  c->compact_rows = c->owned_rows();
+  if (rows) *rows = c->compact_rows;
   return RT0_OK;
 }
 
@@ -912,6 +927,12 @@ int rt0_set_counting(rt0_ctx *c, int enable) {
 int rt0_read_counters(rt0_ctx *c, uint64_t out[5]) {
   if (!c || !out) return RT0_E_ARG;
   for (int i = 0; i < 5; i++) out[i] = c->counters[i];
+  return RT0_OK;
+}
+
+int rt0_scratch_bytes(const rt0_ctx *c, size_t *bytes) {
+  if (!c || !bytes) return RT0_E_ARG;
+  *bytes = c->samples_bytes;
   return RT0_OK;
 }
 

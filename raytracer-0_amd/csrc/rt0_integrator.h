@@ -1675,6 +1675,13 @@ DEV void accumulate(const It &it, const LaunchParams &P, float4 &a, v3 s) {
   }
 }
 
+// Frame-chunked scratch: one plane per frame covering only the launch's
+// rectangle (viewport x band rows), indexed relative to its corner.
+DEV size_t sample_plane(const LaunchParams &P) { return (size_t)(P.vp_x1 - P.vp_x0) * (P.vp_y1 - P.vp_y0); }
+DEV size_t sample_index(const LaunchParams &P, int px, int r) {
+  return (size_t)(r - P.vp_y0) * (P.vp_x1 - P.vp_x0) + (px - P.vp_x0);
+}
+
 // The pass kernel body: 16x16 pixel tile per 256-thread workgroup (four 8x8
 // wave tiles); each lane accumulates its pixel's passes in registers.
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
@@ -1694,7 +1701,7 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   if (!RESTIR && P.samples) {  // frame-chunked: samples out, rt0_sum_kernel accumulates
     const int f0 = (int)blockIdx.z * P.frame_chunk;
     const int f1 = min(P.nframes, f0 + P.frame_chunk);
-    const size_t plane = (size_t)P.n_band_rows * P.width, lp = (size_t)r * P.width + px;
+    const size_t plane = sample_plane(P), lp = sample_index(P, px, r);
     for (int f = f0; f < f1; ++f) {
       it.frame = P.frame0 + (uint32_t)f;
       v3 s = it.sample(px, py);
@@ -1763,7 +1770,7 @@ DEV void sum_body(const LaunchParams &P) {
   const int py = image_row(P, r);
   if (py >= P.height) return;
   const size_t pix = P.compact ? (size_t)r * P.width + px : (size_t)py * P.width + px;
-  const size_t plane = (size_t)P.n_band_rows * P.width, lp = (size_t)r * P.width + px;
+  const size_t plane = sample_plane(P), lp = sample_index(P, px, r);
   float4 a = P.accum[pix];
   for (int f = 0; f < P.nframes; ++f) {
     const float4 s = P.samples[(size_t)f * plane + lp];

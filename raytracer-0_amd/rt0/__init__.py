@@ -32,7 +32,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
            "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read",
-           "rt0_set_temporal_frames", "rt0_set_viewport"]
+           "rt0_set_temporal_frames", "rt0_set_viewport", "rt0_scratch_bytes"]
 
 TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
@@ -131,6 +131,7 @@ def lib():
         "rt0_set_counting": (c_int, [c_void_p, c_int]),
         "rt0_read_counters": (c_int, [c_void_p, P(ctypes.c_uint64)]),
         "rt0_last_kernel_ms": (c_int, [c_void_p, P(c_float), P(c_int)]),
+        "rt0_scratch_bytes": (c_int, [c_void_p, P(ctypes.c_size_t)]),
         "rt0_version": (ctypes.c_char_p, []),
         "rt0_tonemap_ex": (c_int, [c_void_p, c_float, c_int, P(ctypes.c_uint8)]),
         "rt0_png_decode": (c_int, [c_void_p, ctypes.c_size_t, P(c_int), P(c_int), P(P(ctypes.c_uint8))]),
@@ -528,6 +529,12 @@ class Renderer:
         out = (ctypes.c_uint64 * 5)()
         self._chk(lib().rt0_read_counters(self.h, out))
         return dict(zip(("isect", "iter", "nee", "map", "samples"), list(out)))
+
+    def samples_bytes(self):
+        """Device scratch of frame-chunked launches (rt0_scratch_bytes)."""
+        n = ctypes.c_size_t()
+        self._chk(lib().rt0_scratch_bytes(self.h, ctypes.byref(n)))
+        return n.value
 
     def last_kernel_ms(self):
         ms, n = ctypes.c_float(), ctypes.c_int()

@@ -73,9 +73,14 @@ def gather_image(acc, rank, world, band, image=None, bufs=None):
 class BandGather:
     """The per-step gather for band-packed accumulators (rt0_set_accum_buffer_compact):
     every rank renders straight into a [rows, W, 4] buffer holding only its
-    bands, which is the send buffer as it stands; rank 0 scatters the gathered
-    bands into the image with one index_copy_ over cached indices.  No packing,
-    no per-step allocation or host->device index upload."""
+    bands, which is the send buffer as it stands; rank 0 receives every rank's
+    buffer into one preallocated [world, rows, W, 4] tensor (the gather's
+    output list is views of it) and scatters the bands into the image with one
+    index_copy_ over cached indices.  No packing, no per-step allocation or
+    host->device index upload.
+
+    With band = block_band(H, world) every rank owns one contiguous row block
+    (sharded ReSTIR); `send` then passes that block of a full-size accumulator."""
 
     def __init__(self, H, W, rank, world, band, device, channels=4):
         import torch
@@ -85,7 +90,8 @@ class BandGather:
         self.rows = self.max_owned * band  # every rank's buffer has this many rows (RCCL needs equal sizes)
         self.acc = torch.zeros((self.rows, W, channels), dtype=torch.float32, device=device)
         if rank == 0:
-            self.bufs = [torch.empty_like(self.acc) for _ in range(world)]
+            self.recv = torch.empty((world, self.rows, W, channels), dtype=torch.float32, device=device)
+            self.bufs = list(self.recv.unbind(0))  # views: the gather writes straight into recv
             src_slot, dst_band = [], []
             for s in range(world):
                 for j, b in enumerate(owned_bands(s, world, self.nb)):
@@ -95,18 +101,18 @@ class BandGather:
             self.dst = torch.tensor(dst_band, device=device)
             self.image = torch.zeros((self.nb * band, W, channels), dtype=torch.float32, device=device)
 
-    def gather(self):
+    def gather(self, send=None):
         """Collective; rank 0 returns the assembled [H, W, 4] image (a view of a
-        persistent buffer), the other ranks None."""
-        import torch
+        persistent buffer), the other ranks None.  send defaults to self.acc."""
         import torch.distributed as dist
+        send = self.acc if send is None else send
         if self.rank != 0:
-            dist.gather(self.acc, None, dst=0)
+            dist.gather(send, None, dst=0)
             return None
-        dist.gather(self.acc, self.bufs, dst=0)
-        stacked = torch.stack(self.bufs).view(self.world * self.max_owned, self.band, self.W, -1)
+        dist.gather(send, self.bufs, dst=0)
+        bands = self.recv.view(self.world * self.max_owned, self.band, self.W, -1)
         img = self.image.view(self.nb, self.band, self.W, -1)
-        img.index_copy_(0, self.dst, stacked.index_select(0, self.src))
+        img.index_copy_(0, self.dst, bands.index_select(0, self.src))
         return self.image[:self.H]
 
 

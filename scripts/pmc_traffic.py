@@ -6,7 +6,11 @@ gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports half
 the bytes of a 16-B-per-lane streaming read -- doubled here; WRITE_SIZE is exact
 for 16-B-per-lane stores.  Both counters are in KiB.
 
-usage: pmc_traffic.py <fetch pass dir> <write pass dir> <out.json> [W H]
+usage: pmc_traffic.py <fetch pass dir> <write pass dir> <out.json> [W H [valu pass dir [bytes/pixel]]]
+
+bytes/pixel = algorithmic HBM bytes per pixel per launch: 32 for the
+progressive kernel (one float4 accumulator read + write), 160 for a ReSTIR
+pass (+ two reservoir MRT writes and the six reservoir input planes read once).
 """
 import csv
 import json
@@ -43,11 +47,11 @@ def main():
         "dispatches": [len(fetch), len(write)],
         "fetch_bytes_per_launch": sum(fetch) / max(1, len(fetch)),
         "write_bytes_per_launch": sum(write) / max(1, len(write)),
-        "algorithmic_bytes_per_launch": W * H * 16 * 2,
+        "algorithmic_bytes_per_launch": W * H * (float(sys.argv[7]) if len(sys.argv) > 7 else 32.0),
         "note": "FETCH_SIZE x2 (gfx950 16-B/lane read correction), WRITE_SIZE as reported; KiB -> bytes",
     }
     res["traffic_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
-    if len(sys.argv) > 6:  # optional VALU pass: SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU
+    if len(sys.argv) > 6 and sys.argv[6] != "-":  # optional VALU pass: SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU
         v = {}
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU"):
             d, _ = per_dispatch(sys.argv[6], c)

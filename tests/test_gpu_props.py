@@ -74,6 +74,58 @@ def test_band_packed_shards_bitwise(cfgs, gpu_required):
         assert np.array_equal(img, a), world
 
 
+def test_band_packed_buffer_guards(cfgs, gpu_required):
+    """A band-packed buffer is not an image and holds exactly one shard's
+    rows: tonemap refuses it, and a later set_shard that changes the owned
+    rows makes render fail instead of writing past the buffer."""
+    import torch
+    cfg = cfg_by_name(cfgs, "c2_cornell_mis_8")
+    W = H = 64
+    r = rt0.Renderer(W, H)
+    rt0.configure(r, cfg, cfgs)
+    r.set_shard(0, 2, 16)
+    buf = torch.zeros((32, W, 4), dtype=torch.float32, device="cuda:0")
+    assert r.set_accum_buffer_compact(buf.data_ptr()) == 32
+    r.render(1, 1)
+    with pytest.raises(rt0.Rt0Error) as e:
+        r.tonemap(1.0)
+    assert e.value.code == -3
+    r.set_shard(0, 1, 16)  # now owns all 64 rows: the 32-row buffer is too small
+    with pytest.raises(rt0.Rt0Error) as e:
+        r.render(2, 1)
+    assert e.value.code == -4
+    r.set_shard(0, 2, 16)  # back to the rows the buffer was set for
+    r.render(2, 1)
+    r.set_accum_buffer(None)  # the context's own full-size buffer again
+    r.set_shard(0, 1, 16)
+    r.render(1, 1)
+    assert r.tonemap(1.0).shape == (H, W, 4)
+
+
+def test_chunked_viewport_scratch_is_tile_sized(cfgs, gpu_required):
+    """Tile rendering with several passes frame-chunks its launches (a 32x32
+    tile is ~16 waves): the per-frame scratch covers the tile, not the
+    canvas, and the tile equals the same rectangle of a whole-canvas render."""
+    cfg = cfg_by_name(cfgs, "c2_cornell_mis_8")
+    W = H = 256
+    full = rt0.Renderer(W, H)
+    rt0.configure(full, cfg, cfgs)
+    full.render(1, 8)
+    ref = full.read_accum()
+    r = rt0.Renderer(W, H)
+    rt0.configure(r, cfg, cfgs)
+    r.set_viewport(96, 64, 32, 32)
+    r.render(1, 8)
+    _, launches = r.last_kernel_ms()
+    assert launches == 2  # chunked pass + ordered sum
+    assert r.samples_bytes() == 8 * 32 * 32 * 16
+    got = r.read_accum()
+    assert np.array_equal(got[64:96, 96:128], ref[64:96, 96:128])
+    mask = np.ones((H, W), bool)
+    mask[64:96, 96:128] = False
+    assert not got[mask].any()
+
+
 def test_odd_sizes_and_edges(cfgs, gpu_required):
     cfg = cfg_by_name(cfgs, "c1_cornell_cos")
     for w, h in ((1, 1), (17, 5), (130, 67)):

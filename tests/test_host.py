@@ -131,3 +131,37 @@ def test_jit_kernels_build_for_every_config(cfgs):
         scene, sdf = rt0.scene_strings(cfg, cfgs)
         size = rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))
         assert size > 4096, cfg["name"]
+
+
+def test_bench_workloads_match_the_parity_scenes(cfgs):
+    """rt0/workloads.json (read by bench.py, no test imports on the product
+    side) describes the same scenes/flags/cameras as the parity fixtures it
+    names, up to the documented bench overrides (C4: 12 bounces)."""
+    from rt0 import workloads
+    by = {c["name"]: c for c in cfgs["configs"]}
+    wls = workloads.load_all()
+    assert {"c1", "c2", "c3", "c4", "c5"} <= set(wls)
+    for key, wl in wls.items():
+        cfg = by[wl["fixture"]]
+        assert wl["scene_lines"] == (cfg["scene_lines"] or cfgs["cornell_lines"]), key
+        assert wl["defines"] == cfg.get("defines", {}), key
+        assert wl["camera"] == (cfg.get("camera") or cfgs["default_camera"]), key
+        assert wl.get("sdf_kinds", []) == cfg.get("sdf_kinds", []), key
+        extra = {k: v for k, v in wl["constants"].items() if cfg.get("constants", {}).get(k) != v}
+        assert extra == ({"MAX_BOUNCES": 12} if key == "c4" else {}), (key, extra)
+        assert wl.get("models", []) == cfg.get("models", []), key
+    assert (wls["c2"]["width"], wls["c2"]["height"], wls["c2"]["spp"]) == (1024, 1024, 64)
+
+
+def test_bench_flop_model_matches_survey():
+    """Cornell intersection() = 150 FLOP; the C2 event counts of
+    round 1 (14.64 isect, 7.36 iter, 7.28 nee) give ~4700 FLOP/sample."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from rt0 import workloads
+    wl = workloads.get("c2")
+    assert bench.isect_flop(wl["scene_lines"]) == 151.0
+    fps = bench.flop_per_sample({"samples": 100, "isect": 1464, "iter": 736, "nee": 728, "map": 0}, wl)
+    assert 4650 < fps < 4760
