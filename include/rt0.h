@@ -286,6 +286,16 @@ int rt0_read_halo_misses(rt0_ctx *ctx, uint32_t *misses, int reset);
  * once per (scene, config), cached per process.  0 = ahead-of-time kernels
  * that read the scene from HBM. */
 int rt0_set_jit(rt0_ctx *ctx, int enable);
+/* Reference-executor compatibility for the ReSTIR reservoir outputs (MRT1/2,
+ * raytracer.glsl:2171-2174).  The golden vectors come from the reference
+ * shader run on SwiftShader 4.1, which after a lane's `break` out of
+ * radiance()'s bounce loop still runs that iteration's brdf() call
+ * (raytracer.glsl:2094) and lets it overwrite the global g_final_reservoir
+ * (1757) -- a GLES execution artefact, pinned by oracle/gen/mask_kat.py.
+ * 1 = reproduce it (the reservoir chain then matches the reference executor
+ * pass after pass); 0 (default) = GLSL semantics.  Radiance of a pass is the
+ * same either way; only the reservoirs the next passes read differ. */
+int rt0_set_executor_compat(rt0_ctx *ctx, int enable);
 /* Compile the scene-specialised kernel for (scene, config) without a device
  * (hipRTC only): checks the generated code builds; *code_size receives the
  * code-object size.  err (may be NULL) receives the compiler log. */

@@ -11,12 +11,24 @@
  * shaders/pathtracing/raytracer.glsl.  The expanded text is written OUTSIDE of
  * version control (oracle/_gen/, git- and gpurun-ignored).
  *
- * Two textual edits are applied to the expanded text:
+ * Textual edits applied to the expanded text (every fixture):
  *   1. `const Mesh meshes[` -> `Mesh meshes[` (required: SwiftShader 4.1 rejects
  *      dynamic indexing into const struct arrays; semantically neutral).
- *   2. with --nanfix only: powerHeuristic's `max(0.0, (f*f)/denom)` becomes
+ *   2. the `out` parameters of iBox (`out vec3 n`, raytracer.glsl:836) and iSDF
+ *      (`out vec3 n, out int index`, 974) become `inout`.  This is a REAL
+ *      modification of the reference, not a neutral one: GLSL leaves an `out`
+ *      parameter the callee does not assign undefined, and iBox/iSDF return
+ *      false without assigning them while intersection() passes hit.n /
+ *      hit.index (1028, 1041) and relies on them keeping their values
+ *      (HIT_MISS, 998).  SwiftShader copies out a stale register there, which
+ *      turns every SDF miss into hit.index = NUM_MESHES and renders scenes that
+ *      mix quadrics with SDFs black.  `inout` pins the undefined value to "the
+ *      caller's value unchanged", the only reading under which the reference
+ *      renders its own scenes (DESIGN.md 2).
+ *   3. with --nanfix only: powerHeuristic's `max(0.0, (f*f)/denom)` becomes
  *      `denom > 0.0 ? (f*f)/denom : 0.0`, i.e. IEEE-maxNum semantics for the 0/0
  *      case (raytracer.glsl:1233-1238).  Every non-NaN pixel is unchanged.
+ *      No committed fixture uses it (manifest.json: unpatched powerHeuristic).
  * With --kat, the reference main() is renamed and a known-answer main() that
  * writes the RNG stream (seed schedule of raytracer.glsl:2120, 2135, 2143,
  * 1810, 1972/1190) into the three MRTs is appended.

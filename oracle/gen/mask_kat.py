@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""mask_kat.py -- known-answer shaders that pin how the oracle's executor
+(SwiftShader 4.1, run by oracle/gen/glrun.c) masks side effects after `break`.
+
+TEST INFRASTRUCTURE ONLY (build container; needs the kaleido SwiftShader
+bundle).  None of these shaders is reference text: they are minimal GLSL ES
+3.00 programs with the reference's control-flow shape -- a bounded loop
+(radiance(), raytracer.glsl:1994) whose lanes `break` at different iterations,
+followed in the same iteration by a call (brdf(), 2094) into a function that
+writes a GLOBAL (sampleLightsReSTIR's `g_final_reservoir = final_reservoir`,
+1757, read by main() after the loop, 2173-2174).
+
+GLSL ES 3.00 (spec 6.4, "Jumps"): a fragment that executed `break` executes
+nothing more of the loop.  What the executor does instead (every case below;
+tests/test_oracle_golden.py::test_mask_kat_model re-derives each output from
+these rules):
+  1. in the iteration in which a lane breaks, the calls after the `break`
+     still run for it, and writes to globals inside the callee are not masked
+     (break_then_call, global_in_callee_if, nested_break, nested_call);
+     writes in the loop body itself are (global_in_loop);
+  2. the callee sees its parameters as the lane's PREVIOUS call left them:
+     `in` copies and `inout` values after that call (arg_before_break,
+     struct_arg, inout_arg); the caller's argument copies are masked;
+  3. with no previous call the parameter registers hold another fragment's
+     values (the lane of the quad processed before): undefined;
+  4. only that one iteration: later iterations are masked (uniform_stop:
+     also when every lane of the quad breaks together);
+  5. loops inside the callee run for the lane only when the compiler unrolls
+     them -- constant trip count <= 4 with no break/continue (callee_loops);
+  6. `continue` does not produce the effect (after_continue).
+The summary (per-pixel outputs of every case) is tests/golden/mask_kat.json.
+
+usage: python3 oracle/gen/mask_kat.py
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+GEN = os.path.join(REPO, "oracle", "_gen", "mask_kat")
+GLRUN = os.path.join(REPO, "oracle", "_ref", "glrun")
+W = H = 8
+
+HEAD = """#version 300 es
+precision highp float;
+precision highp int;
+uniform vec2 u_resolution;
+uniform uint u_frame;
+layout(location = 0) out vec4 FragColor;
+layout(location = 1) out vec4 ReSTIRData;
+layout(location = 2) out vec4 ReSTIRAux;
+// lane l of the 2x2 quad q stops at iteration stopOf()
+int stopOf(ivec2 p) {
+  int lane = (p.x & 1) + 2 * (p.y & 1);
+  int quad = ((p.x >> 1) + (p.y >> 1)) & 3;
+  return (lane * 3 + quad) % 5;
+}
+float g0; float g1; float g2; float g3;
+"""
+
+# Each body sets g0..g3 (and o0..o3, written to ReSTIRData) and leaves `stop`
+# and the loop-local `loc` in scope for the epilogue.
+EPILOGUE = """
+  FragColor = vec4(g0, g1, g2, g3);
+  ReSTIRData = vec4(o0, o1, o2, o3);
+  ReSTIRAux = vec4(float(stop), 0.0, 0.0, 0.0);
+}
+"""
+
+CASES = {
+    # 1: global written by a callee after the break test; loop-body counter
+    "break_then_call": """
+void touch(float v) { g0 = v; g1 += 1.0; }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    if (i == stop) break;
+    touch(float(i));
+    loc += 1.0;
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 1: the same writes in the loop body (no call): masked
+    "global_in_loop": """
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    if (i == stop) break;
+    g0 = float(i); g1 += 1.0;
+    loc += 1.0;
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 1: the callee's write inside an `if` of the callee (brdf's if-chain)
+    "global_in_callee_if": """
+void touch(float v, bool on) { if (on) { g0 = v; g1 += 1.0; } }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    if (i == stop) break;
+    touch(float(i), gl_FragCoord.x > -1.0);
+    loc += 1.0;
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 1: break nested one `if` deeper (radiance's break sites sit in ifs)
+    "nested_break": """
+void touch(float v) { g0 = v; g1 += 1.0; }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    if (i >= stop) {
+      if (gl_FragCoord.y > -1.0) break;
+    }
+    touch(float(i));
+    loc += 1.0;
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 1+2: a call inside the callee (brdf -> sampleLightsReSTIR)
+    "nested_call": """
+void inner(float v) { g0 = v; g1 += 1.0; }
+void outer(float v, bool b) { float q = v * 2.0; if (b) inner(q); }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    loc = float(i) * 10.0 + 5.0;
+    if (i == stop) break;
+    outer(loc, true);
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 2: the argument is updated BEFORE the break: the callee still sees the
+    # previous call's copy
+    "arg_before_break": """
+void touch(float v) { g0 = v; g1 += 1.0; }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    loc = float(i) * 10.0 + 5.0;
+    if (i == stop) break;
+    touch(loc);
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 2: a struct argument (brdf's `in Hit hit`)
+    "struct_arg": """
+struct S { vec3 p; int k; };
+void touch(S s) { g0 = s.p.x + float(s.k); g1 += 1.0; }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  S s = S(vec3(0.0), 0);
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    s.p = vec3(float(i) * 10.0 + 5.0); s.k = 100 * i;
+    if (i == stop) break;
+    touch(s);
+  }
+  loc = s.p.x;
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 2: an `inout` argument (brdf's r/mask/acc/bounceIsSpecular) and an `in`
+    "inout_arg": """
+void touch(inout float v, float w) { g0 = v + 1000.0 * w; g1 += 1.0; v += 0.5; }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0; float w = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    loc = float(i) * 10.0 + 5.0;
+    if (i == stop) break;
+    w = float(i);
+    touch(loc, w);
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 4: all four lanes of a quad break in the same iteration
+    "uniform_stop": """
+void touch(float v) { g0 = v; g1 += 1.0; }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = 2 + ((int(gl_FragCoord.x) >> 2) & 1);
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    loc = float(i) * 10.0 + 5.0;
+    if (i == stop) break;
+    touch(loc);
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+    # 5: loops inside the callee: trip counts 2, 3, 4, 5, 9, 16 and 2 with
+    # continue / break; a loop bounded by a local (sampleLightsReSTIR's
+    # candidate and spatial loops)
+    "callee_loops": """
+const int NC = 9;
+float o0; float o1; float o2; float o3;
+void work(float v) {
+  for (int i = 0; i < 2; ++i) g0 += 1.0;
+  for (int i = 0; i < 3; ++i) g1 += 1.0;
+  for (int i = 0; i < 4; ++i) g2 += 1.0;
+  for (int i = 0; i < 5; ++i) g3 += 1.0;
+  for (int i = 0; i < NC; ++i) o0 += 1.0;
+  for (int i = 0; i < 2; ++i) { if (v < -100.0) continue; o1 += 1.0; }
+  for (int i = 0; i < 2; ++i) { if (v < -100.0) break; o2 += 1.0; }
+  int n = int(v) + 3;
+  for (int i = 0; i < n; ++i) o3 += 1.0;
+}
+void main() {
+  g0 = 0.0; g1 = 0.0; g2 = 0.0; g3 = 0.0; o0 = 0.0; o1 = 0.0; o2 = 0.0; o3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    loc = 0.0;
+    if (i == stop) break;
+    work(loc);
+  }
+""",
+    # 6: continue instead of break
+    "after_continue": """
+void touch(float v) { g0 = v; g1 += 1.0; }
+void main() {
+  g0 = -1.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float loc = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    if (i == stop) continue;
+    touch(float(i));
+    loc += 1.0;
+  }
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+""",
+}
+
+
+def run_case(name, body):
+    frag = os.path.join(GEN, name + ".frag")
+    with open(frag, "w") as f:
+        f.write(HEAD + body + EPILOGUE)
+    prefix = os.path.join(GEN, name)
+    subprocess.run([GLRUN, "--frag", frag, "--w", str(W), "--h", str(H), "--frames", "1", "--single",
+                    "--restir-out", "--out", prefix], check=True, capture_output=True, text=True)
+
+    def load(tag):
+        return np.fromfile("%s_f1_%s.bin" % (prefix, tag), dtype=np.float32).reshape(H, W, 4)
+
+    g, o, a = load("c"), load("r"), load("a")
+    return [{"x": x, "y": y, "stop": int(a[y, x, 0]), "g": [float(v) for v in g[y, x]],
+             "o": [float(v) for v in o[y, x]]} for y in range(H) for x in range(W)]
+
+
+def main():
+    os.makedirs(GEN, exist_ok=True)
+    out = {"_doc": "per-pixel outputs of the known-answer shaders of oracle/gen/mask_kat.py run by the oracle's "
+                   "executor (SwiftShader 4.1); g = FragColor (g0..g3), o = ReSTIRData (o0..o3)",
+           "width": W, "height": H, "cases": {}}
+    for name, body in CASES.items():
+        rows = run_case(name, body)
+        out["cases"][name] = rows
+        print(name)
+        for r in rows[:4]:
+            print("   x=%d y=%d stop=%d g=%s o=%s" % (r["x"], r["y"], r["stop"], r["g"], r["o"]))
+    with open(os.path.join(REPO, "tests", "golden", "mask_kat.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+
+
+if __name__ == "__main__":
+    main()

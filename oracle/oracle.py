@@ -150,13 +150,16 @@ class Oracle:
         del keep
         return out, rm, ra
 
-    def frames_restir(self, n):
+    def frames_restir(self, n, cfg=None):
         """Passes 1..n with the reference's ReSTIR swap chain (index.js:795-820);
-        returns per-pass samples [n,H,W,4] and reservoirs."""
+        returns per-pass samples [n,H,W,4] and reservoirs.  cfg with time_ms
+        (RENDER_MODE 1 configs): u_time of pass k = pass_time(cfg, k)."""
         z = np.zeros((self.hgt, self.w, 4), np.float32)
         rbuf, raux, rbuf_back, raux_back, h1, h1a, h2, h2a = z, z, z, z, z, z, z, z
         samples, mains, auxs = [], [], []
         for k in range(1, n + 1):
+            if cfg is not None and cfg.get("time_ms"):
+                self.set_time(pass_time(cfg, k), cfg.get("temporal_frames", 5))
             s, m, a = self.frame(k, [rbuf_back, raux_back, h1, h1a, h2, h2a])
             rbuf, raux = m, a  # MRT1/2 written this pass
             samples.append(s)

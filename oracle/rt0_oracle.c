@@ -909,7 +909,19 @@ static void combineReservoirs(const Oracle *o, Res *t, const Res *s, v3 hp, v3 h
     }
   }
 }
-static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float sx, float sy) {
+/* isVisible() as the ghost call of ghost_brdf() executes it: intersection()'s
+ * mesh loop (a `continue` loop) and iSDF's march do not run, so no quadric is
+ * hit; iSDF then reports a hit at its initial t = 4*EPSILON on the SDF of its
+ * never-updated `res` register (the lane's last live map() result: the first
+ * SDF, index NUM_MESHES, in every fixture scene with SDFs). */
+static int ghost_isVisible(Frag *F, v3 from, v3 to) {
+  const Oracle *o = F->o;
+  float dist = length3(sub(to, from));
+  if (dist < EPSILON * 10.0f) return 1;
+  if (o->n_sdfs > 0 && EPSILON * 4.0f < dist - EPSILON * 2.0f) return o->meshes[o->n_meshes].mat.t == M_LIGHT;
+  return 1;
+}
+static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float sx, float sy, int ghost) {
   const Oracle *o = F->o;
   if (!o->use_restir) return V(0, 0, 0);
   if (o->n_lights == 0 || o->light_index[0] < 0) return V(0, 0, 0);
@@ -917,7 +929,7 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
   Res init = EMPTY_RES;
   int maxl = o->n_lights > 4 ? o->n_lights : 4;
   int eff = o->restir_samples < maxl ? o->restir_samples : maxl;
-  for (int i = 0; i < eff; i++) {
+  for (int i = 0; i < eff && !ghost; i++) { /* a ghost call skips every non-unrolled loop */
     v2 rv = hash2(sx + (float)i * 0.1f, sy + (float)i * 0.2f);
     int ai = (int)(rv.x * (float)o->n_lights);
     if (ai < 0) ai = 0;
@@ -977,7 +989,7 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
   int ns = 8;
   if (o->n_lights > 10) ns = 4;
   if (F->frame < 10u) ns = (ns / 2 > 2) ? ns / 2 : 2;
-  for (int i = 0; i < ns; i++) {
+  for (int i = 0; i < ns && !ghost; i++) {
     v2 sr = hash2(sx + (float)i * 0.3f, sy + (float)i * 0.4f);
     float ox = POISSON[i][0] * 16.0f / (float)o->w, oy = POISSON[i][1] * 16.0f / (float)o->h;
     float nx = scx + ox, ny = scy + oy;
@@ -1003,7 +1015,7 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
   else {
     float tp = evaluateTargetFunction(fr.pos, fr.col, hp, hn, mat);
     if (tp <= 0.0f) fr.W = 0.0f;
-    else if (!isVisible(F, hp, fr.pos)) fr.W = 0.0f;
+    else if (!(ghost ? ghost_isVisible(F, hp, fr.pos) : isVisible(F, hp, fr.pos))) fr.W = 0.0f;
     else {
       float cM = gclamp(fr.M, 1.0f, 40.0f);
       float raw = fr.ws / (tp * cM);
@@ -1022,6 +1034,7 @@ static v3 sampleLightsReSTIR(Frag *F, v3 hp, v3 hn, const Material *mat, float s
   F->fr_pos[0] = fr.pos.x; F->fr_pos[1] = fr.pos.y; F->fr_pos[2] = fr.pos.z;
   F->fr_col[0] = fr.col.x; F->fr_col[1] = fr.col.y; F->fr_col[2] = fr.col.z;
   F->fr_ws = fr.ws; F->fr_M = fr.M; F->fr_W = fr.W; F->fr_age = fr.age; F->fr_idx = fr.idx;
+  if (ghost) return V(0, 0, 0); /* only g_final_reservoir survives a ghost call */
   if (fr.W > 0.0f && fr.idx >= 0 && fr.idx < o->n_lights) {
     int ai = fr.idx;
     int act = o->light_index[ai];
@@ -1134,7 +1147,7 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
         if (o->n_lights > 8) {
           float sx = seed + 8652.1f * fr + bounce * 7895.13f;
           float sy = seed + 1234.567f * fr + bounce * 9876.54f;
-          tot = sampleLightsReSTIR(F, x, nl, mat, sx, sy);
+          tot = sampleLightsReSTIR(F, x, nl, mat, sx, sy, 0);
         } else {
           for (int i = 0; i < o->n_lights; ++i) {
             int idx = o->light_index[i];
@@ -1160,7 +1173,7 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
       if (o->use_restir_def) {
         float sx = seed + 8652.1f * fr + bounce * 7895.13f;
         float sy = seed + 1234.567f * fr + bounce * 9876.54f;
-        v3 rc = sampleLightsReSTIR(F, x, nl, mat, sx, sy);
+        v3 rc = sampleLightsReSTIR(F, x, nl, mat, sx, sy, 0);
         *acc = add(*acc, mul(rc, *mask));
       }
     } else if (o->use_mis && o->n_lights > 0) {
@@ -1191,20 +1204,61 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
   }
 }
 
-/* SwiftShader 4.1 executes the loop body with per-lane masks.  After a lane
- * executes `break` or `continue` in radiance()'s loop, the remaining statements
- * of that iteration still run for the lane with its register writes masked --
- * but writes to GLOBAL variables inside called functions (brdf's ++DIFF_BOUNCES /
- * ++SPEC_BOUNCES / ++SCATTERING_EVENTS and sampleLightsReSTIR's
- * g_final_reservoir) are not masked.  Locals assigned after the lane was
- * disabled (c, e, inside) keep the previous iteration's register values.
- * ghost_brdf() reproduces exactly those side effects: brdf on throw-away copies
- * of the caller's locals.  Derived from instrumenting the reference shader under
- * the oracle (tests/golden/manifest.json); only enabled for fixture parity. */
-static void ghost_brdf(Frag *F, const Hit *hit, v3 c, v3 e, float inside, v3 ro, v3 rd, v3 mask, int spec,
-                       float seed, int depth) {
-  v3 acc = V(0, 0, 0);
-  brdf(F, hit, c, e, inside, &ro, &rd, &mask, &acc, &spec, seed, (float)depth);
+/* SwiftShader 4.1's execution of `break` in radiance()'s bounce loop, as pinned
+ * by the known-answer shaders of oracle/gen/mask_kat.py (tests/golden/
+ * mask_kat.json) and by instrumented copies of the reference shader:
+ *  - after a lane executes `break`, the rest of that iteration still CALLS the
+ *    functions that follow (here brdf(), raytracer.glsl:2094) for the lane:
+ *    code inside a callee is not masked by the caller's break mask, so a global
+ *    it writes changes (g_final_reservoir, raytracer.glsl:1757);
+ *  - the callee sees its parameter registers as the lane's PREVIOUS call left
+ *    them: `in` arguments of that call, `inout` ones (r, mask, acc,
+ *    bounceIsSpecular) at their values after it -- the caller's copies into the
+ *    parameters are masked;
+ *  - loops inside the callee do not run for the lane (their masks start from
+ *    the caller's break mask), `if` blocks and straight-line code do.
+ * So the "ghost" brdf() repeats the previous call's material branch (with the
+ * post-call ray for COAT's Schlick pick) and, when that branch leaves the bounce
+ * non-specular and routes light sampling through sampleLightsReSTIR, the ghost
+ * sampleLightsReSTIR skips its candidate/temporal/spatial loops and stores an
+ * EMPTY reservoir (finalizeReservoir sets W = 0) as g_final_reservoir.  With
+ * no previous call the registers hold another fragment's values, but then
+ * g_final_reservoir is still EMPTY and stays EMPTY either way.  `continue`
+ * (the volumetric scatter, 2050) does not produce a ghost (mask_kat.json).
+ * Only enabled for fixture parity (SWIFTSHADER_GHOST). */
+typedef struct {
+  int have;      /* a live brdf() call happened in this fragment */
+  Hit hit;       /* its `in` arguments */
+  v3 e;
+  float inside, bounce;
+  v3 rd;         /* `inout` r.d and bounceIsSpecular after it */
+  int spec;
+} BrdfRegs;
+
+static void ghost_brdf(Frag *F, const BrdfRegs *g, float seed) {
+  const Oracle *o = F->o;
+  if (!g->have) return;
+  int spec = g->spec;
+  const Material *mat = &o->meshes[g->hit.index].mat;
+  if (mat->t == M_DIFF) spec = 0;
+  else if (mat->t == M_SPEC || mat->t == M_REFR_FRESNEL || mat->t == M_REFR_SCHLICK) spec = 1;
+  else if (mat->t == M_COAT) {
+    v3 nl = muls(g->hit.n, g->inside);
+    float nt = mat->nt;
+    float nt_eff = (o->use_spectral && nt < 0.0f) ? spectralIOR(F->hero, fabsf(nt)) : fabsf(nt);
+    spec = or_hash(seed) < schlick(g->rd, nl, 1.00029f, nt_eff);
+  }
+  if (spec || !o->sample_lights || !o->use_restir_def) return;
+  if (o->use_restir && o->use_mis) {
+    if (o->n_lights <= 8) return;
+  } else if (!o->use_restir) {
+    return;
+  }
+  /* ghost sampleLightsReSTIR on the previous call's x, nl, material and seed */
+  float fr = (float)F->frame;
+  float sx = seed + 8652.1f * fr + g->bounce * 7895.13f;
+  float sy = seed + 1234.567f * fr + g->bounce * 9876.54f;
+  sampleLightsReSTIR(F, g->hit.pos, muls(g->hit.n, g->inside), mat, sx, sy, 1);
 }
 
 /* radiance(), raytracer.glsl:1986-2105 */
@@ -1213,8 +1267,8 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
   v3 acc = V(0, 0, 0), mask = V(1, 1, 1);
   int spec = 1;
   v3 prev_nl = V(0, 1, 0);
-  v3 st_c = V(0, 0, 0), st_e = V(0, 0, 0); /* register values of c, e, inside */
-  float st_inside = 0.0f;
+  BrdfRegs regs; /* SWIFTSHADER_GHOST: brdf()'s parameter registers */
+  regs.have = 0;
   for (int depth = 0; depth < o->max_bounces; ++depth) {
     F->n_iter++;
     Hit hit;
@@ -1254,14 +1308,14 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         spec = 0;
         ++F->scat_ev;
         int stop = (F->scat_ev >= o->max_scatter || vmaxc(mask) < 0.01f);
-        if (o->ghost) ghost_brdf(F, &hit, st_c, st_e, st_inside, ro, rd, mask, spec, seed, depth);
+        if (o->ghost) ghost_brdf(F, &regs, seed);
         if (stop) break;
         continue;
       }
     }
     if (t == INF_T) {
       if (!spec && o->sample_lights) {
-        if (o->ghost) ghost_brdf(F, &hit, st_c, st_e, st_inside, ro, rd, mask, spec, seed, depth);
+        if (o->ghost) ghost_brdf(F, &regs, seed);
         break;
       }
       if (o->use_cubemap) {
@@ -1272,7 +1326,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
                    0.5f + 0.5f * cosf(TWO_PI * (0.409f + 0.8f * k)));
         acc = add(acc, mul(mask, sky));
       }
-      if (o->ghost) ghost_brdf(F, &hit, st_c, st_e, st_inside, ro, rd, mask, spec, seed, depth);
+      if (o->ghost) ghost_brdf(F, &regs, seed);
       break;
     }
     const Mesh *mesh = &o->meshes[hit.index];
@@ -1280,7 +1334,6 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
     v3 c = vmax3s(mix3(mesh->mat.c, mul(trgb, mesh->mat.tex_c_mask), (float)mesh->mat.opts[0] * hit.texel[3]), 0.001f);
     float inside = -gsign(dot3(rd, hit.n));
     v3 e = vmax3s(mix3(mesh->mat.e, mul(trgb, mesh->mat.tex_e_mask), (float)mesh->mat.opts[1] * hit.texel[3]), 0.001f);
-    st_c = c; st_e = e; st_inside = inside;
     if (mesh->mat.t == M_LIGHT) {
       mask = mul(mask, c);
       float w = 1.0f;
@@ -1291,11 +1344,15 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         w = powerHeuristic(1.0f, bp, 1.0f, lp);
       }
       acc = add(acc, muls(mul(mask, e), w));
-      if (o->ghost) ghost_brdf(F, &hit, c, e, inside, ro, rd, mask, spec, seed, depth);
+      if (o->ghost) ghost_brdf(F, &regs, seed);
       break;
     }
     prev_nl = muls(hit.n, inside);
     brdf(F, &hit, c, e, inside, &ro, &rd, &mask, &acc, &spec, seed, (float)depth);
+    if (o->ghost) {
+      regs.have = 1; regs.hit = hit; regs.e = e; regs.inside = inside; regs.bounce = (float)depth;
+      regs.rd = rd; regs.spec = spec;
+    }
     if (vmaxc(mask) < 0.01f) break;
     if (F->diff_b >= o->max_diff || F->spec_b >= o->max_spec || F->trans_b >= o->max_trans ||
         F->scat_ev >= o->max_scatter)

@@ -99,6 +99,10 @@ enum : uint32_t {
   F_VOL = 1u << 7,
   F_CUBEMAP = 1u << 8,  // #define USE_CUBEMAP
   F_ANIM = 1u << 9,     // RENDER_MODE 1 (animated: getAnimatedPosition + EMA accumulator)
+  // Reference-executor compatibility (rt0_set_executor_compat): reproduce how
+  // the oracle's GLES executor stores g_final_reservoir after a `break` of the
+  // bounce loop (oracle/gen/mask_kat.py).  Off = GLSL semantics.
+  F_EXEC_GHOST = 1u << 10,
 };
 
 struct LaunchParams {

@@ -93,6 +93,7 @@ struct rt0_ctx {
   int cube_size = 0;
   SceneDev host_scene;   // what d_scene holds (also the JIT's scene data)
   bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
+  bool exec_compat = false;  // rt0_set_executor_compat: F_EXEC_GHOST
   // the scene-specialised kernel of the current (scene, config): looked up once
   // per change instead of regenerating and hashing its source on every render
   void *jit_fn = nullptr;
@@ -515,7 +516,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.uULen = p.aspect * p.uVLen;
   p.aperture = c->cam_params[1];
   p.focal = c->cam_params[2];
-  p.flags = rt0h::flags_from_config(g);
+  p.flags = rt0h::flags_from_config(g) | (c->exec_compat ? F_EXEC_GHOST : 0u);
   p.max_bounces = g.max_bounces;
   p.max_diff = g.max_diff_bounces;
   p.max_spec = g.max_spec_bounces;
@@ -624,6 +625,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   if (c->use_jit && !c->counting) {
     if (c->jit_dirty || !c->jit_fn) {
       rt0h::JitKey key = rt0h::make_jit_key(c->cfg, c->n_sdfs);
+      if (c->exec_compat) key.flags |= F_EXEC_GHOST;
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
       int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit_fn, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
@@ -853,6 +855,13 @@ int rt0_device_accum(rt0_ctx *c, void **dptr, void **stream) {
 int rt0_set_jit(rt0_ctx *c, int enable) {
   if (!c) return RT0_E_ARG;
   c->use_jit = enable != 0;
+  return RT0_OK;
+}
+
+int rt0_set_executor_compat(rt0_ctx *c, int enable) {
+  if (!c) return RT0_E_ARG;
+  if (c->exec_compat != (enable != 0)) c->jit_dirty = true;
+  c->exec_compat = enable != 0;
   return RT0_OK;
 }
 

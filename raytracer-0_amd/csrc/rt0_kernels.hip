@@ -4,15 +4,13 @@
 // from HBM (DynScene) and the flags/constants from kernel arguments (DynCfg);
 // the scene-specialised instance is compiled at run time by rt0_jit.cpp.
 // Five instances: Cornell-class, +SDF, +volumetrics/spectral, +ReSTIR, and the
-// event-counting instance used for the FLOP model.
+// event-counting instance used for the FLOP model; each is its own translation
+// unit (rt0_pass_inst.hip, built once per RT0_VARIANT) so they compile in
+// parallel.  This file holds the small kernels and the launcher table.
 #include "rt0_integrator.h"
 
 using namespace rt0;
 
-template <bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
-__global__ __launch_bounds__(256) void rt0_pass_kernel(const LaunchParams P) {
-  pass_body<DynScene, DynCfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>(P, DynScene{P.scene}, DynCfg(P));
-}
 
 // frame-chunked launches: ordered sum of the per-frame samples (HBM-bound,
 // 16 B/sample read + 32 B/pixel)
@@ -43,17 +41,21 @@ __global__ __launch_bounds__(256) void rt0_tonemap_kernel(const float4 *__restri
 }
 
 // ------------------------------------------------------------ launchers
+extern "C" hipError_t rt0_launch_pass_v0(const LaunchParams *, dim3, hipStream_t);
+extern "C" hipError_t rt0_launch_pass_v1(const LaunchParams *, dim3, hipStream_t);
+extern "C" hipError_t rt0_launch_pass_v2(const LaunchParams *, dim3, hipStream_t);
+extern "C" hipError_t rt0_launch_pass_v3(const LaunchParams *, dim3, hipStream_t);
+extern "C" hipError_t rt0_launch_pass_v4(const LaunchParams *, dim3, hipStream_t);
+
 extern "C" hipError_t rt0_launch_pass(int variant, const LaunchParams *p, dim3 grid, hipStream_t stream) {
-  dim3 block(256);
   switch (variant) {
-    case 0: hipLaunchKernelGGL((rt0_pass_kernel<false, false, false, false, false>), grid, block, 0, stream, *p); break;
-    case 1: hipLaunchKernelGGL((rt0_pass_kernel<false, false, true, false, false>), grid, block, 0, stream, *p); break;
-    case 2: hipLaunchKernelGGL((rt0_pass_kernel<false, true, true, true, false>), grid, block, 0, stream, *p); break;
-    case 3: hipLaunchKernelGGL((rt0_pass_kernel<true, true, true, true, false>), grid, block, 0, stream, *p); break;
-    case 4: hipLaunchKernelGGL((rt0_pass_kernel<true, true, true, true, true>), grid, block, 0, stream, *p); break;
+    case 0: return rt0_launch_pass_v0(p, grid, stream);
+    case 1: return rt0_launch_pass_v1(p, grid, stream);
+    case 2: return rt0_launch_pass_v2(p, grid, stream);
+    case 3: return rt0_launch_pass_v3(p, grid, stream);
+    case 4: return rt0_launch_pass_v4(p, grid, stream);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 extern "C" hipError_t rt0_launch_sum(const LaunchParams *p, dim3 grid, hipStream_t stream) {

@@ -123,6 +123,9 @@ class GlslViewport {
     this.total_tiles = [Math.ceil(this.canvas.width / 32) - 1, Math.ceil(this.canvas.height / 32) - 1];
     this.viewport = this.tile_rendering ? [0, 0, 32, 32] : [0, 0, this.canvas.width, this.canvas.height];
     this._h = addon.create(this.canvas.width, this.canvas.height, this.device);
+    // opts.executorCompat: ReSTIR reservoirs as the reference's GLES executor
+    // stores them (rt0_set_executor_compat); default GLSL semantics
+    if (opts.executorCompat) addon.setExecutorCompat(this._h, true);
     this._compiled = null;
     this.images = {};
     // index.js:256-296: the RGBA noise image (u_rnd_tex) and opts.textures[0..3]

@@ -263,6 +263,16 @@ static napi_value SetTemporalFrames(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+static napi_value SetExecutorCompat(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  bool on = false;
+  napi_get_value_bool(env, argv[1], &on);
+  RC_OR_THROW(rt0_set_executor_compat(c, on ? 1 : 0));
+  return nullptr;
+}
+
 static napi_value ReadAccum(napi_env env, napi_callback_info info) {
   napi_value argv[1];
   if (!get_args(env, info, 1, argv)) return nullptr;
@@ -484,6 +494,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"setCamera", nullptr, SetCamera, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"render", nullptr, Render, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setTemporalFrames", nullptr, SetTemporalFrames, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setExecutorCompat", nullptr, SetExecutorCompat, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setViewport", nullptr, SetViewport, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readAccum", nullptr, ReadAccum, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"tonemap", nullptr, Tonemap, nullptr, nullptr, nullptr, napi_default, nullptr},

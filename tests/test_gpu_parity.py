@@ -4,7 +4,8 @@
   every config, single-sample passes 1..F, same tolerance as the oracle;
 * ReSTIR: conditional parity -- the reference's own reservoir buffers of passes
   k-1..k-3 are uploaded through rt0_write_restir_inputs, pass k's radiance
-  must match;
+  must match -- and the product's own unconditional 6-pass chain against the
+  reference's (rt0_set_executor_compat: the executor's reservoir stores);
 * against the CPU restatement at sizes the fixtures do not cover (128^2 bench
   scene, 12-bounce volumetric C4 scene).
 All calls go through include/rt0.h; nothing here can fall back to the CPU.
@@ -95,7 +96,7 @@ def test_gpu_matches_reference_fixture(name, cfgs, gpu_required):
     assert abs(s.mean() - g.mean()) <= MEAN_TOL.get(name, 5e-3) * max(1.0, abs(g.mean()))
 
 
-@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo"])
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo", "c5_spectral_sphere"])
 def test_gpu_restir_conditional_parity(name, cfgs, gpu_required):
     if not have(name):
         pytest.skip("fixture not generated")
@@ -115,21 +116,72 @@ def test_gpu_restir_conditional_parity(name, cfgs, gpu_required):
         assert 1.0 - ok.mean() <= BAD_FRAC.get(name, BAD_FRAC["default"]), (name, k, 1.0 - ok.mean())
 
 
+# SURVEY 8c on the unconditional chain: per pass <= 1% of pixels outside the
+# tolerance (discrete flips: a shadow ray grazing an edge under gfx950's
+# transcendentals); relative L2 of the mean over the passes <= 1e-3 on the
+# pixels that match in every pass, and <= 5e-3 including the flips (one
+# flipped light pixel of 4096 at pass 1 -- the same in the conditional test,
+# which uploads the reference's reservoirs -- gives 2.6e-3 on c3).  The nearly
+# black restir_mis_demo (mean radiance 6e-5, where a few ulp-level flips of
+# ~1e-4 dominate any relative norm) bounds the RMS of that mean instead.
+CHAIN_REL_L2 = {"c3_outdoor_restir": 1e-3, "anim_restir_demo": 1e-3, "c5_spectral_sphere": 1e-3}
+
+
+def chain_l2_ok(name, got, gold, ok_all):
+    m, g = got.mean(0), gold.mean(0)
+    if name not in CHAIN_REL_L2:
+        return np.sqrt(np.mean((m - g) ** 2)) <= 1e-3, "rms"
+    st = ok_all[..., None]
+    stable = np.linalg.norm((m - g) * st) / max(np.linalg.norm(g * st), 1e-30)
+    full = np.linalg.norm(m - g) / np.linalg.norm(g)
+    return stable <= CHAIN_REL_L2[name] and full <= 5e-3, (stable, full)
+
+
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo", "anim_restir_demo", "c5_spectral_sphere"])
+def test_gpu_restir_chain_matches_reference(name, cfgs, gpu_required):
+    """The product's own multi-pass ReSTIR (its swap chain of index.js:795-820,
+    nothing uploaded) against the reference's chained passes, with the
+    reservoir stores of the reference executor (rt0_set_executor_compat)."""
+    if not have(name):
+        pytest.skip("fixture not generated")
+    cfg = cfg_by_name(cfgs, name)
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    F, H, W = G["samples"].shape[:3]
+    r = make(cfgs, name, W, H)
+    r.set_executor_compat(True)
+    r.set_temporal_frames(cfg.get("temporal_frames", 5))
+    zero = np.zeros((H, W, 4), np.float32)
+    got = []
+    ok_all = np.ones((H, W), bool)
+    for k in range(1, F + 1):
+        r.write_accum(zero)  # single-sample pass (u_bufferA = 0), reservoirs chain on
+        r.render(k, 1, O.pass_time(cfg, k) if cfg.get("time_ms") else 0.0)
+        s = r.read_accum()
+        got.append(s)
+        ok, _ = pixel_match(s[..., :3], G["samples"][k - 1][..., :3])
+        ok_all &= ok
+        assert 1.0 - ok.mean() <= 0.01, (name, k, 1.0 - ok.mean())
+        m, a = r.read_restir(0)
+        okr = pixel_match(m, G["restir_main"][k - 1])[0] & pixel_match(a, G["restir_aux"][k - 1])[0]
+        assert 1.0 - okr.mean() <= 0.01, (name, k, "reservoirs", 1.0 - okr.mean())
+    good, l2 = chain_l2_ok(name, np.stack(got)[..., :3], G["samples"][..., :3], ok_all)
+    assert good, (name, l2)
+
+
 def test_gpu_restir_chain_matches_oracle_chain(cfgs, gpu_required):
-    """Unconditional multi-pass ReSTIR (the product's own swap chain) vs the
-    restatement's swap chain (GLSL semantics, no executor artefacts)."""
+    """GLSL semantics (executor compat off, the default): the product's
+    unconditional chain against the restatement's, both without the executor
+    artefact."""
     name = "c3_outdoor_restir"
     cfg = cfg_by_name(cfgs, name)
     o = O.Oracle(cfg, cfgs, width=64, height=64)
     s_ref, m_ref, a_ref = o.frames_restir(4)
     r = make(cfgs, name, 64, 64)
-    prev = np.zeros((64, 64, 4), np.float32)
+    zero = np.zeros((64, 64, 4), np.float32)
     for k in range(1, 5):
+        r.write_accum(zero)
         r.render(k, 1)
-        acc = r.read_accum()
-        sample = acc - prev
-        prev = acc
-        ok, _ = pixel_match(sample[..., :3], s_ref[k - 1][..., :3])
+        ok, _ = pixel_match(r.read_accum()[..., :3], s_ref[k - 1][..., :3])
         assert 1.0 - ok.mean() <= 0.03, (k, 1.0 - ok.mean())
         m, a = r.read_restir(0)
         okm, _ = pixel_match(m, m_ref[k - 1])

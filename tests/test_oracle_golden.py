@@ -6,10 +6,13 @@ shader run by SwiftShader (oracle/gen/make_golden.py).  This file checks:
     hash2 (308-312) and the bounce/NEE seed schedule -- BIT-EXACTLY;
   * single-sample radiance of every config within the tolerance below;
   * ReSTIR: with the reference's own reservoir buffers of passes k-1..k-3 as
-    input, pass k's radiance matches per pixel ("conditional parity"; the
-    reservoir MRTs themselves carry a SwiftShader masked-execution artefact
-    that the restatement models only under SWIFTSHADER_GHOST).
+    input, pass k's radiance matches per pixel ("conditional parity"), and,
+    with the executor's masked-execution behaviour after `break` modelled
+    (SWIFTSHADER_GHOST; pinned by the known-answer shaders of
+    oracle/gen/mask_kat.py, tests/golden/mask_kat.json), so do pass k's
+    reservoir outputs -- and then the unconditional 6-pass chain.
 """
+import json
 import os
 
 import numpy as np
@@ -114,7 +117,7 @@ def test_oracle_radiance_matches_reference(name, cfgs):
     assert abs(got[m].mean() - gold[m].mean()) <= MEAN_TOL.get(name, 2e-3) * max(1.0, abs(gold[m].mean()))
 
 
-@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo"])
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo", "c5_spectral_sphere"])
 def test_oracle_restir_conditional_parity(name, cfgs):
     if not have(name):
         pytest.skip("fixture %s not generated" % name)
@@ -132,6 +135,120 @@ def test_oracle_restir_conditional_parity(name, cfgs):
         s, _, _ = o.frame(k, ins)
         ok, _ = pixel_match(s[..., :3], G["samples"][k - 1][..., :3])
         assert 1.0 - ok.mean() <= BAD_FRAC.get(name, BAD_FRAC["default"]), (name, k, 1.0 - ok.mean())
+
+
+def _ghost_expected(name, stop):
+    """What the reference executor produces for mask_kat case `name` at a lane
+    that breaks at iteration `stop` (rules 1-6 of oracle/gen/mask_kat.py):
+    (g0, g1, o0) with g0 = None where the value is undefined (rule 3)."""
+    prev = stop - 1  # the lane's previous call (rule 2), none if stop == 0
+    val = None
+    if name in ("break_then_call", "global_in_callee_if", "nested_break"):
+        val, calls, loc = float(prev), stop + 1, float(stop)
+    elif name == "nested_call":
+        val, calls, loc = 2.0 * (10.0 * prev + 5.0), stop + 1, 10.0 * stop + 5.0
+    elif name in ("arg_before_break", "uniform_stop"):
+        val, calls, loc = 10.0 * prev + 5.0, stop + 1, 10.0 * stop + 5.0
+    elif name == "struct_arg":
+        val, calls, loc = 10.0 * prev + 5.0 + 100.0 * prev, stop + 1, 10.0 * stop + 5.0
+    elif name == "inout_arg":  # the inout parameter after the previous call: v + 0.5
+        val, calls, loc = 10.0 * prev + 5.5 + 1000.0 * prev, stop + 1, 10.0 * stop + 5.0
+    elif name == "global_in_loop":  # GLSL semantics (rule 1: loop-body writes are masked)
+        val, calls, loc = (float(prev) if stop > 0 else -1.0), stop, float(stop)
+        return val, calls, loc
+    elif name == "after_continue":  # GLSL semantics (rule 6)
+        return (5.0 if stop != 5 else 4.0), 5, 5.0
+    if stop == 0 and name in ("global_in_callee_if", "nested_call"):
+        calls = None  # the call's effect depends on a parameter (`on`, `b`) that is undefined
+    return (val if stop > 0 else None), calls, loc
+
+
+def test_mask_kat_model():
+    """Every output of the executor known-answer shaders follows rules 1-6
+    (mask_kat.py) -- the model the restatement's SWIFTSHADER_GHOST and the
+    product's rt0_set_executor_compat implement."""
+    K = json.load(open(os.path.join(GOLD, "mask_kat.json")))["cases"]
+    for name, rows in K.items():
+        for r in rows:
+            stop = r["stop"]
+            if name == "callee_loops":
+                # rule 5: loops of <= 4 constant iterations without break/continue
+                # are unrolled and run in the ghost call, the others do not
+                calls = stop + 1
+                assert r["g"] == [2.0 * calls, 3.0 * calls, 4.0 * calls, 5.0 * stop], (name, r)
+                assert r["o"] == [9.0 * stop, 2.0 * stop, 2.0 * stop, 3.0 * stop], (name, r)
+                continue
+            val, calls, loc = _ghost_expected(name, stop)
+            assert calls is None or r["g"][1] == calls, (name, r)
+            assert r["o"][0] == loc, (name, r)
+            if val is not None:
+                assert r["g"][0] == val, (name, r)
+    # GLSL semantics would give g1 == stop for the break cases: the artefact is real
+    assert any(r["g"][1] != r["stop"] for r in K["break_then_call"])
+
+
+def _res_match(a, b):
+    return (np.abs(a - b) <= REL_TOL * np.maximum(1.0, np.abs(b))).all(-1)
+
+
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo", "c5_spectral_sphere"])
+def test_oracle_restir_reservoirs_conditional(name, cfgs):
+    """Pass k's reservoir MRTs (g_final_reservoir, raytracer.glsl:2171-2174)
+    from the reference's own reservoirs of passes k-1..k-3: >= 99% of pixels
+    with the executor model, against 43% (c3) under plain GLSL semantics."""
+    if not have(name):
+        pytest.skip("fixture %s not generated" % name)
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    o = O.Oracle(cfg, cfgs, width=G["samples"].shape[2], height=G["samples"].shape[1],
+                 overrides={"SWIFTSHADER_GHOST": 1})
+    z = np.zeros_like(G["restir_main"][0])
+
+    def out(k, key):
+        return G[key][k - 1] if k >= 1 else z
+
+    for k in range(1, G["samples"].shape[0] + 1):
+        ins = [out(k - 1, "restir_main"), out(k - 1, "restir_aux"), out(k - 2, "restir_main"),
+               out(k - 2, "restir_aux"), out(k - 3, "restir_main"), out(k - 3, "restir_aux")]
+        _, m, a = o.frame(k, ins)
+        ok = _res_match(m, G["restir_main"][k - 1]) & _res_match(a, G["restir_aux"][k - 1])
+        assert ok.mean() >= 0.99, (name, k, ok.mean())
+
+
+# Unconditional chain vs the reference (SURVEY 8c): per pass <= 1% of pixels
+# outside the tolerance, and the relative L2 error of the mean over the passes
+# <= 1e-3.  restir_mis_demo is nearly black (mean radiance 6e-5: 0.02-radius
+# lights in a closed box); there two to five pixels whose ulp-level flips move
+# them by ~1e-4 absolute dominate the relative L2 (3.5e-3 measured), so its
+# bound is on the absolute L2 of that mean instead (<= 1e-3 per pixel, RMS).
+CHAIN_REL_L2 = {"c3_outdoor_restir": 1e-3, "anim_restir_demo": 1e-3, "c5_spectral_sphere": 1e-3}
+
+
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo", "anim_restir_demo", "c5_spectral_sphere"])
+def test_oracle_restir_chain_matches_reference(name, cfgs):
+    """The restatement's own 6-pass ReSTIR swap chain (index.js:795-820), with
+    the executor model, against the reference's chained passes."""
+    if not have(name):
+        pytest.skip("fixture %s not generated" % name)
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    F, H, W = G["samples"].shape[:3]
+    o = O.Oracle(cfg, cfgs, width=W, height=H, overrides={"SWIFTSHADER_GHOST": 1})
+    S, M, A = o.frames_restir(F, cfg)
+    if cfg.get("time_ms"):  # RENDER_MODE 1 fixture passes are mix(0, sample, 1/u_temporalFrames)
+        S = S / np.float32(cfg.get("temporal_frames", 5))
+    ok_all = np.ones((H, W), bool)
+    for k in range(F):
+        ok, _ = pixel_match(S[k][..., :3], G["samples"][k][..., :3])
+        ok_all &= ok
+        assert 1.0 - ok.mean() <= 0.01, (name, k + 1, 1.0 - ok.mean())
+        okr = _res_match(M[k], G["restir_main"][k]) & _res_match(A[k], G["restir_aux"][k])
+        assert 1.0 - okr.mean() <= 0.01, (name, k + 1, "reservoirs", 1.0 - okr.mean())
+    m, g = S[..., :3].mean(0), G["samples"][..., :3].mean(0)
+    if name in CHAIN_REL_L2:  # the restatement has no flipped pixels to exclude here: full image
+        assert np.linalg.norm(m - g) / np.linalg.norm(g) <= CHAIN_REL_L2[name]
+    else:
+        assert np.sqrt(np.mean((m - g) ** 2)) <= 1e-3
 
 
 def test_oracle_accumulation_is_sequential_sum(cfgs):
