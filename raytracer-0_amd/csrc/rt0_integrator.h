@@ -210,6 +210,23 @@ struct Hit {
   int type;  // -1 miss, else T_* (the uv/texel parser's dispatch, raytracer.glsl:1049-1078)
 };
 
+// A sphere-tracing march (iSDF, raytracer.glsl:979-984) handed out of
+// intersection() to the kernel's one march loop (SUSP kernels, see
+// Integrator::march_pending): the ray, the closest quadric distance it must
+// beat, and the loop state (t, step count, last map() id).  Marched in slices
+// of RT0_MARCH_BUDGET steps; `done` hands (t, id) back to intersection(),
+// which the caller repeats with the same ray -- the same sequence of map()
+// evaluations as the reference's uninterrupted loop.
+#ifndef RT0_MARCH_BUDGET
+#define RT0_MARCH_BUDGET 8
+#endif
+struct March {
+  v3 o, d;
+  float tmin, t, id;
+  int i;
+  bool active, done;
+};
+
 // SDF primitives, raytracer.glsl:496-528, 642-698
 DEV float sdBox(v3 p, v3 b) {
   v3 d = vabs(p) - b;
@@ -517,9 +534,13 @@ struct Geometry {
   // intersection(), raytracer.glsl:997-1082.  Returns tmin (INF_T = miss,
   // hit.index = 0 as HIT_MISS).  uv/texel parsing is omitted: only NULL_TEX
   // materials are accepted, so they never reach an output.
+  // With a March slot (ms != null) the SDF march is not run here: the first
+  // call records the ray in *ms and returns -1 (pending); once the kernel's
+  // march loop has finished it (ms->done), the same call with the same ray
+  // recomputes the quadric tests (deterministic) and completes the hit.
   template <bool SDF, class Cfg>
   static DEV float intersect(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, Hit &hit,
-                             unsigned long long &nmap) {
+                             unsigned long long &nmap, March *ms = nullptr) {
     hit.n = mk(0.f, 0.f, 0.f);
     hit.index = 0;
     int type = -1;
@@ -607,11 +628,22 @@ struct Geometry {
       if (sc.n_sdfs() > 0) {  // iSDF, 974-993
         float t = EPSILON * 4.0f;
         float id = 0.f;
-        for (int i = 0; i < C.marching_steps(); ++i) {
-          float dist = map(sc, o + d * t, id, nmap);
-          float h = fabsf(dist);
-          if (h < EPSILON || t > tmin) break;
-          t += h * C.fudge();
+        if (ms) {
+          if (ms->active) return -1.0f;  // still being marched
+          if (!ms->done) {
+            *ms = March{o, d, tmin, t, id, 0, true, false};
+            return -1.0f;
+          }
+          t = ms->t;
+          id = ms->id;
+          ms->done = false;
+        } else {
+          for (int i = 0; i < C.marching_steps(); ++i) {
+            float dist = map(sc, o + d * t, id, nmap);
+            float h = fabsf(dist);
+            if (h < EPSILON || t > tmin) break;
+            t += h * C.fudge();
+          }
         }
         if (!(t > tmin)) {
           hit.n = calcNormal(sc, o + d * t, nmap);
@@ -1041,9 +1073,9 @@ struct Integrator {
   // getAnimatedPosition (RENDER_MODE 1); the static position otherwise
   DEV v3 lpos(int i, const GeomRec &g) const { return flag(F_ANIM) ? anim_pos(P, i) : mk(g.px, g.py, g.pz); }
 
-  DEV float isect(v3 o, v3 d, Hit &h) {
+  DEV float isect(v3 o, v3 d, Hit &h, March *ms = nullptr) {
     if (COUNT) ++n_isect;
-    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map);
+    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map, ms);
   }
 
   // mix(mesh.mat.c, hit.texel.rgb, hit.texel.a) of a shadow ray's light hit
@@ -1061,7 +1093,9 @@ struct Integrator {
   }
 
   // calcDirectLighting, raytracer.glsl:1174-1230
-  DEV v3 direct_light(int li, v3 x, v3 nl, float seed) {
+  // ms/susp: resumable shadow-ray march (SUSP kernels); *susp = true when it
+  // was suspended (the call is repeated with the same arguments later)
+  DEV v3 direct_light(int li, v3 x, v3 nl, float seed, March *ms = nullptr, bool *susp = nullptr) {
     if (COUNT) ++n_nee;
     const GeomRec g = sc.geom(li);
     const MatRec lm = sc.mat(li);
@@ -1077,7 +1111,11 @@ struct Integrator {
         float t = 1.0f;
         hit.index = li;
 #else
-        float t = isect(x + nl * EPSILON, sr, hit);
+        float t = isect(x + nl * EPSILON, sr, hit, ms);
+        if (ms && t < 0.0f) {
+          *susp = true;
+          return dl;
+        }
 #endif
         const MatRec mh = sc.mat(hit.index);
         if (mh.type == M_LIGHT) {
@@ -1090,7 +1128,10 @@ struct Integrator {
       } else if (SDF && g.type == T_SDF) {
         v3 ld = lpos(li, g) + random_sphere_dir(seed + 78.2358f) * mk(g.j0, g.j1, g.j2);  // 1207
         v3 sr = normalize(ld - x);
-        isect(x + nl * EPSILON, sr, hit);
+        if (isect(x + nl * EPSILON, sr, hit, ms) < 0.0f && ms) {
+          *susp = true;
+          return dl;
+        }
         const MatRec mh = sc.mat(hit.index);
         if (mh.type == M_LIGHT) {
           v3 c = vmaxs(light_color(hit, mh), 0.001f);
@@ -1099,7 +1140,11 @@ struct Integrator {
       }
     } else if (lm.type == M_DIR_LIGHT) {
       v3 ld = mk(g.px, g.py, g.pz);
-      float t = isect(x + nl * EPSILON, ld, hit);
+      float t = isect(x + nl * EPSILON, ld, hit, ms);
+      if (ms && t < 0.0f) {
+        *susp = true;
+        return dl;
+      }
       if (t == INF_T) dl = (mk(lm.cr, lm.cg, lm.cb) * mk(lm.er, lm.eg, lm.eb)) * fmaxf(0.001f, dot(ld, nl));
     }
     return dl;
@@ -1463,14 +1508,160 @@ struct Integrator {
   // path ended can start its next sample while the rest of its wave is still
   // bouncing (path regeneration in pass_body).  The path state is what the
   // shader keeps across iterations.
+  //
+  // SUSP kernels (SDF scenes, path regeneration, no ReSTIR): a sphere-tracing
+  // march runs at most RT0_MARCH_BUDGET steps per call.  A lane whose march is
+  // unfinished returns from step() and resumes it at its next call, while the
+  // other lanes of its wave go on with their own bounces and samples -- so one
+  // long march no longer holds 63 finished lanes idle.  A bounce is two
+  // phases: 0 = its ray (and the shading that follows), 1 = its light
+  // sampling (one shadow ray per light), each resumable; every lane still
+  // performs exactly the operations of the uninterrupted loop, in order.
+  static constexpr bool SUSP = SDF && !RESTIR && !COUNT;
+  struct NeeCtx {
+    v3 x, n, acc;  // surface: hit point, nl, sum over lights; volume: scatter point, incoming rd
+    float seed;    // surface: the light-sampling seed base; volume: the path seed
+    int li;        // next light of the loop
+    bool vol, end;  // in-scatter NEE; the path ends after this bounce
+  };
   struct Path {
     v3 ro, rd, acc, mask, prev_nl;
     float seed;
     int depth;
     bool spec;
+    int phase;  // SUSP only
+    March ms;
+    NeeCtx nc;
   };
+  DEV March *march_slot(Path &ps) {
+    if constexpr (!SUSP) return nullptr;
+    // with triangle models the resumed call would walk the BVH again: no budget
+    if constexpr (Scene::kMayHaveModels)
+      if (sc.n_models() > 0 && P.n_tris > 0) return nullptr;
+    return &ps.ms;
+  }
+  // The kernel's one sphere-tracing loop (SUSP): up to RT0_MARCH_BUDGET steps
+  // of the lane's pending march, at a single program point for every lane of
+  // the wave whatever ray (camera, bounce, shadow) it belongs to.  The steps
+  // are iSDF's (raytracer.glsl:979-984) verbatim.
+  DEV void march_pending(Path &ps) {
+    March &m = ps.ms;
+    if (!m.active) return;
+    const int cap = C.marching_steps();
+    float t = m.t, id = m.id;
+    int i = m.i;
+    const int lim = min(cap, i + RT0_MARCH_BUDGET);
+    bool stop = i >= cap;
+    for (; i < lim; ++i) {
+      float dist = G::map(sc, m.o + m.d * t, id, n_map);
+      float h = fabsf(dist);
+      if (h < EPSILON || t > m.tmin) {
+        stop = true;
+        break;
+      }
+      t += h * C.fudge();
+    }
+    if (i >= cap) stop = true;
+    m.t = t;
+    m.id = id;
+    m.i = i;
+    if (stop) {
+      m.active = false;
+      m.done = true;
+    }
+  }
+  // phase 1 of a SUSP bounce: the light-sampling loop of brdf() (1899-1976,
+  // plain or MIS NEE) or of the in-scatter event (2011-2044), resumable per
+  // light.  false = suspended.
+  DEV bool nee_phase(Path &ps) {
+    NeeCtx &nc = ps.nc;
+    March *mq = march_slot(ps);
+    bool susp = false;
+    if (VOL && nc.vol) {
+#ifndef RT0_EXP_NO_VOL_NEE  // profiling experiment only (breaks parity): no in-scatter NEE
+      const v3 sp = nc.x, rd = nc.n;
+      const float seed = ps.seed;
+      const int depth = ps.depth;
+      for_lights(sc, [&](int li) {
+        if (susp || li < nc.li) return;
+        int lidx = sc.light(li);
+        if (lidx < 0) return;
+        const GeomRec lg = sc.geom(lidx);
+        const MatRec lmt = sc.mat(lidx);
+        if (lmt.type != M_LIGHT || lg.type != T_SPHERE) return;
+        v3 dlc = mk(lg.px, lg.py, lg.pz) - sp;
+        float dc = length(dlc);
+        float cam = fsqrt(1.0f - fminf(fmaxf(fdiv(lg.d0, dc * dc), 0.0f), 1.0f));
+        float idc = frcp(dc);
+        v3 dir = sample_cone(mk(dlc.x * idc, dlc.y * idc, dlc.z * idc), 1.0f - cam,
+                             nc_addmul(nc_addmul(seed + 2341.7f, (float)li, 917.3f), (float)depth, 199.1f));
+        Hit sh;
+        float ts = isect(sp + dir * (EPSILON * 20.0f), dir, sh, mq);
+        if (mq && ts < 0.0f) {
+          nc.li = li;
+          susp = true;
+          return;
+        }
+        if (sh.index != lidx) return;
+        float omega = 2.0f * (1.0f - cam);
+        float ct = dot(rd, dir);
+        constexpr float g2 = VOL_G * VOL_G;
+        float den = 1.0f + g2 - 2.0f * VOL_G * ct;
+        float phase = fdiv(1.0f - g2, FOUR_PI * den * fsqrt(den));
+        float Tf = fexp(-VOL_SIGMA_T * ts);
+        ps.acc = ps.acc + ((((ps.mask * mk(lmt.cr, lmt.cg, lmt.cb)) * mk(lmt.er, lmt.eg, lmt.eb)) * phase) * Tf) *
+                              (PI_F * omega);
+      });
+#endif
+      return !susp;
+    }
+    // sample_lights() without ReSTIR: use_restir routes nothing here
+    if (!flag(F_RESTIR)) {
+      if (flag(F_MIS) && sc.n_lights() > 0) {
+        for_lights(sc, [&](int i) {
+          if (susp || i < nc.li) return;
+          int idx = sc.light(i);
+          if (idx < 0) return;
+          const GeomRec lg = sc.geom(idx);
+          const MatRec lmt = sc.mat(idx);
+          if (lmt.type != M_LIGHT) return;
+          v3 ls = direct_light(idx, nc.x, nc.n, nc_addmul(nc.seed, (float)i, 123.456f), mq, &susp);
+          if (susp) {
+            nc.li = i;
+            return;
+          }
+          if (dot(ls, ls) > 0.000001f) {
+            v3 ld = normalize(lpos(idx, lg) - nc.x);  // 1959
+            nc.acc = nc.acc + ls * power_heuristic(light_pdf(lg, lmt, nc.x), cos_pdf(ld, nc.n));
+          }
+        });
+      } else {
+        for_lights(sc, [&](int i) {
+          if (susp || i < nc.li) return;
+          int idx = sc.light(i);
+          if (idx < 0) return;
+          v3 dl = direct_light(idx, nc.x, nc.n, nc.seed, mq, &susp);
+          if (susp) {
+            nc.li = i;
+            return;
+          }
+          nc.acc = nc.acc + dl;
+        });
+      }
+    }
+    if (susp) return false;
+    ps.acc = ps.acc + nc.acc * ps.mask;
+    return true;
+  }
   // false = the path ended (a `break` of the reference loop, or depth reached MAX_BOUNCES)
   DEV bool step(Path &ps) {
+    if constexpr (SUSP) {
+      if (ps.phase == 1) {  // resume this bounce's light sampling
+        if (!nee_phase(ps)) return true;
+        ps.phase = 0;
+        return ps.nc.end ? false : ++ps.depth < C.max_bounces();
+      }
+    }
     v3 &ro = ps.ro, &rd = ps.rd, &acc = ps.acc, &mask = ps.mask, &prev_nl = ps.prev_nl;
     bool &spec = ps.spec;
     const float seed = ps.seed;
@@ -1479,13 +1670,30 @@ struct Integrator {
     {
     if (COUNT) ++n_iter;
     Hit hit;
-    float t = isect(ro, rd, hit);
+    float t = isect(ro, rd, hit, march_slot(ps));
+    if (SUSP && t < 0.0f) return true;  // march pending: step() repeats this bounce once it is done
     if constexpr (VOL) {
       if (flag(F_VOL)) {
         float sd = -flog(fmaxf(hash(nc_addmul(seed + 4729.3f, (float)depth, 991.1f)), 1e-6f)) / VOL_SIGMA_T;
         if (sd < fminf(INF_T, t)) {
           v3 sp = ro + rd * sd;
           mask = mask * (VOL_SIGMA_S / VOL_SIGMA_T);
+          if constexpr (SUSP) {  // the in-scatter NEE becomes phase 1 (it reads sp, the incoming rd and mask)
+            const v3 rd_in = rd;
+            rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
+            ro = sp;
+            spec = false;
+            ++scat_ev;
+            const bool stop = scat_ev >= C.max_scatter() || vmaxc(mask) < 0.01f;
+            if (flag(F_SAMPLE_LIGHTS)) {
+              ps.nc = NeeCtx{sp, rd_in, mk(0.f, 0.f, 0.f), seed, 0, true, stop};
+              ps.phase = 1;
+              if (!nee_phase(ps)) return true;
+              ps.phase = 0;
+            }
+            return stop ? false : ++ps.depth < C.max_bounces();
+          }
+#ifndef RT0_EXP_NO_VOL_NEE  // profiling experiment only (breaks parity): no in-scatter NEE
           if (flag(F_SAMPLE_LIGHTS)) {
             for_lights(sc, [&](int li) {
               int lidx = sc.light(li);
@@ -1513,6 +1721,7 @@ struct Integrator {
                               (PI_F * omega);
             });
           }
+#endif
           rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
           ro = sp;
           spec = false;
@@ -1644,6 +1853,17 @@ struct Integrator {
         acc = acc + mask * mk(cm.r, cm.g, cm.b);
       }
     }
+    if constexpr (SUSP) {  // light sampling becomes phase 1; the end tests below do not depend on it
+      const bool end = vmaxc(mask) < 0.01f || diff_b >= C.max_diff() || spec_b >= C.max_spec() || 0 >= C.max_trans() ||
+                       scat_ev >= C.max_scatter();
+      if (!spec && flag(F_SAMPLE_LIGHTS)) {
+        ps.nc = NeeCtx{x, nl, mk(0.f, 0.f, 0.f), nc_seed4(seed, 8652.1f, fr, 5681.123f, bounce, 7895.13f), 0, false, end};
+        ps.phase = 1;
+        if (!nee_phase(ps)) return true;
+        ps.phase = 0;
+      }
+      return end ? false : ++ps.depth < C.max_bounces();
+    }
     if (!spec && flag(F_SAMPLE_LIGHTS)) acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;
     // ---- end brdf
     if (ghost_on()) {
@@ -1666,6 +1886,7 @@ struct Integrator {
     Path ps{ro, rd, mk(0.f, 0.f, 0.f), mk(1.f, 1.f, 1.f), mk(0.f, 1.f, 0.f), seed, 0, true};
     if (C.max_bounces() > 0)
       while (step(ps)) {
+        if constexpr (SUSP) march_pending(ps);
       }
     return ps.acc;
   }
@@ -1724,6 +1945,7 @@ struct Integrator {
     begin(ps, px, py);
     if (C.max_bounces() > 0)
       while (step(ps)) {
+        if constexpr (SUSP) march_pending(ps);
       }
     return finish(ps);
   }
@@ -1798,7 +2020,8 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       it.begin(ps, px, py);
       bool alive = cfg.max_bounces() > 0;
       while (true) {
-        if (alive) alive = it.step(ps);
+        // a lane whose march is still pending skips step() (its bounce resumes once it is done)
+        if (alive && !(decltype(it)::SUSP && ps.ms.active)) alive = it.step(ps);
         if (!alive) {
           accumulate(it, P, a, it.finish(ps));
           if (++f >= P.nframes) break;
@@ -1806,6 +2029,7 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
           it.begin(ps, px, py);
           alive = cfg.max_bounces() > 0;
         }
+        if constexpr (decltype(it)::SUSP) it.march_pending(ps);
       }
     }
     P.accum[apix] = a;
