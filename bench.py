@@ -88,14 +88,32 @@ def isect_flop(scene):
 MAP_FLOP = {0: 17.0, 1: 16.0, 2: 8.0, 3: 18.0, 4: 16.0, 5: 140.0, 6: 190.0}
 
 
+# Terms the SURVEY 8d formula leaves out, counted from source the same way
+# (per event, events counted by the counting instance, rt0_read_counters_n):
+#  - ReSTIR (raytracer.glsl:1619-1801): per sampleLightsReSTIR call the
+#    finalize + weight arithmetic (1525-1576, 1759-1795) 90; per candidate
+#    (hash2, light pick, evaluateTargetFunction 1361-1387, updateReservoir)
+#    80; per temporal tap (hash2 jitter, two bilinear RGBA32F fetches, unpack
+#    1437-1468, isValidReservoir, decay, combineReservoirs 1579-1611) 210; per
+#    spatial tap (the same without the motion/decay terms) 180.  The
+#    visibility ray is already an intersection() and the final
+#    calcDirectLighting a NEE call.
+#  - triangle models (no reference code): per BVH node visited two slab tests
+#    50, per Moller-Trumbore test (raytracer.glsl:864-892, commented out) 45.
+RESTIR_FLOP = {"restir": 90.0, "restir_cand": 80.0, "restir_ttap": 210.0, "restir_stap": 180.0}
+BVH_FLOP = {"bvh_node": 50.0, "tri": 45.0}
+
+
 def flop_per_sample(c, wl):
     """SURVEY 8d algorithmic FLOP model, per sample:
-    140 + C_isect*isect + 130*iter + (140 + 54*mis)*nee + C_map*map."""
+    140 + C_isect*isect + 130*iter + (140 + 54*mis)*nee + C_map*map,
+    plus the ReSTIR and BVH terms above."""
     n = max(1, c["samples"])
     mis = bool(wl["constants"].get("use_mis", False))
     c_map = sum(MAP_FLOP[k] for k in wl.get("sdf_kinds", [])) or 0.0
+    extra = sum(w * c.get(k, 0) for k, w in list(RESTIR_FLOP.items()) + list(BVH_FLOP.items())) / n
     return (140.0 + isect_flop(wl["scene_lines"]) * c["isect"] / n + 130.0 * c["iter"] / n
-            + (140.0 + 54.0 * mis) * c["nee"] / n + c_map * c["map"] / n)
+            + (140.0 + 54.0 * mis) * c["nee"] / n + c_map * c["map"] / n + extra)
 
 
 def host_threads():
@@ -340,7 +358,7 @@ def main():
             "traffic_unit": "bytes/launch",
             "traffic_source": ("profiles/%s/pmc_%s.json" % (PROFILE_ROUND, args.config)) if pmc else None,
             "flop_per_sample": round(fps, 1),
-            "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3) for k in ("isect", "iter", "nee", "map")},
+            "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3) for k in cnt if k != "samples"},
             "kernel_ms_per_step": round(kern_s * 1000.0, 3),
             "launches_per_step": job.launches,
             "kernel_ms_per_launch": round(kern_launch_s * 1000.0, 3),

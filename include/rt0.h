@@ -308,6 +308,14 @@ int rt0_jit_compile(const char *scene_text, const char *const *sdf_meshes, int n
  * instance; it never runs in a timed render unless enabled. */
 int rt0_set_counting(rt0_ctx *ctx, int enable);
 int rt0_read_counters(rt0_ctx *ctx, uint64_t out[5]);
+/* All event counters (the first five as above), for the FLOP model of the
+ * ReSTIR and triangle-model workloads: [5] sampleLightsReSTIR calls,
+ * [6] ReSTIR candidates evaluated (raytracer.glsl:1635-1654), [7] temporal
+ * history taps read (1485-1523), [8] spatial taps read (1725-1748), [9] BVH
+ * nodes visited, [10] triangle tests.  Copies min(n, RT0_N_COUNTERS) values
+ * (zero-fills the rest); returns RT0_N_COUNTERS. */
+#define RT0_N_COUNTERS 11
+int rt0_read_counters_n(rt0_ctx *ctx, uint64_t *out, int n);
 
 /* Wall time of the kernels of the last rt0_render (HIP events on the
  * context's stream), milliseconds, and the number of kernel launches. */

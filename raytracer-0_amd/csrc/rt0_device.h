@@ -127,7 +127,7 @@ struct LaunchParams {
   int32_t compact;  // accum holds only this shard's bands: row r of the band-compressed grid
   const float4 *rin[6];  // spatial main/aux, history1 main/aux, history2 main/aux
   float4 *rout_main, *rout_aux;
-  unsigned long long *counters;  // 5 x u64 (counting instance only)
+  unsigned long long *counters;  // RT0_N_COUNTERS x u64 (counting instance only)
   // Sharded ReSTIR: rows [valid_lo, valid_hi) of the input reservoir planes hold
   // data (own block + exchanged halo); a bilinear fetch outside them bumps
   // *halo_miss (null when the whole image is local).

@@ -76,7 +76,7 @@ struct rt0_ctx {
   bool counting = false;
   int temporal_frames = 5;
   int vp[4] = {0, 0, 0, 0};  // gl.viewport (x, y, w, h); w or h <= 0 = whole canvas  // GlslViewport.temporalFrames (index.js:236) -> u_temporalFrames
-  uint64_t counters[5] = {};
+  uint64_t counters[RT0_N_COUNTERS] = {};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
   int last_launches = 0;
@@ -161,7 +161,7 @@ int rt0_create(int width, int height, int device, rt0_ctx **out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipMalloc(&c->d_scene, sizeof(SceneDev)) != hipSuccess ||
-      hipMalloc(&c->d_counters, 5 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc(&c->d_counters, RT0_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess ||
       hipMalloc(&c->d_halo_miss, sizeof(uint32_t)) != hipSuccess ||
       hipMemset(c->d_halo_miss, 0, sizeof(uint32_t)) != hipSuccess) {
     rt0_destroy(c);
@@ -638,7 +638,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       return rt0h::jit_launch(jit_fn, &lp, grid.x, grid.y, gz, c->stream) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
     return rt0_launch_pass(variant, &lp, dim3(grid.x, grid.y, gz), c->stream);
   };
-  if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 5 * sizeof(unsigned long long), c->stream));
+  if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, RT0_N_COUNTERS * sizeof(unsigned long long), c->stream));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   int launches = 0;
   if (restir) {
@@ -719,9 +719,9 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
     if (c->counting) {
-      unsigned long long h[5];
+      unsigned long long h[RT0_N_COUNTERS];
       HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
-      for (int i = 0; i < 5; i++) c->counters[i] = h[i];
+      for (int i = 0; i < RT0_N_COUNTERS; i++) c->counters[i] = h[i];
     }
   }
   return RT0_OK;
@@ -754,9 +754,9 @@ int rt0_sync(rt0_ctx *c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->last_launches) HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
   if (c->counting) {
-    unsigned long long h[5];
+    unsigned long long h[RT0_N_COUNTERS];
     HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
-    for (int i = 0; i < 5; i++) c->counters[i] = h[i];
+    for (int i = 0; i < RT0_N_COUNTERS; i++) c->counters[i] = h[i];
   }
   return RT0_OK;
 }
@@ -937,6 +937,13 @@ int rt0_read_counters(rt0_ctx *c, uint64_t out[5]) {
   if (!c || !out) return RT0_E_ARG;
   for (int i = 0; i < 5; i++) out[i] = c->counters[i];
   return RT0_OK;
+}
+
+int rt0_read_counters_n(rt0_ctx *c, uint64_t *out, int n) {
+  if (!c || !out || n < 0) return RT0_E_ARG;
+  for (int i = 0; i < n && i < RT0_N_COUNTERS; i++) out[i] = c->counters[i];
+  for (int i = RT0_N_COUNTERS; i < n; i++) out[i] = 0;
+  return RT0_N_COUNTERS;
 }
 
 int rt0_scratch_bytes(const rt0_ctx *c, size_t *bytes) {

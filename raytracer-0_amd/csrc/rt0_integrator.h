@@ -335,7 +335,7 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
 // first, the far child on a per-lane stack in LDS (stride = block size so the
 // 64 lanes of a wave hit 64 different banks).  Returns the leaf-order triangle
 // index or -1; tmin is updated.
-DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
+DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
   __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
   int32_t *stk = stk_base + threadIdx.x;
   int sp = 0, node = 0, best = -1;
@@ -414,6 +414,7 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
     float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
     float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
     int cl = lk.x, cr = lk.y;
+    if (cnt) ++cnt[0];  // counting instance: nodes visited (two child boxes each)
 #if RT0_LEAF_UNIFIED
     // leaves are tested in place, left before right; the first leaf test of
     // every lane runs in one block whichever side it is on
@@ -429,6 +430,7 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
     }
     if (l0 >= 0) {
       float t;
+      if (cnt) cnt[1] += 1 + (l1 >= 0);  // triangle tests
       if (tri_test(tris[l0], o, d, tmin, t)) {
         tmin = t;
         best = l0;
@@ -540,7 +542,7 @@ struct Geometry {
   // recomputes the quadric tests (deterministic) and completes the hit.
   template <bool SDF, class Cfg>
   static DEV float intersect(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, Hit &hit,
-                             unsigned long long &nmap, March *ms = nullptr) {
+                             unsigned long long &nmap, March *ms = nullptr, unsigned long long *nbvh = nullptr) {
     hit.n = mk(0.f, 0.f, 0.f);
     hit.index = 0;
     int type = -1;
@@ -605,7 +607,7 @@ struct Geometry {
     });
     if constexpr (Scene::kMayHaveModels) {  // TRIANGLE models (after the quadrics, before the SDF march)
       if (sc.n_models() > 0 && P.n_tris > 0) {
-        const int ti = bvh_closest(P, o, d, m, tmin);
+        const int ti = bvh_closest(P, o, d, m, tmin, nbvh);
         if (ti >= 0) {
           const TriDev T = P.tris[ti];
           const v3 e0 = mk(T.e0x, T.e0y, T.e0z), e1 = mk(T.e1x, T.e1y, T.e1z);
@@ -1057,6 +1059,9 @@ struct Integrator {
   float hero;
   int diff_b, spec_b, scat_ev;
   unsigned long long n_isect, n_iter, n_nee, n_map;
+  // counting instance only: ReSTIR calls / candidates / temporal taps /
+  // spatial taps, BVH nodes / triangle tests (rt0_read_counters_n [5..10])
+  unsigned long long n_restir = 0, n_cand = 0, n_ttap = 0, n_stap = 0, n_bvh[2] = {0, 0};
   Res fin;  // g_final_reservoir (raytracer.glsl:1616)
   // F_EXEC_GHOST: brdf()'s parameter registers as the lane's last live call
   // left them (see ghost_brdf)
@@ -1075,7 +1080,7 @@ struct Integrator {
 
   DEV float isect(v3 o, v3 d, Hit &h, March *ms = nullptr) {
     if (COUNT) ++n_isect;
-    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map, ms);
+    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map, ms, COUNT ? n_bvh : nullptr);
   }
 
   // mix(mesh.mat.c, hit.texel.rgb, hit.texel.a) of a shadow ray's light hit
@@ -1271,6 +1276,7 @@ struct Integrator {
     if (!flag(F_RESTIR)) return mk(0.f, 0.f, 0.f);
     const int nl = sc.n_lights();
     if (nl == 0 || sc.light(0) < 0) return mk(0.f, 0.f, 0.f);
+    if (COUNT && !GHOST) ++n_restir;
     const float scx = fcx / P.res_x, scy = fcy / P.res_y;
     Res init = empty_res();
     int eff = GHOST ? 0 : min(C.restir_samples(), max(4, nl));
@@ -1282,6 +1288,7 @@ struct Integrator {
       if (li < 0 || li >= sc.n_meshes() + sc.n_sdfs()) continue;
       const GeomRec lg = sc.geom(li);
       const MatRec lmt = sc.mat(li);
+      if (COUNT) ++n_cand;
       v3 lp = lpos(li, lg);  // 1645
       v3 lc = mk(lmt.cr, lmt.cg, lmt.cb) * mk(lmt.er, lmt.eg, lmt.eb);
       float tv = target_fn(lp, lc, hp, hn, mat);
@@ -1314,6 +1321,7 @@ struct Integrator {
           float px = (scx + m3.x * ms) + (hjx - 0.5f) * 0.002f;
           float py = (scy + m3.y * ms) + (hjy - 0.5f) * 0.002f;
           if (!(px < 0.01f || px > 0.99f || py < 0.01f || py > 0.99f)) {
+            if (COUNT && !GHOST) ++n_ttap;
             float4 md = tex2d(P.rin[lvl == 0 ? 2 : 4], px, py);
             float4 ad = tex2d(P.rin[lvl == 0 ? 3 : 5], px, py);
             h = unpack(md, ad);
@@ -1354,7 +1362,10 @@ struct Integrator {
       hash2(nc_addmul(sx, (float)i, 0.3f), nc_addmul(sy, (float)i, 0.4f), srx, sry);
       float nx = scx + (PX[i] * 16.0f) / P.res_x, ny = scy + (PY[i] * 16.0f) / P.res_y;
       Res nb = empty_res();
-      if (!(nx < 0.0f || nx > 1.0f || ny < 0.0f || ny > 1.0f)) nb = unpack(tex2d(P.rin[0], nx, ny), tex2d(P.rin[1], nx, ny));
+      if (!(nx < 0.0f || nx > 1.0f || ny < 0.0f || ny > 1.0f)) {
+        if (COUNT) ++n_stap;
+        nb = unpack(tex2d(P.rin[0], nx, ny), tex2d(P.rin[1], nx, ny));
+      }
       if (nb.M > 0.0f) {
         if (nb.idx >= 0) {
           v3 ldf = nb.pos - hp;
@@ -2058,6 +2069,12 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     atomicAdd(&P.counters[2], it.n_nee);
     atomicAdd(&P.counters[3], it.n_map);
     atomicAdd(&P.counters[4], (unsigned long long)P.nframes);
+    atomicAdd(&P.counters[5], it.n_restir);
+    atomicAdd(&P.counters[6], it.n_cand);
+    atomicAdd(&P.counters[7], it.n_ttap);
+    atomicAdd(&P.counters[8], it.n_stap);
+    atomicAdd(&P.counters[9], it.n_bvh[0]);
+    atomicAdd(&P.counters[10], it.n_bvh[1]);
   }
 }
 

@@ -30,7 +30,7 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_accum_buffer_compact", "rt0_set_restir_buffers", "rt0_device_restir",
            "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_set_executor_compat", "rt0_jit_compile", "rt0_set_counting",
-           "rt0_read_counters", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
+           "rt0_read_counters", "rt0_read_counters_n", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
            "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read",
            "rt0_set_temporal_frames", "rt0_set_viewport", "rt0_scratch_bytes"]
 
@@ -131,6 +131,7 @@ def lib():
                                     ctypes.c_char_p, ctypes.c_size_t]),
         "rt0_set_counting": (c_int, [c_void_p, c_int]),
         "rt0_read_counters": (c_int, [c_void_p, P(ctypes.c_uint64)]),
+        "rt0_read_counters_n": (c_int, [c_void_p, P(ctypes.c_uint64), c_int]),
         "rt0_last_kernel_ms": (c_int, [c_void_p, P(c_float), P(c_int)]),
         "rt0_scratch_bytes": (c_int, [c_void_p, P(ctypes.c_size_t)]),
         "rt0_version": (ctypes.c_char_p, []),
@@ -531,10 +532,15 @@ class Renderer:
     def set_counting(self, on):
         self._chk(lib().rt0_set_counting(self.h, int(bool(on))))
 
+    COUNTER_NAMES = ("isect", "iter", "nee", "map", "samples", "restir", "restir_cand", "restir_ttap",
+                     "restir_stap", "bvh_node", "tri")
+
     def counters(self):
-        out = (ctypes.c_uint64 * 5)()
-        self._chk(lib().rt0_read_counters(self.h, out))
-        return dict(zip(("isect", "iter", "nee", "map", "samples"), list(out)))
+        out = (ctypes.c_uint64 * len(self.COUNTER_NAMES))()
+        rc = lib().rt0_read_counters_n(self.h, out, len(out))
+        if rc < 0:
+            self._chk(rc)
+        return dict(zip(self.COUNTER_NAMES, list(out)))
 
     def samples_bytes(self):
         """Device scratch of frame-chunked launches (rt0_scratch_bytes)."""

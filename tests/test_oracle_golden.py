@@ -97,7 +97,8 @@ def test_rng_hash_schedule_bitexact():
 
 NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
               "c4_mandelbulb_vol", "spectral_vol", "mis_demo_sdfbox", "menger_coat", "thinlens_glass",
-              "tex_sdf_metal", "tex_light_sphere", "tex_check_test", "cube_spheres", "cube_sdf_metal"]
+              "tex_sdf_metal", "tex_light_sphere", "tex_check_test", "cube_spheres", "cube_sdf_metal",
+              "sdf_triprism", "sdf_cone", "spectral_cornell", "vol_cornell_2"]
 
 
 @pytest.mark.parametrize("name", NON_RESTIR)
