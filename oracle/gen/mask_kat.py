@@ -27,7 +27,13 @@ these rules):
      also when every lane of the quad breaks together);
   5. loops inside the callee run for the lane only when the compiler unrolls
      them -- constant trip count <= 4 with no break/continue (callee_loops);
-  6. `continue` does not produce the effect (after_continue).
+  6. `continue` does not produce the effect (after_continue);
+  7. a local array indexed by a loop variable inside a function (map()'s
+     `sdf_meshes[i]`, raytracer.glsl:701-709) is read at the index held by
+     the FIRST lane of the 2x2 quad (x, y both even): once that lane has
+     left the caller's loop, the other three read a stale index -- here
+     element 0 (local_array_index).  This is why two-SDF scenes render
+     differently with their SDF statements swapped.
 The summary (per-pixel outputs of every case) is tests/golden/mask_kat.json.
 
 usage: python3 oracle/gen/mask_kat.py
@@ -230,6 +236,29 @@ void main() {
     if (i == stop) break;
     work(loc);
   }
+""",
+    # 7: a callee's local array indexed by its loop variable (map()'s
+    # sdf_meshes[i] min-combine) while quad-mates have left the caller's loop;
+    # per-iteration results in g0..g3, o0..o1
+    "local_array_index": """
+float f(float v) {
+  float arr[2];
+  arr[0] = v;
+  arr[1] = 0.5 * v;
+  float r = arr[0];
+  for (int i = 1; i < 2; ++i) r = mix(arr[i], r, float(r < arr[i]));
+  return r;
+}
+void main() {
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  float acc[6];
+  for (int k = 0; k < 6; ++k) acc[k] = -1.0;
+  for (int i = 0; i < 6; ++i) {
+    acc[i] = f(float(i + 1) * 10.0 + gl_FragCoord.x);
+    if (i == stop) break;
+  }
+  g0 = acc[0]; g1 = acc[1]; g2 = acc[2]; g3 = acc[3];
+  float o0 = acc[4], o1 = acc[5], o2 = 0.0, o3 = 0.0;
 """,
     # 6: continue instead of break
     "after_continue": """

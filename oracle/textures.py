@@ -1,4 +1,5 @@
-"""Deterministic synthetic asset textures for the texture fixtures.
+"""Asset textures for the texture fixtures: the reference's own files, and
+deterministic synthetic stand-ins.
 
 TEST INFRASTRUCTURE ONLY (imported by oracle/gen/make_golden.py and tests/).
 The reference samples four image textures (textures/tex0-3.png, index.html:262)
@@ -16,7 +17,35 @@ restatement and the GPU see the same texels:
   an alpha channel that varies over the image (MAT_LIGHT_4_TEX / MAT_TEST mix
   by texel.a, raytracer.glsl:1203, 2071).
 """
+import os
+
 import numpy as np
+
+# The reference's asset files, copied unchanged as test inputs
+# (tests/golden/assets/: textures/rgba_noise/rgba_noise256.png,
+# textures/tex0-3.png, cubemaps/Tropical Beach/*.jpg).  Decoded with Pillow --
+# PNG is lossless, and Pillow's libjpeg is the decoder family browsers use for
+# the reference's JPEG faces; the same pixels go to the reference executor
+# (oracle/gen/glrun.c), the restatement and the GPU, so the fixtures test the
+# integrator, not the decoders (rt0's own PNG/JPEG decoders are checked
+# against Pillow in tests/test_image_io.py).
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "assets")
+# index.html:267-270: left, bottom, back, right, top, front = -X -Y -Z +X +Y +Z
+CUBE_FACES = ("left", "bottom", "back", "right", "top", "front")
+
+
+def asset_rgba(name):
+    """RGBA8 [h, w, 4] of an asset file; RGB images get alpha 255 (what
+    texImage2D(RGBA) of an opaque image holds)."""
+    from PIL import Image
+    im = Image.open(os.path.join(ASSETS, name))
+    return np.asarray(im.convert("RGBA"), np.uint8).copy()
+
+
+def asset_cube():
+    from PIL import Image
+    return [np.asarray(Image.open(os.path.join(ASSETS, "tropical_beach", f + ".jpg")).convert("RGB"), np.uint8).copy()
+            for f in CUBE_FACES]
 
 
 def _hash32(x):
@@ -70,16 +99,26 @@ def cube_faces(n=64):
 
 
 def cubemap_for(cfg):
-    """Cube faces for a configs.json entry with "cubemap": true, else None."""
-    return cube_faces(64) if cfg.get("cubemap") else None
+    """Cube faces for a configs.json entry: "cubemap": true -> the synthetic
+    faces, "asset" -> the reference's Tropical Beach faces, else None."""
+    c = cfg.get("cubemap")
+    if c == "asset":
+        return asset_cube()
+    return cube_faces(64) if c else None
 
 
 def textures_for(cfg):
     """{unit: uint8 [h, w, 4]} for a configs.json entry's "textures" list
-    ("noise" -> unit 4 = u_rnd_tex; "imageN" -> unit N = u_texN)."""
+    ("noise" -> unit 4 = u_rnd_tex; "imageN" -> unit N = u_texN; the
+    reference's files: "asset:noise" -> unit 4, "asset:texN" -> unit N)."""
     out = {}
     for name in cfg.get("textures", []):
-        if name == "noise":
+        if name == "asset:noise":
+            out[4] = asset_rgba("rgba_noise256.png")
+        elif name.startswith("asset:tex"):
+            k = int(name[9:])
+            out[k] = asset_rgba("tex%d.png" % k)
+        elif name == "noise":
             out[4] = noise256()
         elif name.startswith("image"):
             k = int(name[5:])
