@@ -139,6 +139,10 @@ struct LaunchParams {
   // to the accumulator in frame order (the same sequential sum).  samples ==
   // null: one chunk, accumulated in registers.
   int32_t frame_chunk;
+  // ReSTIR passes (one sample per pixel per launch): each wave owns a pool of
+  // 64*refill pixels (refill 8x8 blocks stacked in y) and a lane whose path
+  // ended takes the pool's next pixel; 1 = one pixel per lane
+  int32_t refill;
   float4 *samples;
   // Asset textures: RGBA8 texels (R in the low byte), row 0 = t 0; null =
   // unbound unit.

@@ -32,6 +32,8 @@ extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_mo
 // shard of the 1024^2 bench image: 0.96 / 0.95 / 0.91 of linear for 2 / 4 / 8
 // shards, against 0.89 / 0.78 / 0.61 unchunked).
 static const long kTargetWaves = 16384;
+// Pixels per lane of a ReSTIR pass (LaunchParams::refill); RT0_REFILL overrides.
+static const int kRestirRefill = 1;  // measured: C3 R=2 0.796 vs 0.636 ms, C5 R=4 -3.5%
 static const long kChunkWaves = 65536;
 
 enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
@@ -619,6 +621,14 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     return RT0_OK;
   }
   dim3 grid((p.vp_x1 - p.vp_x0 + 15) / 16, (p.vp_y1 - p.vp_y0 + 15) / 16);
+  // ReSTIR passes refill finished lanes from a per-wave pixel pool (pass_body):
+  // a workgroup then covers 16 x 16*refill launch rows
+  p.refill = 1;
+  if (restir && !c->counting) {
+    static const int refill = getenv("RT0_REFILL") ? std::max(1, atoi(getenv("RT0_REFILL"))) : kRestirRefill;
+    p.refill = refill;
+    grid.y = (p.vp_y1 - p.vp_y0 + 16 * refill - 1) / (16 * refill);
+  }
   // scene-specialised kernel (compiled once per scene/config, cached); the
   // counting instance is always the ahead-of-time one
   void *jit_fn = nullptr;

@@ -1994,9 +1994,77 @@ DEV size_t sample_index(const LaunchParams &P, int px, int r) {
 
 // The pass kernel body: 16x16 pixel tile per 256-thread workgroup (four 8x8
 // wave tiles); each lane accumulates its pixel's passes in registers.
+// ReSTIR pass with lane refill: the wave owns 64*P.refill pixels -- P.refill
+// 8x8 blocks stacked in y -- and a lane whose path has ended writes its pixel
+// (accumulator + reservoir MRTs) and takes the pool's next pixel, so lanes
+// whose ray left for the sky do not idle while their neighbours bounce.  The
+// pixels of one pass are independent (they read only the previous passes'
+// reservoirs), so the result is the same as one pixel per lane.
+template <class It, class Scene, class Cfg>
+DEV void restir_refill_body(const LaunchParams &P, It &it, const Scene &sc, const Cfg &cfg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int R = P.refill, pool = 64 * R;
+  const int x0 = P.vp_x0 + blockIdx.x * 16 + ((wave & 1) << 3);
+  const int r0 = P.vp_y0 + blockIdx.y * 16 * R + (wave >> 1) * 8 * R;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  typename It::Path ps;
+  int pi = lane, next = 64;
+  bool have = true, alive = false, valid = false;
+  int px = 0, py = 0;
+  auto start = [&]() {
+    px = x0 + (pi & 7);
+    const int r = r0 + ((pi >> 6) << 3) + ((pi >> 3) & 7);
+    py = (px < P.vp_x1 && r < P.vp_y1) ? image_row(P, r) : P.height;
+    valid = py < P.height;
+    alive = false;
+    if (valid) {
+      it.frame = P.frame0;
+      it.begin(ps, px, py);
+      alive = cfg.max_bounces() > 0;
+    }
+  };
+  start();
+  while (true) {
+    if (alive) alive = it.step(ps);
+    const bool done = have && !alive;
+    if (done && valid) {
+      const size_t pix = (size_t)py * P.width + px;
+      float4 a = P.accum[pix];
+      accumulate(it, P, a, it.finish(ps));
+      P.accum[pix] = a;
+      if (P.rout_main != nullptr && P.rout_aux != nullptr) {
+        if (it.flag(F_RESTIR_DEF)) {
+          const Res &q = it.fin;
+          P.rout_main[pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
+          P.rout_aux[pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+        } else {
+          P.rout_main[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+          P.rout_aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      valid = false;
+    }
+    const unsigned long long fin = __ballot(done);
+    if (done) {
+      pi = next + __popcll(fin & below);
+      if (pi < pool) start();
+      else have = false;
+    }
+    next += __popcll(fin);
+    if (__ballot(have) == 0ull) break;
+  }
+}
+
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   if constexpr (Scene::kStatic) Scene::stage();  // LDS copy of the scene records (before any early exit)
+  if constexpr (RESTIR && !COUNT) {
+    if (P.refill > 1) {
+      Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT> it(P, sc, cfg);
+      restir_refill_body(P, it, sc, cfg);
+      return;
+    }
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
   const int ly = (lane >> 3) + ((wave >> 1) << 3);
