@@ -1994,6 +1994,41 @@ DEV size_t sample_index(const LaunchParams &P, int px, int r) {
 
 // The pass kernel body: 16x16 pixel tile per 256-thread workgroup (four 8x8
 // wave tiles); each lane accumulates its pixel's passes in registers.
+// XCD-aware tile order.  Workgroups are dealt round-robin over the 8 XCDs
+// (blocks b and b+8 share one, MI355X_MICROARCH.md "Workgroup dispatch"),
+// and each XCD has its own 4 MiB L2: mapping the blocks of one XCD onto one
+// contiguous run of tiles (row-major) keeps the spatial/temporal reservoir
+// taps and the BVH nodes of neighbouring tiles in the same L2.  A bijection
+// on the grid's (x, y) blocks, so it changes no result.
+//   RT0_XCD_REMAP 1: one contiguous run per XCD (whole bands of the image);
+//   RT0_XCD_REMAP c > 1: runs of c consecutive tiles per XCD, interleaved
+//   (8c tiles per round), keeping the work of the XCDs balanced.
+#ifndef RT0_XCD_REMAP
+#define RT0_XCD_REMAP 0
+#endif
+DEV void block_tile(int &bx, int &by) {
+#if RT0_XCD_REMAP == 1
+  const int gx = (int)gridDim.x, n = (int)(gridDim.x * gridDim.y);
+  const int L = (int)blockIdx.x + (int)blockIdx.y * gx;
+  const int q = n >> 3, rem = n & 7, k = L & 7, j = L >> 3;
+  const int t = k * q + min(k, rem) + j;
+  bx = t % gx;
+  by = t / gx;
+#elif RT0_XCD_REMAP > 1
+  const int gx = (int)gridDim.x, n = (int)(gridDim.x * gridDim.y);
+  const int L = (int)blockIdx.x + (int)blockIdx.y * gx;
+  constexpr int c = RT0_XCD_REMAP;
+  const int base = (L / (8 * c)) * (8 * c);
+  int t = base + (L & 7) * c + ((L >> 3) % c);
+  if (base + 8 * c > n) t = L;  // ragged last round: identity
+  bx = t % gx;
+  by = t / gx;
+#else
+  bx = (int)blockIdx.x;
+  by = (int)blockIdx.y;
+#endif
+}
+
 // ReSTIR pass with lane refill: the wave owns 64*P.refill pixels -- P.refill
 // 8x8 blocks stacked in y -- and a lane whose path has ended writes its pixel
 // (accumulator + reservoir MRTs) and takes the pool's next pixel, so lanes
@@ -2004,8 +2039,10 @@ template <class It, class Scene, class Cfg>
 DEV void restir_refill_body(const LaunchParams &P, It &it, const Scene &sc, const Cfg &cfg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int R = P.refill, pool = 64 * R;
-  const int x0 = P.vp_x0 + blockIdx.x * 16 + ((wave & 1) << 3);
-  const int r0 = P.vp_y0 + blockIdx.y * 16 * R + (wave >> 1) * 8 * R;
+  int bx, by;
+  block_tile(bx, by);
+  const int x0 = P.vp_x0 + bx * 16 + ((wave & 1) << 3);
+  const int r0 = P.vp_y0 + by * 16 * R + (wave >> 1) * 8 * R;
   const unsigned long long below = (1ull << lane) - 1ull;
   typename It::Path ps;
   int pi = lane, next = 64;
@@ -2068,8 +2105,10 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
   const int ly = (lane >> 3) + ((wave >> 1) << 3);
-  const int px = P.vp_x0 + blockIdx.x * 16 + lx;
-  const int r = P.vp_y0 + blockIdx.y * 16 + ly;
+  int bx, by;
+  block_tile(bx, by);
+  const int px = P.vp_x0 + bx * 16 + lx;
+  const int r = P.vp_y0 + by * 16 + ly;
   if (px >= P.vp_x1 || r >= P.vp_y1) return;
   const int py = image_row(P, r);
   if (py >= P.height) return;
