@@ -10,10 +10,12 @@
 // It follows shaders/pathtracing/raytracer.glsl (line numbers cited per
 // function) in fp32: every operation is rounded with Math.fround, and the RNG
 // reproduces the reference executor's uint->float conversion, so frame k of a
-// pixel draws the same random numbers as the reference.  Scope: the quadric
-// scenes of the C1/C2 configs -- planes, spheres, boxes, every material, sky,
-// plain NEE and MIS.  SDF, volumetrics, spectral and ReSTIR configs are
-// rejected (the C oracle covers them).
+// pixel draws the same random numbers as the reference.  Scope: the C1/C2/C4
+// configs -- planes, spheres, boxes, SDFs (every #sdf_meshes kind, sphere-traced
+// with calcNormal), every untextured material, sky, plain NEE, MIS, SDF lights,
+// homogeneous volumetrics (free-flight sampling, in-scatter NEE, HG phase, fog
+// transmittance).  Spectral, ReSTIR, cubemap and texture configs are rejected
+// (the C oracle covers them).
 const f = Math.fround;
 
 // ------------------------------------------------------------------ RNG
@@ -76,8 +78,74 @@ const fsin = (x) => f(Math.sin(x)), fcos = (x) => f(Math.cos(x));
 const EPS = f(0.001), INF_T = f(1e4), TWO_PI = f(6.28318531), ONE_OVER_PI = f(0.31830989), FOUR_PI = f(12.5663706);
 const RAD = f(0.01745329);
 
+const PI_F = f(3.14159265), VOL_SIGMA_T = f(0.15), VOL_SIGMA_S = f(0.13), VOL_G = f(0.5);
+
+// ------------------------------------------------ SDF primitives (496-576, 642-698)
+function sdBox(p, b) {
+  const d = sub(vabs(p), b);
+  return f(length(V(gmax(d.x, 0), gmax(d.y, 0), gmax(d.z, 0))) + gmin(gmax(d.x, gmax(d.y, d.z)), 0));
+}
+function sdCone(p, c) {
+  const qx = f(Math.sqrt(f(f(p.x * p.x) + f(p.z * p.z)))), qy = p.y;
+  const d1 = f(-qy - c.z), d2 = gmax(f(f(qx * c.x) + f(qy * c.y)), qy);
+  const a = gmax(d1, 0), b = gmax(d2, 0);
+  return f(f(Math.sqrt(f(f(a * a) + f(b * b)))) + gmin(gmax(d1, d2), 0));
+}
+function gmod(x, y) { return f(x - f(y * Math.floor(f(x / y)))); }
+function menger(p, scale) {
+  let d = sdBox(p, scale), s = 1;
+  for (let m = 0; m < 4; m++) {
+    const ps = muls(p, s);
+    const a = V(f(gmod(ps.x, 2) - 1), f(gmod(ps.y, 2) - 1), f(gmod(ps.z, 2) - 1));
+    s = f(s * 3);
+    const r = V(Math.abs(f(1 - f(3 * Math.abs(a.x)))), Math.abs(f(1 - f(3 * Math.abs(a.y)))), Math.abs(f(1 - f(3 * Math.abs(a.z)))));
+    const da = gmax(r.x, r.y), db = gmax(r.y, r.z), dc = gmax(r.z, r.x);
+    d = gmax(f(f(gmin(da, gmin(db, dc)) - 1) / s), d);
+  }
+  return d;
+}
+function mul5(a, b, c, d, e) { return f(f(f(f(a * b) * c) * d) * e); }
+function mandelbulb(p) {
+  let w = p, m = dot(w, w), dz = 1;
+  for (let i = 0; i < 3; i++) {
+    const m2 = f(m * m), m4 = f(m2 * m2);
+    dz = f(f(f(8 * f(Math.sqrt(f(f(m4 * m2) * m)))) * dz) + 1);
+    const x = w.x, x2 = f(x * x), x4 = f(x2 * x2);
+    const y = w.y, y2 = f(y * y), y4 = f(y2 * y2);
+    const z = w.z, z2 = f(z * z), z4 = f(z2 * z2);
+    const k3 = f(x2 + z2);
+    const k2 = isqrt(f(f(f(mul5(k3, k3, k3, k3, k3) * k3) * k3)));
+    const k1 = f(f(f(f(f(x4 + y4) + z4) - f(f(6 * y2) * z2)) - f(f(6 * x2) * y2)) + f(f(2 * z2) * x2));
+    const k4 = f(f(x2 - y2) + z2);
+    const pxz = f(f(x4 - f(f(6 * x2) * z2)) + z4);
+    const wx = f(p.x + f(f(f(f(mul5(64, x, y, z, f(x2 - z2)) * k4) * pxz) * k1) * k2));
+    const wy = f(f(p.y + mul5(-16, y2, k3, k4, k4)) + f(k1 * k1));
+    const poly = f(f(f(f(f(x4 * x4) - f(f(f(28 * x4) * x2) * z2)) + f(f(70 * x4) * z4)) - f(f(f(28 * x2) * z2) * z4)) + f(z4 * z4));
+    const wz = f(p.z + f(f(f(f(f(f(-8 * y) * k4) * poly) * k1) * k2)));
+    w = V(wx, wy, wz);
+    m = dot(w, w);
+    if (m > 4) break;
+  }
+  return f(f(f(f(0.25 * f(Math.log(m))) * f(Math.sqrt(m)))) / dz);
+}
+// randomSphereDirection (1143-1147), sampleHG (1157-1171)
+function randomSphereDirection(seed) {
+  const r = hash2(seed, seed), rx = f(r[0] * TWO_PI), ry = f(r[1] * TWO_PI);
+  const sy = fsin(ry), cy = fcos(ry);
+  return V(f(fsin(rx) * sy), f(fsin(rx) * cy), fcos(rx));
+}
+function sampleHG(w, seed) {
+  const uv = hash2(seed, f(seed + f(1.789))), g = VOL_G;
+  const sqr = f(f(1 - f(g * g)) / f(f(1 - g) + f(f(2 * g) * uv[0])));
+  const cosT = f(f(f(1 + f(g * g)) - f(sqr * sqr)) / f(2 * g));
+  const sinT = f(Math.sqrt(gmax(0, f(1 - f(cosT * cosT)))));
+  const phi = f(TWO_PI * uv[1]);
+  const [t, b] = CpuRenderer.binormals(w);
+  return normalize(add(add(muls(t, f(fcos(phi) * sinT)), muls(b, f(fsin(phi) * sinT))), muls(w, cosT)));
+}
+
 // ------------------------------------------------------- scene grammar
-const T_SPHERE = 0, T_PLANE = 1, T_BOX = 2;
+const T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_SDF = 3;
 const M_LIGHT = 0, M_DIR_LIGHT = 1, M_DIFF = 2, M_SPEC = 3, M_REFR_FRESNEL = 4, M_REFR_SCHLICK = 5, M_COAT = 6;
 // Material table, raytracer.glsl:165-224 ([c, e, nt, type]; textured ones omitted)
 const MATS = {
@@ -107,7 +175,7 @@ const MATS = {
   MAT_COAT_PURPLE: [[0.50196078431, 0, 0.50196078431], [0, 0, 0], 1.4, M_COAT],
   MAT_COAT_WAX: [[0.9333, 0.6666, 0.6], [0.005, 0.005, 0.005], 1.4, M_COAT],
 };
-const TYPES = { SPHERE: T_SPHERE, PLANE: T_PLANE, BOX: T_BOX };
+const TYPES = { SPHERE: T_SPHERE, PLANE: T_PLANE, BOX: T_BOX, SDF: T_SDF };
 
 // parse "vecN(a, b, ...)" with GLSL scalar broadcast
 function parseVec(s, n) {
@@ -135,7 +203,13 @@ function parseScene(lines) {
     });
   });
   if (lights.length === 0) lights.push(-1);
-  return { meshes, lights };
+  // meshes[NUM_MESHES + i] addresses SDF i: the SDF lines follow the quadrics
+  let nMeshes = meshes.length;
+  meshes.forEach((m, i) => {
+    if (m.t === T_SDF && nMeshes === meshes.length) nMeshes = i;
+    else if (m.t !== T_SDF && nMeshes < meshes.length) throw new Error('SDF meshes must follow the quadrics');
+  });
+  return { meshes, lights, nMeshes };
 }
 
 // ---------------------------------------------------------- renderer
@@ -143,11 +217,11 @@ class CpuRenderer {
   // cfg: a tests/golden/configs.json entry; cornell: cfgs.cornell_lines; camera default
   constructor(cfg, cornellLines, defaultCamera, width, height) {
     const defs = Object.assign({ USE_PROCEDURAL_SKY: true, USE_BIASED_SAMPLING: true }, cfg.defines || {});
-    for (const k of ['USE_RESTIR', 'USE_SPECTRAL', 'USE_VOLUMETRICS', 'USE_CUBEMAP'])
+    for (const k of ['USE_RESTIR', 'USE_SPECTRAL', 'USE_CUBEMAP'])
       if (defs[k]) throw new Error(k + ' is outside the JS baseline');
     const c = Object.assign({
       MAX_BOUNCES: 12, MAX_DIFF_BOUNCES: 4, MAX_SPEC_BOUNCES: 4, MAX_TRANS_BOUNCES: 12, MAX_SCATTERING_EVENTS: 12,
-      sample_lights: true, use_mis: false, use_restir: false,
+      sample_lights: true, use_mis: false, use_restir: false, MARCHING_STEPS: 128, FUDGE_FACTOR: 0.9,
     }, cfg.constants || {});
     if (c.use_restir) throw new Error('use_restir is outside the JS baseline');
     this.sky = !!defs.USE_PROCEDURAL_SKY;
@@ -157,12 +231,55 @@ class CpuRenderer {
     this.sampleLights = !!c.sample_lights; this.mis = !!c.use_mis;
     const sc = parseScene(cfg.scene_lines || cornellLines);
     this.meshes = sc.meshes; this.lights = sc.lights;
+    this.nMeshes = sc.nMeshes; this.nSdf = sc.meshes.length - sc.nMeshes;
+    this.sdfKinds = Array.from({ length: this.nSdf }, (_, i) => ((cfg.sdf_kinds || [])[i] || 0));
+    this.vol = !!defs.USE_VOLUMETRICS;
+    this.marchSteps = c.MARCHING_STEPS; this.fudge = f(c.FUDGE_FACTOR);
     this.w = width; this.h = height;
     const cam = cfg.camera || defaultCamera;
     this.camPos = V(f(cam.origin[0]), f(cam.origin[1]), f(cam.origin[2]));
     this.camLook = V(f(cam.lookat[0]), f(cam.lookat[1]), f(cam.lookat[2]));
     this.camParams = V(f(cam.fov), f(cam.aperture), f(cam.focalLength));
     this.nIsect = 0;
+    this.nMap = 0;
+  }
+
+  // map(), raytracer.glsl:700-712 (+ the #sdf_meshes statements, index.html:702-717) -> [d, id]
+  map(p) {
+    this.nMap++;
+    let rx = 0, ry = 0;
+    for (let i = 0; i < this.nSdf; i++) {
+      const m = this.meshes[this.nMeshes + i];
+      const q = sub(p, m.pos), j = V(m.joker[0], m.joker[1], m.joker[2]);
+      let d;
+      switch (this.sdfKinds[i]) {
+        case 0: d = sdBox(q, j); break;
+        case 1: { const dd = sub(vabs(q), j); d = f(length(V(gmax(dd.x, 0), gmax(dd.y, 0), gmax(dd.z, 0))) - m.joker[3]); break; }
+        case 2: d = f(length(q) - m.joker[0]); break;
+        case 3: {
+          const qa = vabs(q);
+          d = gmax(f(qa.z - m.joker[1]), f(gmax(f(f(qa.x * f(0.866025)) + f(q.y * 0.5)), -q.y) - f(m.joker[0] * 0.5)));
+          break;
+        }
+        case 4: d = sdCone(q, j); break;
+        case 5: d = menger(q, j); break;
+        default: d = mandelbulb(q); break;
+      }
+      if (i === 0) { rx = d; ry = 0; } else {
+        const a = rx < d ? 1 : 0;
+        rx = mixf(d, rx, a); ry = mixf(f(i), ry, a);
+      }
+    }
+    return [rx, ry];
+  }
+  // 714-722
+  calcNormal(p) {
+    const E = EPS;
+    const a = muls(V(1, -1, -1), this.map(add(p, V(E, -E, -E)))[0]);
+    const b = muls(V(-1, -1, 1), this.map(add(p, V(-E, -E, E)))[0]);
+    const c = muls(V(-1, 1, -1), this.map(add(p, V(-E, E, -E)))[0]);
+    const d = muls(V(1, 1, 1), this.map(add(p, V(E, E, E)))[0]);
+    return normalize(add(add(add(a, b), c), d));
   }
 
   // intersection(), raytracer.glsl:997-1082 -> {t, n, pos, index}
@@ -170,7 +287,7 @@ class CpuRenderer {
     this.nIsect++;
     let tmin = INF_T, type = -1, index = 0, n = V(0, 0, 0);
     const ms = this.meshes;
-    for (let i = 0; i < ms.length; i++) {
+    for (let i = 0; i < this.nMeshes; i++) {
       const m = ms[i];
       if (m.joker[0] === 0) continue;
       if (m.t === T_SPHERE) {  // 818-833
@@ -202,6 +319,20 @@ class CpuRenderer {
           step(dd.x, dd.z) * step(dd.y, dd.z));
         n = normalize(mul(s, st));
         tmin = t; type = T_BOX; index = i;
+      }
+    }
+    if (this.nSdf > 0) {  // iSDF, 974-993
+      let t = f(EPS * 4), res = [0, 0];
+      for (let i = 0; i < this.marchSteps; i++) {
+        res = this.map(add(o, muls(d, t)));
+        const h = Math.abs(res[0]);
+        if (h < EPS || t > tmin) break;
+        t = f(t + f(h * this.fudge));
+      }
+      if (!(t > tmin)) {
+        n = this.calcNormal(add(o, muls(d, t)));
+        index = this.nMeshes + Math.trunc(res[1]);
+        tmin = t; type = T_SDF;
       }
     }
     let pos = V(0, 0, 0);
@@ -241,6 +372,14 @@ class CpuRenderer {
   directLight(li, x, nl, seed) {
     const L = this.meshes[li];
     if (L.mt === M_LIGHT) {
+      if (L.t === T_SDF) {  // 1205-1216
+        const ld = add(L.pos, mul(randomSphereDirection(f(seed + f(78.2358))), V(L.joker[0], L.joker[1], L.joker[2])));
+        const sr = normalize(sub(ld, x));
+        const hit = this.intersect(add(x, muls(nl, EPS)), sr);
+        const mh = this.meshes[hit.index];
+        if (mh.mt !== M_LIGHT) return V(0, 0, 0);
+        return muls(mul(vmaxs(mh.c, f(0.001)), mh.e), gmax(f(0.001), dot(sr, nl)));
+      }
       if (L.t !== T_SPHERE) return V(0, 0, 0);
       const sw = sub(L.pos, x);
       const r2 = f(L.joker[0] * L.joker[0]), d2 = dot(sw, sw);
@@ -250,7 +389,8 @@ class CpuRenderer {
       const mh = this.meshes[hit.index];
       if (mh.mt !== M_LIGHT) return V(0, 0, 0);
       const weight = f(2 * f(1 - cosA));
-      return muls(muls(mul(vmaxs(mh.c, f(0.001)), mh.e), weight), gmax(f(0.001), dot(sr, nl)));
+      const fog = this.vol ? f(Math.exp(f(-VOL_SIGMA_T * hit.t))) : 1;
+      return muls(muls(muls(mul(vmaxs(mh.c, f(0.001)), mh.e), weight), gmax(f(0.001), dot(sr, nl))), fog);
     }
     if (L.mt === M_DIR_LIGHT) {
       const hit = this.intersect(add(x, muls(nl, EPS)), L.pos);
@@ -286,6 +426,37 @@ class CpuRenderer {
     const fr = f(frame);
     for (let depth = 0; depth < this.maxB; depth++) {
       const hit = this.intersect(ro, rd);
+      if (this.vol) {
+        const sd = f(f(-f(Math.log(gmax(hash(f(f(seed + f(4729.3)) + f(f(depth) * f(991.1)))), f(1e-6))))) / VOL_SIGMA_T);
+        if (sd < gmin(INF_T, hit.t)) {
+          const sp = add(ro, muls(rd, sd));
+          mask = muls(mask, f(VOL_SIGMA_S / VOL_SIGMA_T));
+          if (this.sampleLights) {
+            for (let li = 0; li < this.lights.length; li++) {
+              const lidx = this.lights[li];
+              if (lidx < 0) continue;
+              const L = this.meshes[lidx];
+              if (L.mt !== M_LIGHT || L.t !== T_SPHERE) continue;
+              const dlc = sub(L.pos, sp), dc = length(dlc);
+              const r2 = f(L.joker[0] * L.joker[0]);
+              const cam = f(Math.sqrt(f(1 - clamp(f(r2 / f(dc * dc)), 0, 1))));
+              const s2 = f(f(f(seed + f(2341.7)) + f(f(li) * f(917.3))) + f(f(depth) * f(199.1)));
+              const dir = CpuRenderer.coneSample(V(f(dlc.x / dc), f(dlc.y / dc), f(dlc.z / dc)), f(1 - cam), s2);
+              const sh = this.intersect(add(sp, muls(dir, f(EPS * 20))), dir);
+              if (sh.index !== lidx) continue;
+              const omega = f(2 * f(1 - cam)), ct = dot(rd, dir);
+              const g2 = f(VOL_G * VOL_G), den = f(f(1 + g2) - f(f(2 * VOL_G) * ct));
+              const phase = f(f(1 - g2) / f(f(FOUR_PI * den) * f(Math.sqrt(den))));
+              const Tf = f(Math.exp(f(-VOL_SIGMA_T * sh.t)));
+              acc = add(acc, muls(muls(muls(mul(mul(mask, L.c), L.e), phase), Tf), f(PI_F * omega)));
+            }
+          }
+          rd = sampleHG(rd, f(f(seed + f(8293.7)) + f(f(depth) * f(773.3))));
+          ro = sp; spec = false; scat++;
+          if (scat >= this.maxSc || vmaxc(mask) < f(0.01)) break;
+          continue;
+        }
+      }
       if (hit.t === INF_T) {
         if (!spec && this.sampleLights) break;
         if (this.sky) {

@@ -1,7 +1,7 @@
 """The JS CPU integrator (oracle/js/rt0_cpu.js) -- the reported CPU baseline
 of bench.py, SURVEY 8d -- renders what the reference renders: checked against
 the golden fixtures (the reference shader under SwiftShader) and the C oracle
-on the quadric configs it covers.  CPU only."""
+on the configs it covers (quadrics, SDFs, volumetrics).  CPU only."""
 import json
 import os
 import shutil
@@ -32,13 +32,14 @@ def match(a, b):
 
 
 @pytest.mark.parametrize("name", ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
-                                  "thinlens_glass"])
+                                  "thinlens_glass", "menger_coat", "sdf_cone", "sdf_triprism", "mis_demo_sdfbox"])
 def test_js_integrator_matches_reference_fixtures(name, cfgs, tmp_path):
     gold = np.load(os.path.join(REPO, "tests", "golden", name + ".npz"))["samples"]
     F, H, W = gold.shape[:3]
     for k in (1, F):
         got = js_image(name, W, H, k, 1, tmp_path)
-        assert match(got, gold[k - 1]) >= 0.99, (name, k)
+        # SDF scenes: every path grazes many edges (the oracle's own allowance, test_oracle_golden.BAD_FRAC)
+        assert match(got, gold[k - 1]) >= (0.98 if name == "menger_coat" else 0.99), (name, k)
 
 
 def test_js_integrator_matches_c_oracle_accumulated(cfgs, tmp_path):
@@ -48,6 +49,18 @@ def test_js_integrator_matches_c_oracle_accumulated(cfgs, tmp_path):
     got = js_image("c2_cornell_mis_8", 48, 40, 1, 3, tmp_path)
     assert match(got, ref) >= 0.99
     assert abs(got[..., :3].mean() - ref[..., :3].mean()) <= 1e-3 * ref[..., :3].mean()
+
+
+@pytest.mark.parametrize("name", ["c4_mandelbulb_vol", "vol_cornell_2"])
+def test_js_integrator_matches_c_oracle_sdf_volumetrics(name, cfgs, tmp_path):
+    """C4's feature set (Mandelbulb SDF, homogeneous medium, in-scatter NEE):
+    the JS baseline against the C restatement, single-sample frames."""
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    o = O.Oracle(cfg, cfgs, width=24, height=24)
+    for k in (1, 2):
+        ref = o.frame(k)[0]
+        got = js_image(name, 24, 24, k, 1, tmp_path)
+        assert match(got, ref) >= 0.99, (name, k)
 
 
 def test_js_bench_mode_reports_throughput():
