@@ -283,7 +283,7 @@ static void dump(const char *prefix, int frame, const char *tag, int w, int h,
 
 int main(int argc, char **argv) {
   const char *frag = NULL, *prefix = "out";
-  int w = 64, h = 64, frames = 4, single = 0, restir_out = 0;
+  int w = 64, h = 64, frames = 4, frame0 = 1, single = 0, restir_out = 0;
   float cam[9] = {0, 0, 2.8f, 0, 0, -1, 50, 0, 3.5f};
   float time_ms = 0.0f;
   float dtime_ms = 0.0f;
@@ -298,6 +298,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "--w")) w = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--h")) h = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--frames")) frames = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--frame0")) frame0 = atoi(argv[++i]); /* u_frame of the first pass */
     else if (!strcmp(argv[i], "--single")) single = 1;
     else if (!strcmp(argv[i], "--restir-out")) restir_out = 1;
     else if (!strcmp(argv[i], "--time")) time_ms = (float)atof(argv[++i]);
@@ -404,7 +405,7 @@ int main(int argc, char **argv) {
 
   for (int pass = 1; pass <= frames; pass++) {
     p_glUseProgram(prog);
-    if (frame_loc >= 0) p_glUniform1ui(frame_loc, (GLuint)pass);
+    if (frame_loc >= 0) p_glUniform1ui(frame_loc, (GLuint)(frame0 + pass - 1));
     if (time_loc >= 0) p_glUniform1f(time_loc, time_ms + (float)(pass - 1) * dtime_ms);
     if (tf_loc >= 0) p_glUniform1i(tf_loc, temporal_frames);
     p_glActiveTexture(GL_TEXTURE0 + 0);
@@ -432,10 +433,10 @@ int main(int argc, char **argv) {
     if (p_glGetError() != 0) die("GL error after draw");
     fprintf(stderr, "glrun: pass %d done at %.1f s after link\n", pass, now_s() - t0);
 
-    dump(prefix, pass, "c", w, h, fb, 0);
+    dump(prefix, frame0 + pass - 1, "c", w, h, fb, 0);
     if (restir_out) {
-      dump(prefix, pass, "r", w, h, fb, 1);
-      dump(prefix, pass, "a", w, h, fb, 2);
+      dump(prefix, frame0 + pass - 1, "r", w, h, fb, 1);
+      dump(prefix, frame0 + pass - 1, "a", w, h, fb, 2);
     }
 
     /* swapReSTIRBuffers (index.js:795-820) */

@@ -25,7 +25,10 @@
  *      mix quadrics with SDFs black.  `inout` pins the undefined value to "the
  *      caller's value unchanged", the only reading under which the reference
  *      renders its own scenes (DESIGN.md 2).
- *   3. with --nanfix only: powerHeuristic's `max(0.0, (f*f)/denom)` becomes
+ *   3. the volumetric in-scatter light loop's `if (c) continue;` statements are
+ *      rewritten as the equivalent `if (!(c)) { ... }` (SwiftShader 4.1 does not
+ *      finish the loop as written; see the edit below).  GLSL semantics unchanged.
+ *   4. with --nanfix only: powerHeuristic's `max(0.0, (f*f)/denom)` becomes
  *      `denom > 0.0 ? (f*f)/denom : 0.0`, i.e. IEEE-maxNum semantics for the 0/0
  *      case (raytracer.glsl:1233-1238).  Every non-NaN pixel is unchanged.
  *      No committed fixture uses it (manifest.json: unpatched powerHeuristic).
@@ -184,7 +187,7 @@ function main() {
   const n1 = src.split('const Mesh meshes[').length - 1;
   if (n1 !== 1) throw new Error('expected exactly one `const Mesh meshes[`, found ' + n1);
   src = src.replace('const Mesh meshes[', 'Mesh meshes[');
-  // 3. iBox / iSDF leave their `out` normal (and iSDF its `out` index) unassigned
+  // 2. iBox / iSDF leave their `out` normal (and iSDF its `out` index) unassigned
   //    on a miss (raytracer.glsl:836-859, 974-993).  GLSL makes such values
   //    undefined; SwiftShader copies out a stale register, which after the first
   //    SDF hit turns every later SDF miss into hit.index = NUM_MESHES (black
@@ -201,6 +204,27 @@ function main() {
   for (const [from, to] of patches) {
     if (src.split(from).length !== 2) throw new Error('patch target not found: ' + from);
     src = src.replace(from, to);
+  }
+  // 3. the in-scatter light loop of the volumetric branch (raytracer.glsl:
+  //    2011-2044) skips lights with `if (...) continue;` three times.  SwiftShader
+  //    4.1 does not finish that loop: an 8x8 render with it ran > 20 min (killed),
+  //    the same shader with each `if (c) continue; rest` written as the
+  //    equivalent `if (!(c)) { rest }` renders in 1.9 s, as does one without the
+  //    loop.  GLSL semantics are unchanged; USE_VOLUMETRICS scenes only (the block
+  //    is preprocessed out everywhere else).
+  {
+    const head = 'for (int li = 0; li < num_lights; ++li) {';
+    const tail = 'acc += mask * lm.mat.c * lm.mat.e * phase * T_fog * (PI * omega);';
+    if (src.split(head).length !== 2 || src.split(tail).length !== 2) throw new Error('volumetric light loop not found');
+    const i = src.indexOf(head), j = src.indexOf(tail, i) + tail.length;
+    let body = src.slice(i, j), n = 0;
+    for (const cond of ['light_idx < 0', 'lm.mat.t != LIGHT || lm.t != SPHERE', 'sh.index != light_idx']) {
+      const from = 'if (' + cond + ') continue;';
+      if (body.split(from).length !== 2) throw new Error('volumetric loop pattern not found: ' + from);
+      body = body.replace(from, 'if (!(' + cond + ')) {');
+      n++;
+    }
+    src = src.slice(0, i) + body + ' ' + '}'.repeat(n) + src.slice(j);
   }
   if (nanfix) {
     const needle = 'return max(0.0, (f * f) / denom);';

@@ -643,10 +643,9 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     }
     jit_fn = c->jit_fn;
   }
-  auto launch = [&](const LaunchParams &lp, unsigned gz) -> hipError_t {
-    if (jit_fn)
-      return rt0h::jit_launch(jit_fn, &lp, grid.x, grid.y, gz, c->stream) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
-    return rt0_launch_pass(variant, &lp, dim3(grid.x, grid.y, gz), c->stream);
+  auto launch = [&](const LaunchParams &lp, unsigned gz, dim3 g) -> hipError_t {
+    if (jit_fn) return rt0h::jit_launch(jit_fn, &lp, g.x, g.y, gz, c->stream) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
+    return rt0_launch_pass(variant, &lp, dim3(g.x, g.y, gz), c->stream);
   };
   if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, RT0_N_COUNTERS * sizeof(unsigned long long), c->stream));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
@@ -663,7 +662,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       p.rin[5] = c->d_restir[R_H2A];
       p.rout_main = c->d_restir[R_OUT_MAIN];
       p.rout_aux = c->d_restir[R_OUT_AUX];
-      HIPCHK(c, launch(p, 1));
+      HIPCHK(c, launch(p, 1, grid));
       launches++;
       // swapReSTIRBuffers, index.js:795-820
       float4 **R = c->d_restir;
@@ -712,13 +711,13 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
           c->samples_bytes = need;
         }
         p.samples = c->d_samples;
-        HIPCHK(c, launch(p, (unsigned)chunks));
+        HIPCHK(c, launch(p, (unsigned)chunks, grid));
         HIPCHK(c, rt0_launch_sum(&p, grid, c->stream));
         launches += 2;
       } else {
         p.frame_chunk = p.nframes;
         p.samples = nullptr;
-        HIPCHK(c, launch(p, 1));
+        HIPCHK(c, launch(p, 1, grid));
         launches++;
       }
     }

@@ -79,8 +79,18 @@ DEV float flog(float x) { return __logf(x); }
 // -ffp-contract=fast, or with the ROCm 7.0 hipRTC that PyTorch bundles (and
 // that a process importing torch binds to), the backend fuses across it.  An
 // empty asm on the product makes it opaque, so no compiler can fuse it.
+// RT0_OPQ 1 additionally hides every product from the compiler (empty asm).
+// Off by default: under -ffp-contract=fast-honor-pragmas with the pinned
+// hipRTC the contract(off) pragmas alone keep the products unfused (every GPU
+// parity test is green either way), and the asm costs a v_mov + s_nop each:
+// 5.66 vs 5.80 ms per 64-spp C2 launch (profiles/r02/ab_c2knobs).
+#ifndef RT0_OPQ
+#define RT0_OPQ 0
+#endif
 DEV float opq(float x) {
+#if RT0_OPQ
   asm("" : "+v"(x));
+#endif
   return x;
 }
 DEV float nc_fract(float x) {
@@ -220,6 +230,7 @@ struct Hit {
 #ifndef RT0_MARCH_BUDGET
 #define RT0_MARCH_BUDGET 8
 #endif
+
 struct March {
   v3 o, d;
   float tmin, t, id;
@@ -262,7 +273,7 @@ DEV float mandelbulb(v3 p) {
   float dz = 1.0f;
   for (int i = 0; i < 3; ++i) {
     float m2 = m * m, m4 = m2 * m2;
-    dz = 8.0f * fsqrt(m4 * m2 * m) * dz + 1.0f;
+    const float dzn = 8.0f * fsqrt(m4 * m2 * m) * dz + 1.0f;
     float x = w.x, x2 = x * x, x4 = x2 * x2;
     float y = w.y, y2 = y * y, y4 = y2 * y2;
     float z = w.z, z2 = z * z, z4 = z2 * z2;
@@ -270,11 +281,15 @@ DEV float mandelbulb(v3 p) {
     float k2 = frsq(k3 * k3 * k3 * k3 * k3 * k3 * k3);
     float k1 = x4 + y4 + z4 - 6.0f * y2 * z2 - 6.0f * x2 * y2 + 2.0f * z2 * x2;
     float k4 = x2 - y2 + z2;
-    w.x = p.x + 64.0f * x * y * z * (x2 - z2) * k4 * (x4 - 6.0f * x2 * z2 + z4) * k1 * k2;
-    w.y = p.y + -16.0f * y2 * k3 * k4 * k4 + k1 * k1;
-    w.z = p.z + -8.0f * y * k4 * (x4 * x4 - 28.0f * x4 * x2 * z2 + 70.0f * x4 * z4 - 28.0f * x2 * z2 * z4 + z4 * z4) * k1 * k2;
-    m = dot(w, w);
-    if (m > 4.0f) break;
+    v3 wn;
+    wn.x = p.x + 64.0f * x * y * z * (x2 - z2) * k4 * (x4 - 6.0f * x2 * z2 + z4) * k1 * k2;
+    wn.y = p.y + -16.0f * y2 * k3 * k4 * k4 + k1 * k1;
+    wn.z = p.z + -8.0f * y * k4 * (x4 * x4 - 28.0f * x4 * x2 * z2 + 70.0f * x4 * z4 - 28.0f * x2 * z2 * z4 + z4 * z4) * k1 * k2;
+    const float mn = dot(wn, wn);
+    dz = dzn;
+    w = wn;
+    m = mn;
+    if (m > 4.0f) break;  // a branch: the select form took 124.8 vs 80.8 ms per C4 step
   }
   return fdiv(0.25f * flog(m) * fsqrt(m), dz);
 }
@@ -1923,8 +1938,11 @@ struct Integrator {
     const float flx = step_(0.5f, ax), fly = step_(0.5f, ay);
     const float hx = mixf(ax, 1.0f - ax, flx), hy = mixf(ay, 1.0f - ay, fly);
     const float sx = fsqrt(2.0f * hx), sy = fsqrt(2.0f * hy);
-    const float dx = mixf(sx - 1.0f, 1.0f - sx, flx) / (P.res_x * 0.5f) + stx;
-    const float dy = mixf(sy - 1.0f, 1.0f - sy, fly) / (P.res_y * 0.5f) + sty;
+    // x * (1/(res/2)): the reciprocal is per launch (hoisted), the division it
+    // replaces was a ~10-instruction correctly rounded expansion per sample
+    // (ulp-level, like the contracted geometry; 5.59 vs 5.80 ms per C2 launch)
+    const float dx = mixf(sx - 1.0f, 1.0f - sx, flx) * (1.0f / (P.res_x * 0.5f)) + stx;
+    const float dy = mixf(sy - 1.0f, 1.0f - sy, fly) * (1.0f / (P.res_y * 0.5f)) + sty;
     const v3 fp = normalize(((u * dx) * P.uULen + (v * dy) * P.uVLen) + w) * P.focal;
     v3 ro = mk(P.cam_px, P.cam_py, P.cam_pz), rd;
     if (P.aperture != 0.0f) {
@@ -2092,6 +2110,36 @@ DEV void restir_refill_body(const LaunchParams &P, It &it, const Scene &sc, cons
   }
 }
 
+// Path regeneration: the lane runs its pixel's passes back to back as ONE
+// loop of bounce steps; when its path ends it accumulates the sample and
+// starts the next pass at once instead of idling until the longest path of
+// its wave has finished.  Each pixel's samples are still produced and summed
+// in pass order, so the result is bit-identical to the plain loop.
+template <class It, class Cfg>
+DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int py, size_t apix) {
+  float4 a = P.accum[apix];
+  if (P.nframes > 0) {
+    typename It::Path ps;
+    int f = 0;
+    it.frame = P.frame0;
+    it.begin(ps, px, py);
+    bool alive = cfg.max_bounces() > 0;
+    while (true) {
+      // a lane whose march is still pending skips step() (its bounce resumes once it is done)
+      if (alive && !(It::SUSP && ps.ms.active)) alive = it.step(ps);
+      if (!alive) {
+        accumulate(it, P, a, it.finish(ps));
+        if (++f >= P.nframes) break;
+        it.frame = P.frame0 + (uint32_t)f;
+        it.begin(ps, px, py);
+        alive = cfg.max_bounces() > 0;
+      }
+      if constexpr (It::SUSP) it.march_pending(ps);
+    }
+  }
+  P.accum[apix] = a;
+}
+
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   if constexpr (Scene::kStatic) Scene::stage();  // LDS copy of the scene records (before any early exit)
@@ -2125,32 +2173,7 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       P.samples[(size_t)f * plane + lp] = make_float4(s.x, s.y, s.z, 0.f);
     }
   } else if constexpr (!RESTIR && !COUNT) {
-    // Path regeneration: the lane runs its pixel's passes back to back as ONE
-    // loop of bounce steps; when its path ends it accumulates the sample and
-    // starts the next pass at once instead of idling until the longest path
-    // of its wave has finished.  Each pixel's samples are still produced and
-    // summed in pass order, so the result is bit-identical to the plain loop.
-    float4 a = P.accum[apix];
-    if (P.nframes > 0) {
-      typename Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::Path ps;
-      int f = 0;
-      it.frame = P.frame0;
-      it.begin(ps, px, py);
-      bool alive = cfg.max_bounces() > 0;
-      while (true) {
-        // a lane whose march is still pending skips step() (its bounce resumes once it is done)
-        if (alive && !(decltype(it)::SUSP && ps.ms.active)) alive = it.step(ps);
-        if (!alive) {
-          accumulate(it, P, a, it.finish(ps));
-          if (++f >= P.nframes) break;
-          it.frame = P.frame0 + (uint32_t)f;
-          it.begin(ps, px, py);
-          alive = cfg.max_bounces() > 0;
-        }
-        if constexpr (decltype(it)::SUSP) it.march_pending(ps);
-      }
-    }
-    P.accum[apix] = a;
+    regen_pixel(P, it, cfg, px, py, apix);
   } else {
     float4 a = P.accum[apix];
     for (int f = 0; f < P.nframes; ++f) {
