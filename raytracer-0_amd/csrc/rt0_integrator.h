@@ -230,6 +230,9 @@ struct Hit {
 #ifndef RT0_MARCH_BUDGET
 #define RT0_MARCH_BUDGET 8
 #endif
+#ifndef RT0_FAST_SHADOW  // A/B knob: shadow rays through Geometry::shadow_light
+#define RT0_FAST_SHADOW 1
+#endif
 
 struct March {
   v3 o, d;
@@ -548,6 +551,97 @@ struct Geometry {
     return normalize(((a + b) + c) + d);
   }
 
+  // One candidate of intersection()'s mesh loop (raytracer.glsl:1009-1044):
+  // mesh i's hit distance if it is valid and beats `bound` (the running tmin),
+  // as iSphere (818-833, centre animated in RENDER_MODE 1, 819), iPlane
+  // (812-815) or iBox (836-851) decide it; returns the mesh type, -1 = no hit.
+  // Branch-free (v_cndmask selects): a lane never waits on another lane's
+  // taken branch inside the mesh loop.  m = 1/d (iBox's, hoisted), mo = m*o.
+  template <class Cfg>
+  static DEV int prim(const LaunchParams &P, const Scene &sc, const Cfg &C, int i, v3 o, v3 d, v3 m, v3 mo,
+                      float bound, float &t) {
+    const GeomRec g = sc.geom(i);
+    t = bound;
+    if (g.j0 == 0.0f) return -1;  // raytracer.glsl:1009
+    const v3 gp = mk(g.px, g.py, g.pz);
+    if (g.type == T_SPHERE) {
+      v3 oc = o - ((C.flags() & F_ANIM) ? anim_pos(P, i) : gp);
+      float b = dot(oc, d);
+      float c = dot(oc, oc) - g.d0;
+      float disc = b * b - c;
+      float sd = fsqrt(fmaxf(disc, 0.0f));
+      float t0 = -b - sd, t1 = -b + sd;
+      bool ok0 = (t0 > EPSILON && t0 < bound);
+      bool ok1 = (t1 > EPSILON && t1 < bound);
+      t = ok0 ? t0 : t1;
+      return disc >= 0.0f && (ok0 || ok1) ? (int)T_SPHERE : -1;
+    } else if (g.type == T_PLANE) {
+      int ax = -1;
+      if constexpr (Scene::kStatic) ax = axis_of(gp);  // folds: the normal is compile-time data
+      if (ax >= 0) {
+        // axis-aligned normal s*e_ax: dot(n, v) == s*v[ax] exactly for finite v,
+        // and 1/(s*d[ax]) == s*m[ax] (v_rcp is sign-symmetric) -- same bits,
+        // without the zero terms and a second reciprocal
+        const float s = ax == 0 ? gp.x : (ax == 1 ? gp.y : gp.z);
+        const float oa = ax == 0 ? o.x : (ax == 1 ? o.y : o.z);
+        const float ma = ax == 0 ? m.x : (ax == 1 ? m.y : m.z);
+        t = (g.d0 - s * oa) * (s * ma);
+      } else {
+        t = fdiv(g.d0 - dot(gp, o), dot(gp, d));
+      }
+      return (t > EPSILON && t < bound) ? (int)T_PLANE : -1;
+    } else if (g.type == T_BOX) {
+      // iBox's m*(centre - o) as m*centre - m*o: one FMA per axis (ulp-level,
+      // like the other contracted geometry); the box normal (853-856) depends
+      // only on the winner and its t, so intersect() evaluates it once after the loop
+      v3 nv = mk(__builtin_fmaf(m.x, gp.x, -mo.x), __builtin_fmaf(m.y, gp.y, -mo.y), __builtin_fmaf(m.z, gp.z, -mo.z));
+      v3 k = vabs(m) * g.d0;
+      v3 t1 = nv - k, t2 = nv + k;
+      float tN = fmaxf(fmaxf(t1.x, t1.y), t1.z);
+      float tF = fminf(fminf(t2.x, t2.y), t2.z);
+      t = (tN > 0.0f) ? tN : tF;
+      return !(tN > tF || tF < 0.0f) && !(t < EPSILON || t >= bound) ? (int)T_BOX : -1;
+    }
+    return -1;
+  }
+
+  // intersection() as calcDirectLighting's shadow ray reads it (raytracer.glsl:
+  // 1189-1196): only "is the closest hit a LIGHT, and which one" -- for
+  // scene-specialised quadric scenes.  The closest hit of intersection() is the
+  // lowest-index mesh of least valid t (strict < in index order), so it is a
+  // light iff the closest light (tL, iL) beats every other mesh: non-light i
+  // occludes iff t_i < tL, or t_i == tL and i < iL.  The light tests run
+  // first; the occluder tests are then independent of one another (no running
+  // tmin chain, no index/type bookkeeping).  A ray that hits nothing has
+  // hit.index = 0 (HIT_MISS, 105): lit iff mesh 0 is a light.  Returns the
+  // light's mesh or -1; tl = the closest hit's t.
+  template <class Cfg>
+  static DEV int shadow_light(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, float &tl) {
+    const v3 m = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+    const v3 mo = m * o;
+    float tL = INF_T;
+    int iL = -1;
+    for_meshes(sc, [&](int i) {
+      if (sc.mat(i).type != M_LIGHT) return;
+      float t;
+      const bool ok = prim<Cfg>(P, sc, C, i, o, d, m, mo, tL, t) >= 0;
+      tL = ok ? t : tL;
+      iL = ok ? i : iL;
+    });
+    // the next float above tL: a bound that also admits t == tL
+    const float tL_up = __int_as_float(__float_as_int(tL) + 1);
+    bool occ = false;
+    for_meshes(sc, [&](int i) {
+      if (sc.mat(i).type == M_LIGHT) return;
+      float t;
+      occ |= prim<Cfg>(P, sc, C, i, o, d, m, mo, i < iL ? tL_up : tL, t) >= 0;
+    });
+    tl = tL;
+    if (occ) return -1;
+    if (iL >= 0) return iL;
+    return sc.mat(0).type == M_LIGHT ? 0 : -1;
+  }
+
   // intersection(), raytracer.glsl:997-1082.  Returns tmin (INF_T = miss,
   // hit.index = 0 as HIT_MISS).  uv/texel parsing is omitted: only NULL_TEX
   // materials are accepted, so they never reach an output.
@@ -571,54 +665,12 @@ struct Geometry {
     // normal of iBox (853-856) depends only on the winning box and its t, so
     // it is evaluated once after the loop for the winner.
     for_meshes(sc, [&](int i) {
-      const GeomRec g = sc.geom(i);
-      if (g.j0 == 0.0f) return;  // raytracer.glsl:1009
-      const v3 gp = mk(g.px, g.py, g.pz);
-      if (g.type == T_SPHERE) {  // iSphere, 818-833 (centre animated in RENDER_MODE 1, 819)
-        v3 oc = o - ((C.flags() & F_ANIM) ? anim_pos(P, i) : gp);
-        float b = dot(oc, d);
-        float c = dot(oc, oc) - g.d0;
-        float disc = b * b - c;
-        float sd = fsqrt(fmaxf(disc, 0.0f));
-        float t0 = -b - sd, t1 = -b + sd;
-        bool ok0 = (t0 > EPSILON && t0 < tmin);
-        bool ok1 = (t1 > EPSILON && t1 < tmin);
-        float t = ok0 ? t0 : t1;
-        bool ok = disc >= 0.0f && (ok0 || ok1);
-        tmin = ok ? t : tmin;
-        type = ok ? (int)T_SPHERE : type;
-        hit.index = ok ? i : hit.index;
-      } else if (g.type == T_PLANE) {  // iPlane, 812-815
-        float t;
-        int ax = -1;
-        if constexpr (Scene::kStatic) ax = axis_of(gp);  // folds: the normal is compile-time data
-        if (ax >= 0) {
-          // axis-aligned normal s*e_ax: dot(n, v) == s*v[ax] exactly for finite v,
-          // and 1/(s*d[ax]) == s*m[ax] (v_rcp is sign-symmetric) -- same bits,
-          // without the zero terms and a second reciprocal
-          const float s = ax == 0 ? gp.x : (ax == 1 ? gp.y : gp.z);
-          const float oa = ax == 0 ? o.x : (ax == 1 ? o.y : o.z);
-          const float ma = ax == 0 ? m.x : (ax == 1 ? m.y : m.z);
-          t = (g.d0 - s * oa) * (s * ma);
-        } else {
-          t = fdiv(g.d0 - dot(gp, o), dot(gp, d));
-        }
-        bool ok = (t > EPSILON && t < tmin);
-        tmin = ok ? t : tmin;
-        type = ok ? (int)T_PLANE : type;
-        hit.index = ok ? i : hit.index;
-      } else if (g.type == T_BOX) {  // iBox, 836-851
-        v3 nv = mk(__builtin_fmaf(m.x, gp.x, -mo.x), __builtin_fmaf(m.y, gp.y, -mo.y), __builtin_fmaf(m.z, gp.z, -mo.z));
-        v3 k = vabs(m) * g.d0;
-        v3 t1 = nv - k, t2 = nv + k;
-        float tN = fmaxf(fmaxf(t1.x, t1.y), t1.z);
-        float tF = fminf(fminf(t2.x, t2.y), t2.z);
-        float t = (tN > 0.0f) ? tN : tF;
-        bool ok = !(tN > tF || tF < 0.0f) && !(t < EPSILON || t >= tmin);
-        tmin = ok ? t : tmin;
-        type = ok ? (int)T_BOX : type;
-        hit.index = ok ? i : hit.index;
-      }
+      float t;
+      const int ty = prim<Cfg>(P, sc, C, i, o, d, m, mo, tmin, t);
+      const bool ok = ty >= 0;
+      tmin = ok ? t : tmin;
+      type = ok ? ty : type;
+      hit.index = ok ? i : hit.index;
     });
     if constexpr (Scene::kMayHaveModels) {  // TRIANGLE models (after the quadrics, before the SDF march)
       if (sc.n_models() > 0 && P.n_tris > 0) {
@@ -1089,6 +1141,27 @@ struct Integrator {
       : P(p), sc(s), C(c), n_isect(0), n_iter(0), n_nee(0), n_map(0) {}
 
   DEV bool flag(uint32_t f) const { return (C.flags() & f) != 0; }
+  // Shadow rays of sphere lights through G::shadow_light: scene-specialised
+  // scenes of quadrics only (no SDF march, no triangle models, no textured
+  // light colour to evaluate at the hit).  RT0_FAST_SHADOW 0 = intersect().
+  static constexpr bool fast_shadow() {
+    if constexpr (Scene::kStatic) return RT0_FAST_SHADOW && Scene::kSdfs == 0 && !Scene::kMayHaveModels && !Scene::any_tex();
+    else return false;
+  }
+  static constexpr bool kFastShadow = fast_shadow();
+  // material of a shadow ray's light: folds to the one light mesh of a
+  // single-light scene, a per-lane record otherwise
+  DEV MatRec light_mat(int il) const {
+    int n = 0, only = 0;
+    if constexpr (Scene::kStatic)
+      static_for<0, Scene::kMeshes>([&](int i) {
+        if (sc.mat(i).type == M_LIGHT) {
+          ++n;
+          only = i;
+        }
+      });
+    return sc.mat(n == 1 ? only : il);
+  }
   // a light/sphere position as the reference reads it where it calls
   // getAnimatedPosition (RENDER_MODE 1); the static position otherwise
   DEV v3 lpos(int i, const GeomRec &g) const { return flag(F_ANIM) ? anim_pos(P, i) : mk(g.px, g.py, g.pz); }
@@ -1127,6 +1200,20 @@ struct Integrator {
         float d2 = dot(sw, sw);
         float cos_a_max = fsqrt(1.0f - fminf(fmaxf(fdiv(g.d0, d2), 0.0f), 1.0f));
         v3 sr = sample_cone(normalize(sw), 1.0f - cos_a_max, seed + 23.1656f);
+        if constexpr (kFastShadow) {
+          float t;
+          if (COUNT) ++n_isect;
+          const int il = G::template shadow_light<Cfg>(P, sc, C, x + nl * EPSILON, sr, t);
+          if (il >= 0) {
+            const MatRec mh = light_mat(il);
+            float weight = 2.0f * (1.0f - cos_a_max);
+            float T_fog = 1.0f;
+            if (VOL && flag(F_VOL)) T_fog = fexp(-VOL_SIGMA_T * t);
+            v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
+            dl = (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
+          }
+          return dl;
+        }
 #ifdef RT0_EXP_NO_SHADOW  // profiling experiment only (breaks parity): shadow ray skipped
         float t = 1.0f;
         hit.index = li;
@@ -1379,7 +1466,11 @@ struct Integrator {
       Res nb = empty_res();
       if (!(nx < 0.0f || nx > 1.0f || ny < 0.0f || ny > 1.0f)) {
         if (COUNT) ++n_stap;
+#ifdef RT0_EXP_SPATIAL_SELF  // profiling experiment only (breaks parity): every tap reads the pixel's own texels
+        nb = unpack(tex2d(P.rin[0], scx, scy), tex2d(P.rin[1], scx, scy));
+#else
         nb = unpack(tex2d(P.rin[0], nx, ny), tex2d(P.rin[1], nx, ny));
+#endif
       }
       if (nb.M > 0.0f) {
         if (nb.idx >= 0) {

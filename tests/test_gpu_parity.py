@@ -25,7 +25,7 @@ REL_TOL = 1e-3
 # fraction of pixels allowed to differ (discrete flips from ulp-level
 # differences between gfx950 transcendentals and the reference executor's, and
 # from FMA contraction outside the RNG; ray-marched SDF scenes amplify them)
-BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol": 0.03, "menger_coat": 0.03,
+BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol_1l": 0.03, "menger_coat": 0.03,
             "mis_demo_sdfbox": 0.02, "restir_mis_demo": 0.02, "c3_outdoor_restir": 0.01,
             # glossy METAL reflections grazing the slab's front edge; the noise
             # texture's bilinear weights differ from SwiftShader's by ~6e-4
@@ -37,7 +37,9 @@ BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol": 0.03, "m
 # mean radiance vs the fixture (default 5e-3); cube_sdf_metal: SwiftShader's
 # image of this SDF-only scene depends on the order of its SDF statements
 # (tests/test_oracle_golden.py MEAN_TOL)
-MEAN_TOL = {"cube_sdf_metal": 0.025}
+MEAN_TOL = {"cube_sdf_metal": 0.025,
+            # 8x8 per-frame volumetric fixtures: one flip onto the light moves the mean by up to 0.03
+            "c4_mandelbulb_vol": 0.1, "vol_cornell_2": 0.02, "spectral_vol_1l": 0.05}
 
 
 def cfg_by_name(cfgs, name):
@@ -78,7 +80,7 @@ def have(name):
 
 
 NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "cornell_nee_plain",
-              "mis_demo_sdfbox", "menger_coat", "thinlens_glass", "c4_mandelbulb_vol", "spectral_vol",
+              "mis_demo_sdfbox", "menger_coat", "thinlens_glass", "c4_mandelbulb_vol", "spectral_vol_1l",
               "tex_sdf_metal", "tex_light_sphere", "tex_check_test", "cube_spheres", "cube_sdf_metal",
               "sdf_triprism", "sdf_cone", "spectral_cornell", "vol_cornell_2",
               "page_scene0_slabfirst", "tex_check_assets", "page_scene1", "cube_spheres_assets"]
@@ -221,7 +223,8 @@ def test_gpu_restir_chain_matches_oracle_chain(cfgs, gpu_required):
 
 @pytest.mark.parametrize("name,size,frames", [("c2_cornell_mis_8", 128, 2), ("cornell_nee_plain", 96, 1),
                                               ("c4_mandelbulb_vol", 48, 1), ("tex_check_test", 96, 2),
-                                              ("tex_light_sphere", 96, 1), ("cube_spheres", 96, 2)])
+                                              ("tex_light_sphere", 96, 1), ("cube_spheres", 96, 2),
+                                              ("spectral_vol", 64, 2)])
 def test_gpu_matches_oracle_beyond_fixtures(name, size, frames, cfgs, gpu_required):
     cfg = cfg_by_name(cfgs, name)
     over = {"MAX_BOUNCES": 12} if name == "c4_mandelbulb_vol" else {}
