@@ -352,10 +352,18 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
 // closest triangle hit along (o, d) before tmin: depth-first, nearer child
 // first, the far child on a per-lane stack in LDS (stride = block size so the
 // 64 lanes of a wave hit 64 different banks).  Returns the leaf-order triangle
-// index or -1; tmin is updated.
-DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
+// index or -1; tmin is updated.  ANY: stop at the first hit before tmin (an
+// occlusion query: whether some triangle lies in (EPSILON, tmin)).
+// The per-lane traversal stacks: ONE LDS array for every traversal of the
+// kernel (closest-hit and occlusion instances alike -- a __shared__ array
+// declared inside the template would be one array per instance).
+DEV int32_t *bvh_stack_lds() {
   __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
-  int32_t *stk = stk_base + threadIdx.x;
+  return stk_base + threadIdx.x;
+}
+template <bool ANY = false>
+DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
+  int32_t *stk = bvh_stack_lds();
   int sp = 0, node = 0, best = -1;
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
   const TriDev *__restrict__ tris = P.tris;
@@ -412,6 +420,7 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
         }
       }
       pend = -1;
+      if (ANY && best >= 0) break;
     } else if (has && pend < 0) {
       pend = l0 >= 0 ? l0 : l1;
     }
@@ -457,6 +466,7 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
         tmin = t;
         best = l1;
       }
+      if (ANY && best >= 0) break;
     }
 #else
     if (tl != F_INF && cl < 0) {  // leaves are tested in place
@@ -475,6 +485,7 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
       }
       tr = F_INF;
     }
+    if (ANY && best >= 0) break;
 #endif
     if (tl != F_INF && tr != F_INF) {
       const bool lfirst = tl <= tr;
@@ -616,7 +627,8 @@ struct Geometry {
   // hit.index = 0 (HIT_MISS, 105): lit iff mesh 0 is a light.  Returns the
   // light's mesh or -1; tl = the closest hit's t.
   template <class Cfg>
-  static DEV int shadow_light(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, float &tl) {
+  static DEV int shadow_light(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, float &tl,
+                              unsigned long long *nbvh = nullptr) {
     const v3 m = mk(frcp(d.x), frcp(d.y), frcp(d.z));
     const v3 mo = m * o;
     float tL = INF_T;
@@ -637,9 +649,42 @@ struct Geometry {
       occ |= prim<Cfg>(P, sc, C, i, o, d, m, mo, i < iL ? tL_up : tL, t) >= 0;
     });
     tl = tL;
-    if (occ) return -1;
-    if (iL >= 0) return iL;
-    return sc.mat(0).type == M_LIGHT ? 0 : -1;
+    int il = occ ? -1 : (iL >= 0 ? iL : (sc.mat(0).type == M_LIGHT ? 0 : -1));
+    if constexpr (Scene::kMayHaveModels) {
+      // triangles come after the quadrics (strict <): one before tL is the
+      // closest hit, and no model is a light -- an occlusion query suffices
+      if (il >= 0 && sc.n_models() > 0 && P.n_tris > 0) {
+        float tt = tL;
+        if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) il = -1;
+      }
+    }
+    return il;
+  }
+  // isVisible() (raytracer.glsl:1539-1557) in the same spirit: the closest
+  // quadric (t_q, i_q), then one occlusion query of the triangles up to
+  // min(t_q, dist - 2*EPSILON): a triangle there is the closest hit and hides
+  // `to`; otherwise the quadric decides (a light is transparent to the test).
+  template <class Cfg>
+  static DEV bool visible_fast(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, float lim,
+                               unsigned long long *nbvh = nullptr) {
+    const v3 m = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+    const v3 mo = m * o;
+    float tq = INF_T;
+    int iq = 0;
+    for_meshes(sc, [&](int i) {
+      float t;
+      const bool ok = prim<Cfg>(P, sc, C, i, o, d, m, mo, tq, t) >= 0;
+      tq = ok ? t : tq;
+      iq = ok ? i : iq;
+    });
+    if constexpr (Scene::kMayHaveModels) {
+      if (sc.n_models() > 0 && P.n_tris > 0) {
+        float tt = fminf(tq, lim);
+        if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) return false;
+      }
+    }
+    if (tq < lim) return sc.mat(iq).type == M_LIGHT;
+    return true;
   }
 
   // intersection(), raytracer.glsl:997-1082.  Returns tmin (INF_T = miss,
@@ -1144,11 +1189,10 @@ struct Integrator {
   // Shadow rays of sphere lights through G::shadow_light: scene-specialised
   // scenes of quadrics only (no SDF march, no triangle models, no textured
   // light colour to evaluate at the hit).  RT0_FAST_SHADOW 0 = intersect().
-  static constexpr bool fast_shadow() {
-    if constexpr (Scene::kStatic) return RT0_FAST_SHADOW && Scene::kSdfs == 0 && !Scene::kMayHaveModels && !Scene::any_tex();
-    else return false;
+  DEV bool fast_shadow() const {
+    if constexpr (Scene::kStatic) return RT0_FAST_SHADOW && Scene::kSdfs == 0 && !Scene::any_tex();
+    else return RT0_FAST_SHADOW && sc.n_sdfs() == 0 && !sc.any_tex();
   }
-  static constexpr bool kFastShadow = fast_shadow();
   // material of a shadow ray's light: folds to the one light mesh of a
   // single-light scene, a per-lane record otherwise
   DEV MatRec light_mat(int il) const {
@@ -1200,10 +1244,10 @@ struct Integrator {
         float d2 = dot(sw, sw);
         float cos_a_max = fsqrt(1.0f - fminf(fmaxf(fdiv(g.d0, d2), 0.0f), 1.0f));
         v3 sr = sample_cone(normalize(sw), 1.0f - cos_a_max, seed + 23.1656f);
-        if constexpr (kFastShadow) {
+        if (fast_shadow()) {
           float t;
           if (COUNT) ++n_isect;
-          const int il = G::template shadow_light<Cfg>(P, sc, C, x + nl * EPSILON, sr, t);
+          const int il = G::template shadow_light<Cfg>(P, sc, C, x + nl * EPSILON, sr, t, COUNT ? n_bvh : nullptr);
           if (il >= 0) {
             const MatRec mh = light_mat(il);
             float weight = 2.0f * (1.0f - cos_a_max);
@@ -1295,6 +1339,11 @@ struct Integrator {
     float dist = length(sd);
     if (dist < EPSILON * 10.0f) return true;
     sd = normalize(sd);
+    if (fast_shadow()) {
+      if (COUNT) ++n_isect;
+      return G::template visible_fast<Cfg>(P, sc, C, from + (sd * EPSILON) * 2.0f, sd, dist - EPSILON * 2.0f,
+                                           COUNT ? n_bvh : nullptr);
+    }
     Hit h;
     float t = isect(from + (sd * EPSILON) * 2.0f, sd, h);
     if (t < dist - EPSILON * 2.0f) {
