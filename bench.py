@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(HERE, "raytracer-0_amd"))
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
-PROFILE_ROUND = "r02"  # profiles/<round>/ holding the PMC summary of the default workload
+PROFILE_ROUND = "r02/s2"  # profiles/<dir>/ holding the PMC summaries (pmc_<config>.json) of each workload
 BAND = 16
 
 

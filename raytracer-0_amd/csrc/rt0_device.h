@@ -71,8 +71,23 @@ struct BvhNode {
   float rz0, rx1, ry1, rz1;
   int32_t left, right, pad0, pad1;
 };
+// Bvh4Node 128 B (one L2 line): the 4-wide tree the host collapses from the
+// binary LBVH (rt0_host.cpp: collapse_bvh4).  Child boxes as SoA over the four
+// slots (mn.x[k] .. mx.z[k]); link[k] >= 0 internal node, < 0 leaf =
+// ~(first | (count - 1) << RT0_LEAF_SHIFT): triangles [first, first + count)
+// of the leaf order.  An empty slot holds the box (+inf)^3..(+inf)^3, which
+// no slab test enters.
+struct Bvh4Node {
+  float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
+  int32_t link[4];
+  int32_t pad[4];
+};
+#define RT0_LEAF_SHIFT 27  // leaf first index < 2^27, count <= 16
+#ifndef RT0_BVH_WIDE
+#define RT0_BVH_WIDE 0  // 1: walk the 4-wide tree (measured slower on C5); built only when selected
+#endif
 #ifndef RT0_BVH_STACK
-#define RT0_BVH_STACK 48  // traversal stack entries per lane (LDS); the build checks the depth
+#define RT0_BVH_STACK 48  // traversal stack entries per lane (LDS); the build checks the bound
 #endif
 
 struct SceneDev {
@@ -154,6 +169,7 @@ struct LaunchParams {
   int32_t cube_size;
   // Triangle models: LBVH nodes (root 0) and triangles in leaf order; n_tris 0 = none.
   const BvhNode *bvh;
+  const Bvh4Node *bvh4;  // the same tree collapsed 4-wide (RT0_BVH_WIDE)
   const TriDev *tris;
   int32_t n_tris;
   // RENDER_MODE 1 (F_ANIM): the accumulator is an EMA with weight ema_alpha =

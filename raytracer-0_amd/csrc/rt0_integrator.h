@@ -362,7 +362,7 @@ DEV int32_t *bvh_stack_lds() {
   return stk_base + threadIdx.x;
 }
 template <bool ANY = false>
-DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
+DEV int bvh2_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
   int32_t *stk = bvh_stack_lds();
   int sp = 0, node = 0, best = -1;
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
@@ -502,6 +502,107 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
     }
   }
   return best;
+}
+
+// (t, link) compare-exchange: the nearer child first
+DEV void cx_near(float &ta, int &ca, float &tb, int &cb) {
+  const bool s = tb < ta;
+  const float t = s ? tb : ta;
+  const int c = s ? cb : ca;
+  tb = s ? ta : tb;
+  cb = s ? ca : cb;
+  ta = t;
+  ca = c;
+}
+// The same query over the 4-wide tree (Bvh4Node): one 128-B node fetch tests
+// four child boxes, so a ray makes about half the dependent node fetches of
+// the binary walk.  Hit leaves are tested first, in slot order, through one
+// triangle-test site (a lane walks the triangles of all its hit leaves in one
+// loop); the internal children still entered before the updated tmin are
+// sorted by entry distance (5-exchange network), the nearest is visited next
+// and the others are pushed far to near.  The build bounds the pushes along
+// any root-to-leaf path by RT0_BVH_STACK - 1.
+template <bool ANY = false>
+DEV int bvh4_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
+  int32_t *stk = bvh_stack_lds();
+  int sp = 0, node = 0, best = -1;
+  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh4);
+  const TriDev *__restrict__ tris = P.tris;
+  // fewer than n_tris nodes, each visited at most once: the cap only
+  // guarantees that every wave exits even on a corrupt tree
+  for (int guard = P.n_tris + 8; guard > 0; --guard) {
+    const float4 *nd = nodes + 8 * node;
+    const float4 mnx = nd[0], mny = nd[1], mnz = nd[2], mxx = nd[3], mxy = nd[4], mxz = nd[5];
+    const int4 lk = reinterpret_cast<const int4 *>(nd)[6];
+    float t0 = box_enter(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, tmin);
+    float t1 = box_enter(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, tmin);
+    float t2 = box_enter(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, tmin);
+    float t3 = box_enter(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, tmin);
+    int c0 = lk.x, c1 = lk.y, c2 = lk.z, c3 = lk.w;
+    if (cnt) cnt[0] += 2;  // counted in the binary node's unit: pairs of slab tests
+    unsigned lm = (t0 != F_INF && c0 < 0 ? 1u : 0u) | (t1 != F_INF && c1 < 0 ? 2u : 0u) |
+                  (t2 != F_INF && c2 < 0 ? 4u : 0u) | (t3 != F_INF && c3 < 0 ? 8u : 0u);
+    if (lm) {
+      int cur = 0, end = 0;
+      for (;;) {
+        if (cur == end) {
+          if (lm == 0) break;
+          const int k = __builtin_ctz(lm);
+          lm &= lm - 1;
+          const int e = ~(k == 0 ? c0 : (k == 1 ? c1 : (k == 2 ? c2 : c3)));
+          cur = e & ((1 << RT0_LEAF_SHIFT) - 1);
+          end = cur + (e >> RT0_LEAF_SHIFT) + 1;
+        }
+        float t;
+        if (cnt) ++cnt[1];  // triangle tests
+        if (tri_test(tris[cur], o, d, tmin, t)) {
+          tmin = t;
+          best = cur;
+        }
+        ++cur;
+        if (ANY && best >= 0) break;
+      }
+      if (ANY && best >= 0) break;
+    }
+    // internal children still entered before tmin (leaves are done)
+    t0 = (c0 < 0 || !(t0 < tmin)) ? F_INF : t0;
+    t1 = (c1 < 0 || !(t1 < tmin)) ? F_INF : t1;
+    t2 = (c2 < 0 || !(t2 < tmin)) ? F_INF : t2;
+    t3 = (c3 < 0 || !(t3 < tmin)) ? F_INF : t3;
+    cx_near(t0, c0, t1, c1);
+    cx_near(t2, c2, t3, c3);
+    cx_near(t0, c0, t2, c2);
+    cx_near(t1, c1, t3, c3);
+    cx_near(t1, c1, t2, c2);
+    if (t0 == F_INF) {
+      if (sp == 0) break;
+      node = stk[256 * --sp];
+      continue;
+    }
+    node = c0;
+    if (t3 != F_INF) {
+      stk[256 * sp] = c3;
+      sp = min(sp + 1, RT0_BVH_STACK - 1);
+    }
+    if (t2 != F_INF) {
+      stk[256 * sp] = c2;
+      sp = min(sp + 1, RT0_BVH_STACK - 1);
+    }
+    if (t1 != F_INF) {
+      stk[256 * sp] = c1;
+      sp = min(sp + 1, RT0_BVH_STACK - 1);
+    }
+  }
+  return best;
+}
+
+template <bool ANY = false>
+DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
+#if RT0_BVH_WIDE
+  return bvh4_closest<ANY>(P, o, d, inv, tmin, cnt);
+#else
+  return bvh2_closest<ANY>(P, o, d, inv, tmin, cnt);
+#endif
 }
 
 // getAnimatedPosition(meshes[i].pos, i, u_time) (raytracer.glsl:263-298),

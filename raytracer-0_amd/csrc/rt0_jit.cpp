@@ -63,6 +63,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // 8) instead of the ahead-of-time kernels' 48: 48 x 256 lanes x 4 B = 48 KiB
   // per workgroup would cap a CU at three workgroups
   if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
+  o << "#define RT0_BVH_WIDE " << k.bvh_wide << "\n";
   o << "using __hip_internal::int32_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
   o << strip_includes(rt0_jit_source_text);
   const int nt = s.n_total;
@@ -327,8 +328,15 @@ uint32_t flags_from_config(const rt0_config &g) {
   return f;
 }
 
+bool bvh_wide_selected() {
+  static const bool w = getenv("RT0_BVH_WIDE") && atoi(getenv("RT0_BVH_WIDE")) != 0;
+  return w;
+}
+
 JitKey make_jit_key(const rt0_config &g, int n_sdfs) {
   JitKey k;
+  // RT0_BVH_WIDE=1: the 4-wide walk instead of the binary one (A/B knob)
+  k.bvh_wide = bvh_wide_selected() ? 1 : 0;
   k.flags = flags_from_config(g);
   k.max_bounces = g.max_bounces;
   k.max_diff = g.max_diff_bounces;

@@ -5,9 +5,10 @@
 # Env: TESTS=0 skips pytest; CONFIGS="c2 c1 c3 c4 c5" picks workloads;
 #      PROFILE=0 skips rocprof; PMC=0 skips the counter passes.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/r2
+O=gpurun_out/${OUT:-r2}
+mkdir -p $O
 export TMPDIR=/tmp
-O=gpurun_out/r2
+
 ok_or_fail() { local rc=$1; if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "GPU step failed rc=$rc: stopping"; exit "$rc"; fi; }
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > $O/pytest_gpu.log 2>&1

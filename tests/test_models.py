@@ -9,7 +9,8 @@ agree within the usual per-pixel tolerance.
 
 CPU: scene grammar with TRIANGLE entries, OBJ reading, mesh generators, the
 oracle's brute-force path.  GPU: BVH build (counts, depth bound), render parity
-vs the brute-force oracle, JIT == AOT, rebuild on model/scene change.
+vs the brute-force oracle, JIT == AOT, rebuild on model/scene change, the
+4-wide walk (RT0_BVH_WIDE=1) == the binary one.
 """
 import os
 
@@ -210,3 +211,41 @@ def test_c5_matches_bruteforce_oracle(cfgs, gpu_required):
         m, a = r.read_restir(0)
         okr = pixel_match(m, Mr[k - 1]) & pixel_match(a, Ar[k - 1])
         assert okr.mean() >= 0.97, (k, okr.mean())
+
+
+_WIDE_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = sys.argv[1:3]
+import oracle as O, rt0
+import test_models as T
+cfgs = O.load_configs()
+out = []
+for name, w, h, k in (("tri_models", 64, 64, 2), ("c5_spectral_models", 48, 48, 1)):
+    r = T.make(T.cfg_by_name(cfgs, name), cfgs, w, h)
+    r.render(k, 1)
+    out.append(r.read_accum())
+np.savez(sys.argv[3], *out)
+"""
+
+
+@pytest.mark.gpu
+def test_wide_bvh_walk_matches_binary(cfgs, gpu_required, tmp_path):
+    """RT0_BVH_WIDE=1 (the 4-wide tree collapsed from the LBVH, read at
+    process start, so it runs in a child process) finds the same closest hits
+    as the default binary walk: the images agree pixel for pixel (a triangle
+    tie at equal t may resolve to the other triangle: >= 99.9% bitwise)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    out = tmp_path / "wide.npz"
+    env = dict(os.environ, RT0_BVH_WIDE="1", PYTHONPATH=here)
+    subprocess.run([sys.executable, "-c", _WIDE_CHILD, os.path.join(repo, "raytracer-0_amd"),
+                    os.path.join(repo, "oracle"), str(out)], env=env, check=True, timeout=300)
+    wide = np.load(out)
+    for i, (name, w, h, k) in enumerate((("tri_models", 64, 64, 2), ("c5_spectral_models", 48, 48, 1))):
+        r = make(cfg_by_name(cfgs, name), cfgs, w, h)
+        r.render(k, 1)
+        got = r.read_accum()
+        same = (got == wide["arr_%d" % i]).all(-1)
+        assert same.mean() >= 0.999, (name, same.mean())
