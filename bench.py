@@ -47,7 +47,7 @@ sys.path.insert(0, os.path.join(HERE, "raytracer-0_amd"))
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
-PROFILE_ROUND = "r02/s2"  # profiles/<dir>/ holding the PMC summaries (pmc_<config>.json) of each workload
+PROFILE_ROUND = "r02/final"  # profiles/<dir>/ holding the PMC summaries (pmc_<config>.json) of each workload
 BAND = 16
 
 
@@ -154,6 +154,7 @@ def cpu_baseline_c(wl, budget_s=8.0):
     """Time the C restatement (OpenMP, all host threads we are allowed) on a
     bounded sample of the same workload: a full-width band of 64 rows through
     the image centre, successive passes, scaled by samples."""
+    import numpy as np
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as O
     threads = host_threads()
@@ -162,7 +163,19 @@ def cpu_baseline_c(wl, budget_s=8.0):
     cfg = {"scene_lines": wl["scene_lines"], "sdf_kinds": wl.get("sdf_kinds", []), "defines": wl["defines"],
            "constants": wl["constants"], "camera": wl["camera"], "models": wl.get("models", [])}
     o = O.Oracle(cfg, {"cornell_lines": None, "default_camera": wl["camera"]}, width=W, height=H)
-    o.frame(1, rows=(r0, r0 + 8), threads=threads)  # warm
+    what = ""
+    if wl.get("models"):
+        # the restatement (like the reference, which has no triangle path at
+        # all) loops over every triangle per ray: a one-row sample, ~5 s a row
+        from rt0 import meshes, workloads
+        inst = workloads.model_instances(wl)
+        soup = [meshes.world_triangles(v, t, pos, scale) for v, t, pos, scale, _ in inst]
+        v9 = np.concatenate(soup)
+        o.set_triangles(v9, np.concatenate([np.full(len(x), i[4], np.int32) for x, i in zip(soup, inst)]))
+        rows, r0 = 1, H // 2
+        what = ", brute force over all %d triangles per ray" % len(v9)
+    else:
+        o.frame(1, rows=(r0, r0 + 8), threads=threads)  # warm
     n = 0
     t0 = time.time()
     while time.time() - t0 < budget_s:
@@ -172,7 +185,7 @@ def cpu_baseline_c(wl, budget_s=8.0):
     samples = n * rows * W
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": "oracle/rt0_oracle.c (OpenMP x%d), rows %d..%d of the %dx%d bench image, %d passes "
-                      "(%d samples, %.1f s)" % (threads, r0, r0 + rows - 1, W, H, n, samples, dt)}
+                      "(%d samples, %.1f s)%s" % (threads, r0, r0 + rows - 1, W, H, n, samples, dt, what)}
 
 
 # ---------------------------------------------------------------- workloads
@@ -405,14 +418,17 @@ def main():
         torch.cuda.synchronize()
         out["secondary_refcaps_Msamples_s"] = round(W * H * sec["spp"] * args.steps
                                                     / (time.perf_counter() - t1) / 1e6, 3)
-    if not args.no_cpu_baseline and world == 1 and wl.get("models"):
-        out["cpu_baseline"] = None  # brute-force triangles in the restatement: minutes per row, no bounded sample
-    elif not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-        js = cpu_baseline_js(wl)
+    if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
+        # the JS integrator covers quadrics, SDFs, media and MIS (SURVEY 8d's
+        # C1/C2/C4 feature sets), not ReSTIR or triangle models
+        js_gap = ("ReSTIR" if workloads.restir(wl) else None) or ("triangle models" if wl.get("models") else None)
+        js = None if js_gap else cpu_baseline_js(wl)
         c_port = cpu_baseline_c(wl)
         out["cpu_baseline"] = js if js and "value" in js else c_port
         out["cpu_baseline_c"] = c_port  # the C oracle on the same sample (OpenMP)
-        if js and "error" in js:
+        if js_gap:
+            out["cpu_baseline_js_skipped"] = "the JS CPU integrator has no %s: the C restatement is the baseline" % js_gap
+        elif js and "error" in js:
             out["cpu_baseline_js_error"] = js["error"][-160:]
     print(json.dumps(out), flush=True)
     if dist:

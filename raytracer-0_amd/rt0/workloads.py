@@ -41,3 +41,19 @@ def configure(renderer, wl, constants=None):
 
 def restir(wl):
     return bool(wl.get("defines", {}).get("USE_RESTIR"))
+
+
+def model_instances(wl):
+    """[(positions, triangles, pos, scale, k)] of each TRIANGLE entry k whose
+    scale (joker.x) is non-zero, as librt0's BVH build instances them."""
+    import rt0
+    from rt0 import meshes as M
+    gens = {"icosphere": M.icosphere, "wavy_icosphere": M.wavy_icosphere}
+    cfg = {"scene_lines": wl["scene_lines"], "sdf_kinds": wl.get("sdf_kinds", [])}
+    scene, sdf = rt0.scene_strings(cfg, {"cornell_lines": None})
+    meshes, ne, ns, _ = rt0.parse_scene(scene, sdf)
+    out = []
+    for k, (m, inst) in enumerate(zip(wl.get("models", []), meshes[ne + ns:])):
+        if inst.joker[0] != 0.0:
+            out.append(gens[m["kind"]](m["level"]) + (list(inst.pos), inst.joker[0], k))
+    return out
