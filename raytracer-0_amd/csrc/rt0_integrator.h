@@ -87,6 +87,12 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_OPQ
 #define RT0_OPQ 0
 #endif
+// ReSTIR reservoir taps fetched per batch (temporal levels together, spatial
+// taps RT0_TAP_BATCH at a time); 1 = one tap at a time.  The scene-specialised
+// kernels of ReSTIR scenes without models use 2 (rt0_jit.cpp)
+#ifndef RT0_TAP_BATCH
+#define RT0_TAP_BATCH 1
+#endif
 DEV float opq(float x) {
 #if RT0_OPQ
   asm("" : "+v"(x));
@@ -1466,6 +1472,10 @@ struct Integrator {
     if (P.halo_miss && (y0 < P.valid_lo || y1 >= P.valid_hi)) atomicAdd(P.halo_miss, 1u);
     float4 t00 = t[(size_t)y0 * P.width + x0], t10 = t[(size_t)y0 * P.width + x1];
     float4 t01 = t[(size_t)y1 * P.width + x0], t11 = t[(size_t)y1 * P.width + x1];
+    return bil_lerp(t00, t10, t01, t11, a, b);
+  }
+  DEV static float4 bil_lerp(float4 t00, float4 t10, float4 t01, float4 t11, float a, float b) {
+#pragma clang fp contract(off)
     float4 r;
     float top, bot;
     top = t00.x + opq(a * (t10.x - t00.x)); bot = t01.x + opq(a * (t11.x - t01.x)); r.x = top + opq(b * (bot - top));
@@ -1473,6 +1483,40 @@ struct Integrator {
     top = t00.z + opq(a * (t10.z - t00.z)); bot = t01.z + opq(a * (t11.z - t01.z)); r.z = top + opq(b * (bot - top));
     top = t00.w + opq(a * (t10.w - t00.w)); bot = t01.w + opq(a * (t11.w - t01.w)); r.w = top + opq(b * (bot - top));
     return r;
+  }
+  // tex2d split in two so that several taps' loads can be issued before any
+  // of them is consumed (RT0_TAP_BATCH): the texel addresses and weights of a
+  // tap (the same arithmetic as tex2d; `count` = the tap is really fetched,
+  // for the sharded-ReSTIR halo check), then the lerp of the loaded texels
+  struct Bil {
+    uint32_t i00, i10, i01, i11;
+    float a, b;
+  };
+  DEV Bil bil_at(float u, float v, bool count) {
+#pragma clang fp contract(off)
+    float x = opq(u * P.res_x) - 0.5f, y = opq(v * P.res_y) - 0.5f;
+    float fx0 = floorf(x), fy0 = floorf(y);
+    Bil r;
+    r.a = x - fx0;
+    r.b = y - fy0;
+    int x0 = (int)fx0, y0 = (int)fy0;
+    int x1 = min(max(x0 + 1, 0), P.width - 1), y1 = min(max(y0 + 1, 0), P.height - 1);
+    x0 = min(max(x0, 0), P.width - 1);
+    y0 = min(max(y0, 0), P.height - 1);
+    if (count && P.halo_miss && (y0 < P.valid_lo || y1 >= P.valid_hi)) atomicAdd(P.halo_miss, 1u);
+    r.i00 = (uint32_t)(y0 * P.width + x0);
+    r.i10 = (uint32_t)(y0 * P.width + x1);
+    r.i01 = (uint32_t)(y1 * P.width + x0);
+    r.i11 = (uint32_t)(y1 * P.width + x1);
+    return r;
+  }
+  // the bilinear main/aux reservoir pair of a tap
+  DEV static void bil_fetch2(const float4 *__restrict__ tm, const float4 *__restrict__ ta, const Bil &q, float4 &m,
+                             float4 &a) {
+    const float4 m00 = tm[q.i00], m10 = tm[q.i10], m01 = tm[q.i01], m11 = tm[q.i11];
+    const float4 a00 = ta[q.i00], a10 = ta[q.i10], a01 = ta[q.i01], a11 = ta[q.i11];
+    m = bil_lerp(m00, m10, m01, m11, q.a, q.b);
+    a = bil_lerp(a00, a10, a01, a11, q.a, q.b);
   }
   DEV Res unpack(float4 m, float4 a) {
     Res r = empty_res();
@@ -1562,8 +1606,38 @@ struct Integrator {
     }
     Res tr = init;
     if (frame > 2u) {
+#if RT0_TAP_BATCH > 1
+      // both history levels' texels are fetched before either is combined
+      // (the same taps and arithmetic; only the loads move up)
+      bool hin[2];
+      float4 hm[2], ha[2];
+      {
+        Bil hq[2];
+#pragma unroll
+        for (int lvl = 0; lvl < 2; lvl++) {  // sampleTemporalHistory, 1485-1523
+          v3 m3 = hp - mk(P.cam_px, P.cam_py, P.cam_pz);
+          float ms = 0.001f * (float)(lvl + 1);
+          float hjx, hjy;
+          hash2(nc_addmul(scx, (float)((uint32_t)lvl + frame), 0.1f),
+                nc_addmul(scy, (float)((uint32_t)lvl + frame), 0.1f), hjx, hjy);
+          float px = (scx + m3.x * ms) + (hjx - 0.5f) * 0.002f;
+          float py = (scy + m3.y * ms) + (hjy - 0.5f) * 0.002f;
+          hin[lvl] = !(px < 0.01f || px > 0.99f || py < 0.01f || py > 0.99f);
+          if (COUNT && !GHOST && hin[lvl]) ++n_ttap;
+          hq[lvl] = bil_at(px, py, hin[lvl]);
+        }
+        bil_fetch2(P.rin[2], P.rin[3], hq[0], hm[0], ha[0]);
+        bil_fetch2(P.rin[4], P.rin[5], hq[1], hm[1], ha[1]);
+      }
+#endif
       for (int lvl = 0; lvl < 2; lvl++) {
         Res h = empty_res();
+#if RT0_TAP_BATCH > 1
+        if (hin[lvl]) {
+          h = unpack(lvl == 0 ? hm[0] : hm[1], lvl == 0 ? ha[0] : ha[1]);
+          if (valid_res(h)) h.age += (float)(lvl + 1);
+        }
+#else
         {  // sampleTemporalHistory, 1485-1523
           v3 m3 = hp - mk(P.cam_px, P.cam_py, P.cam_pz);
           float ms = 0.001f * (float)(lvl + 1);
@@ -1580,6 +1654,7 @@ struct Integrator {
             if (valid_res(h)) h.age += (float)(lvl + 1);
           }
         }
+#endif
         if (valid_res(h) && h.M > 0.0f && h.age < 30.0f) {
           if (flag(F_ANIM) && h.idx >= 0 && h.idx < nl) {  // history follows the moving light, 1669-1676
             const int act = sc.light(h.idx);
@@ -1609,6 +1684,45 @@ struct Integrator {
     if (GHOST) ns = 0;
     const float PX[8] = {-0.4706f, 0.8090f, -0.2628f, 0.6882f, -0.9511f, 0.1625f, 0.5000f, -0.6882f};
     const float PY[8] = {0.4706f, 0.2628f, -0.8090f, -0.5000f, -0.1625f, 0.9511f, -0.6882f, 0.5000f};
+#if RT0_TAP_BATCH > 1
+    // RT0_TAP_BATCH taps at a time: their texel loads are issued together
+    // before the first of them is combined, so a lane waits for one memory
+    // round trip per batch instead of one per tap.  Same taps, same order,
+    // same arithmetic (out-of-range taps load clamped texels and drop them).
+    for (int i0 = 0; i0 < ns; i0 += RT0_TAP_BATCH) {
+      float tsx[RT0_TAP_BATCH], tsy[RT0_TAP_BATCH];
+      bool tin[RT0_TAP_BATCH];
+      float4 tm[RT0_TAP_BATCH], ta[RT0_TAP_BATCH];
+      {
+        Bil tq[RT0_TAP_BATCH];
+#pragma unroll
+        for (int j = 0; j < RT0_TAP_BATCH; ++j) {
+          const int i = i0 + j, ic = min(i, 7);
+          hash2(nc_addmul(sx, (float)i, 0.3f), nc_addmul(sy, (float)i, 0.4f), tsx[j], tsy[j]);
+          float nx = scx + (PX[ic] * 16.0f) / P.res_x, ny = scy + (PY[ic] * 16.0f) / P.res_y;
+          tin[j] = i < ns && !(nx < 0.0f || nx > 1.0f || ny < 0.0f || ny > 1.0f);
+          if (COUNT && tin[j]) ++n_stap;
+          tq[j] = bil_at(nx, ny, tin[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < RT0_TAP_BATCH; ++j) bil_fetch2(P.rin[0], P.rin[1], tq[j], tm[j], ta[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < RT0_TAP_BATCH; ++j) {
+        if (i0 + j >= ns) break;
+        Res nb = empty_res();
+        if (tin[j]) nb = unpack(tm[j], ta[j]);
+        if (nb.M > 0.0f) {
+          if (nb.idx >= 0) {
+            v3 ldf = nb.pos - hp;
+            if (dot(ldf, ldf) > 225.0f) continue;
+          }
+          if (nb.age > (flag(F_ANIM) ? 2.0f : 30.0f * 0.8f) || tsx[j] < 0.03f) continue;  // 1743
+          combine(fr, nb, hp, hn, mat, tsy[j]);
+        }
+      }
+    }
+#else
     for (int i = 0; i < ns; i++) {
       float srx, sry;
       hash2(nc_addmul(sx, (float)i, 0.3f), nc_addmul(sy, (float)i, 0.4f), srx, sry);
@@ -1631,6 +1745,7 @@ struct Integrator {
         combine(fr, nb, hp, hn, mat, sry);
       }
     }
+#endif
     // finalizeReservoir, 1525-1576
     if (fr.ws <= 0.0f || fr.M <= 0.0f) {
       fr.W = 0.0f;

@@ -64,6 +64,11 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // per workgroup would cap a CU at three workgroups
   if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
   o << "#define RT0_BVH_WIDE " << k.bvh_wide << "\n";
+  // ReSTIR scenes without models fetch their reservoir taps two at a time
+  // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
+  // occupancy target below); with a BVH the extra registers cost more than
+  // the halved round trips save (C5 22.95 vs 18.39 ms), so 1 there
+  if (k.restir && s.n_models == 0) o << "#ifndef RT0_TAP_BATCH\n#define RT0_TAP_BATCH 2\n#endif\n";
   o << "using __hip_internal::int32_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
   o << strip_includes(rt0_jit_source_text);
   const int nt = s.n_total;
@@ -150,15 +155,16 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
   if (const char *w = getenv("RT0_JIT_WAVES_PER_EU"))  // tuning knob: occupancy target
     o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w) << "))) ";
-  // occupancy targets measured per kernel family (scripts/ab_configs.sh, ab_c5.sh):
-  // BVH traversal is load-latency bound -- C5 4096^2 129.9 ms (3 waves/SIMD:
-  // 131 VGPRs and a 48-entry LDS stack) -> 78.3 ms at 6; the ReSTIR kernel
-  // (C3) 9.71 -> 9.32 ms at 5; the quadric/SDF kernels already sit at <= 64
-  // VGPRs (8 waves) and are left alone
+  // occupancy targets measured per kernel family (scripts/ab_configs.sh, ab_c5.sh,
+  // gpu_ab_taps.sh): BVH traversal is load-latency bound -- C5 4096^2 129.9 ms
+  // (3 waves/SIMD: 131 VGPRs and a 48-entry LDS stack) -> 78.3 ms at 6; the
+  // ReSTIR kernel with batched taps at 4 (128 VGPRs; at 5 it spills: C3 0.85
+  // ms per pass, at 3 0.65, at 4 0.60); the quadric/SDF kernels already sit at
+  // <= 64 VGPRs (8 waves) and are left alone
   else if (s.n_models > 0)
     o << "__attribute__((amdgpu_waves_per_eu(6))) ";
   else if (k.restir)
-    o << "__attribute__((amdgpu_waves_per_eu(5))) ";
+    o << "__attribute__((amdgpu_waves_per_eu(4))) ";
   o << "void rt0_jit_pass(const LaunchParams P) {\n"
        "  rt0::pass_body<rt0::JitScene, rt0::JitCfg, "
     << (k.restir ? "true" : "false") << ", " << (k.vol ? "true" : "false") << ", " << (k.sdf ? "true" : "false")
