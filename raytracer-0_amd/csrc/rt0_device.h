@@ -71,6 +71,15 @@ struct BvhNode {
   float rz0, rx1, ry1, rz1;
   int32_t left, right, pad0, pad1;
 };
+// BvhNodeH 32 B: the same node with both child boxes in binary16, rounded
+// outward (min corners toward -inf, max corners toward +inf), so a box only
+// grows and the walk finds the same closest hit (RT0_BVH_HALF).  u[0..5] hold
+// the halves lx0 ly0 | lz0 lx1 | ly1 lz1 | rx0 ry0 | rz0 rx1 | ry1 rz1 (low |
+// high 16 bits), then the two links.
+struct BvhNodeH {
+  uint32_t u[6];
+  int32_t left, right;
+};
 // Bvh4Node 128 B (one L2 line): the 4-wide tree the host collapses from the
 // binary LBVH (rt0_host.cpp: collapse_bvh4).  Child boxes as SoA over the four
 // slots (mn.x[k] .. mx.z[k]); link[k] >= 0 internal node, < 0 leaf =
@@ -170,6 +179,7 @@ struct LaunchParams {
   // Triangle models: LBVH nodes (root 0) and triangles in leaf order; n_tris 0 = none.
   const BvhNode *bvh;
   const Bvh4Node *bvh4;  // the same tree collapsed 4-wide (RT0_BVH_WIDE)
+  const BvhNodeH *bvh16;  // the same nodes with binary16 boxes (RT0_BVH_HALF)
   const TriDev *tris;
   int32_t n_tris;
   // RENDER_MODE 1 (F_ANIM): the accumulator is an EMA with weight ema_alpha =

@@ -25,7 +25,8 @@ extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, 
                                          hipStream_t stream);
 extern "C" hipError_t rt0_launch_sum(const LaunchParams *p, dim3 grid, hipStream_t stream);
 extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_model, float3 lo, float3 hi,
-                                    BvhNode *d_nodes, TriDev *d_tris, int *depth_out, hipStream_t s);
+                                    BvhNode *d_nodes, BvhNodeH *d_hnodes, TriDev *d_tris, int *depth_out,
+                                    hipStream_t s);
 
 // A pass launch with fewer than kTargetWaves waves (16 per SIMD of the 1024
 // SIMDs) is frame-chunked up to kChunkWaves (measured on one 1/2/4/8-way band
@@ -57,6 +58,7 @@ struct rt0_ctx {
   bool bvh_dirty = false;
   BvhNode *d_bvh = nullptr;
   Bvh4Node *d_bvh4 = nullptr;  // the same tree collapsed 4-wide (collapse_bvh4)
+  BvhNodeH *d_bvh16 = nullptr;  // the binary nodes with binary16 boxes
   TriDev *d_tris = nullptr;
   int n_tris = 0, bvh_depth = 0;
   int bvh4_stack = 0;  // pushes bound of the 4-wide walk along any root-to-leaf path
@@ -193,6 +195,7 @@ void rt0_destroy(rt0_ctx *c) {
   if (c->d_cube) (void)hipFree(c->d_cube);
   if (c->d_bvh) (void)hipFree(c->d_bvh);
   if (c->d_bvh4) (void)hipFree(c->d_bvh4);
+  if (c->d_bvh16) (void)hipFree(c->d_bvh16);
   if (c->d_tris) (void)hipFree(c->d_tris);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -514,9 +517,11 @@ static int build_bvh(rt0_ctx *c) {
   const int n = (int)owner.size();
   if (c->d_bvh) HIPCHK(c, hipFree(c->d_bvh));
   if (c->d_bvh4) HIPCHK(c, hipFree(c->d_bvh4));
+  if (c->d_bvh16) HIPCHK(c, hipFree(c->d_bvh16));
   if (c->d_tris) HIPCHK(c, hipFree(c->d_tris));
   c->d_bvh = nullptr;
   c->d_bvh4 = nullptr;
+  c->d_bvh16 = nullptr;
   c->d_tris = nullptr;
   c->n_tris = 0;
   c->bvh_depth = 0;
@@ -527,12 +532,13 @@ static int build_bvh(rt0_ctx *c) {
   HIPCHK(c, hipMalloc(&d_v, v.size() * sizeof(float)));
   HIPCHK(c, hipMalloc(&d_owner, owner.size() * sizeof(int32_t)));
   HIPCHK(c, hipMalloc(&c->d_bvh, (size_t)std::max(1, n - 1) * sizeof(BvhNode)));
+  HIPCHK(c, hipMalloc(&c->d_bvh16, (size_t)std::max(1, n - 1) * sizeof(BvhNodeH)));
   HIPCHK(c, hipMalloc(&c->d_tris, (size_t)n * sizeof(TriDev)));
   HIPCHK(c, hipMemcpyAsync(d_v, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(d_owner, owner.data(), owner.size() * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   int depth = 0;
   hipError_t e = rt0_bvh_build(n, d_v, d_owner, make_float3(lo[0], lo[1], lo[2]), make_float3(hi[0], hi[1], hi[2]),
-                               c->d_bvh, c->d_tris, &depth, c->stream);
+                               c->d_bvh, c->d_bvh16, c->d_tris, &depth, c->stream);
   (void)hipFree(d_v);
   (void)hipFree(d_owner);
   if (e != hipSuccess) return fail(c, RT0_E_HIP, std::string("BVH build: ") + hipGetErrorString(e));
@@ -686,6 +692,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.cube_size = c->cube_size;
   p.bvh = c->d_bvh;
   p.bvh4 = c->d_bvh4;
+  p.bvh16 = c->d_bvh16;
   p.tris = c->d_tris;
   p.n_tris = c->n_tris;
   p.accum = c->acc();

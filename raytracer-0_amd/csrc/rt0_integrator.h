@@ -352,6 +352,11 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
 #ifndef RT0_LEAF_UNIFIED
 #define RT0_LEAF_UNIFIED 1
 #endif
+#ifndef RT0_BVH_HALF  // walk the binary16 copies of the nodes (BvhNodeH)
+#define RT0_BVH_HALF 0
+#endif
+DEV float h16_lo(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu)); }
+DEV float h16_hi(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)); }
 #ifndef RT0_LEAF_DEFER  // Aila-Laine style postponed leaf: A/B knob
 #define RT0_LEAF_DEFER 0
 #endif
@@ -442,11 +447,23 @@ DEV int bvh2_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, uns
   return best;
 #endif
   for (int guard = 2 * P.n_tris + 8; guard > 0; --guard) {
+#if RT0_BVH_HALF
+    // 32-B nodes with binary16 boxes rounded outward: half the bytes per
+    // visit, the same closest hit (a box only grows)
+    const uint4 *hn = reinterpret_cast<const uint4 *>(P.bvh16) + 2 * node;
+    const uint4 q0 = hn[0], q1 = hn[1];
+    float tl = box_enter(h16_lo(q0.x), h16_hi(q0.x), h16_lo(q0.y), h16_hi(q0.y), h16_lo(q0.z), h16_hi(q0.z), o, inv,
+                         tmin);
+    float tr = box_enter(h16_lo(q0.w), h16_hi(q0.w), h16_lo(q1.x), h16_hi(q1.x), h16_lo(q1.y), h16_hi(q1.y), o, inv,
+                         tmin);
+    int cl = (int)q1.z, cr = (int)q1.w;
+#else
     const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
     const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
     float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
     float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
     int cl = lk.x, cr = lk.y;
+#endif
     if (cnt) ++cnt[0];  // counting instance: nodes visited (two child boxes each)
 #if RT0_LEAF_UNIFIED
     // leaves are tested in place, left before right; the first leaf test of
