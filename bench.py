@@ -230,7 +230,10 @@ class Progressive:
 
 class Restir:
     """C3/C5: one pass per launch (frame-to-frame reservoir dependency); N>1:
-    contiguous row blocks + per-pass halo exchange + block gather."""
+    two round-robin row bands per rank (the sky rows of C3/C5 cost a fraction
+    of the geometry rows: contiguous blocks left the slowest of 8 ranks at
+    2.2-2.3x the mean, scripts/restir_shard_sim.py) + per-pass halo exchange
+    at each band boundary + band gather."""
 
     def __init__(self, rt0, torch, wl, rank, world, local):
         import rt0.shard as shard
@@ -243,16 +246,22 @@ class Restir:
         self.sh, self.gather = None, None
         dev = "cuda:%d" % local
         if world > 1:
-            self.sh = shard.RestirShard(self.r, rank, world, H, W, dev)
-            band = self.sh.band
+            band = shard.interleaved_band(H, world)
+            self.sh = shard.RestirShard(self.r, rank, world, H, W, dev, band=band)
             self.gather = shard.BandGather(H, W, rank, world, band, dev)
-            # full-size accumulator padded to world x band rows: the block of this
-            # rank is the gather's send buffer as it stands
-            self.acc = torch.zeros((world * band, W, 4), dtype=torch.float32, device=dev)
+            # full-size accumulator padded to whole bands; this rank's bands are
+            # packed into the gather's send buffer (one index_select per step,
+            # into a preallocated buffer)
+            nb = (H + band - 1) // band
+            self.acc = torch.zeros((nb * band, W, 4), dtype=torch.float32, device=dev)
             self.r.set_accum_buffer(self.acc.data_ptr())
-            lo, hi = shard.block_rows(rank, band, H)
-            self.send = self.acc[rank * band:(rank + 1) * band]
-            self.samples_per_step = (hi - lo) * W * self.spp
+            own = shard.owned_band_rows(rank, world, band, H)
+            rows = [y for lo, _ in own for y in range(lo, lo + band)]
+            self.rows = torch.tensor(rows, dtype=torch.long, device=dev)
+            # every rank's send buffer has the gather's row count (RCCL needs equal sizes)
+            self.send_buf = torch.zeros((self.gather.rows, W, 4), dtype=torch.float32, device=dev)
+            self.send = self.send_buf[:len(rows)]
+            self.samples_per_step = sum(hi - lo for lo, hi in own) * W * self.spp
         else:
             self.acc = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
             self.r.set_accum_buffer(self.acc.data_ptr())
@@ -274,7 +283,11 @@ class Restir:
         self.launches = n
         if self.gather is not None:
             t = time.perf_counter()
-            self.gather.gather(self.send)
+            if self.sh is not None:
+                self.torch.index_select(self.acc, 0, self.rows, out=self.send)
+                self.gather.gather(self.send_buf)
+            else:
+                self.gather.gather(self.send)
             self.torch.cuda.synchronize()
             self.gather_s.append(time.perf_counter() - t)
 

@@ -156,6 +156,10 @@ struct LaunchParams {
   // data (own block + exchanged halo); a bilinear fetch outside them bumps
   // *halo_miss (null when the whole image is local).
   int32_t valid_lo, valid_hi;
+  // halo_rows > 0: the shard owns the row bands b with b % n_shards == shard
+  // (several per shard when band * n_shards < height) and holds `halo_rows`
+  // exchanged rows on either side of each; a fetch elsewhere bumps *halo_miss
+  int32_t halo_rows;
   uint32_t *halo_miss;
   // Frame-chunked launch (few pixels per device, e.g. 8-way sharding): grid.z
   // = chunk index, each lane renders frames [z*frame_chunk, +frame_chunk) of

@@ -699,10 +699,16 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.compact = c->compact ? 1 : 0;
   p.counters = c->d_counters;
   p.ema_alpha = 1.0f / (float)c->temporal_frames;  // raytracer.glsl:2164
-  if (c->n_shards > 1) {  // one contiguous block per shard (checked for ReSTIR in render_impl)
+  p.halo_rows = 0;
+  if (c->n_shards > 1 && (long)c->band * c->n_shards >= c->H) {  // one contiguous block per shard
     const int lo = c->shard * c->band, hi = std::min(c->H, lo + c->band);
     p.valid_lo = std::max(0, lo - c->halo);
     p.valid_hi = std::min(c->H, hi + c->halo);
+    p.halo_miss = c->d_halo_miss;
+  } else if (c->n_shards > 1) {  // several bands per shard, dealt round-robin
+    p.valid_lo = 0;
+    p.valid_hi = c->H;
+    p.halo_rows = std::max(1, c->halo);
     p.halo_miss = c->d_halo_miss;
   } else {
     p.valid_lo = 0;
@@ -725,11 +731,12 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   if (!c->has_scene) return fail(c, RT0_E_STATE, "rt0_render before rt0_set_scene*");
   const bool restir = (c->cfg.defines & RT0_USE_RESTIR) != 0;
   // ReSTIR reads neighbouring pixels of the previous passes' reservoirs: a
-  // shard must own one contiguous row block, whose halo the caller exchanges
-  // between passes (rt0_device_restir; rt0/shard.py)
-  if (restir && c->n_shards > 1 && c->band * c->n_shards < c->H)
-    return fail(c, RT0_E_UNSUPPORTED, "ReSTIR sharding needs one contiguous row block per shard "
-                                      "(band_rows * n_shards >= height)");
+  // shard owns one contiguous row block or several round-robin bands, whose
+  // halo rows the caller exchanges between passes (rt0_device_restir;
+  // rt0/shard.py); a halo reaches into the neighbouring bands only
+  if (restir && c->n_shards > 1 && (long)c->band * c->n_shards < c->H && c->halo > c->band)
+    return fail(c, RT0_E_UNSUPPORTED, "ReSTIR sharding over round-robin bands needs halo <= band_rows (" +
+                                          std::to_string(c->halo) + " > " + std::to_string(c->band) + ")");
   if (restir && c->n_shards > 1 && n > 1)
     return fail(c, RT0_E_ARG, "sharded ReSTIR renders one pass per call (halo exchange between passes)");
   // a band-packed caller buffer holds exactly the rows of the shard it was set

@@ -1476,6 +1476,16 @@ struct Integrator {
     }
     return true;
   }
+  // Sharded ReSTIR: does this shard hold reservoir row y (an own band, or
+  // within halo_rows of one: the rows the exchange brings in)?
+  DEV bool row_local(int y) const {
+    if (P.halo_rows <= 0) return y >= P.valid_lo && y < P.valid_hi;
+    const int b = y / P.band, off = y - b * P.band;
+    const bool own = b % P.n_shards == P.shard;
+    const bool below = b > 0 && (b - 1) % P.n_shards == P.shard && off < P.halo_rows;
+    const bool above = (b + 1) % P.n_shards == P.shard && off >= P.band - P.halo_rows;
+    return own || below || above;
+  }
   // GL LINEAR + CLAMP_TO_EDGE fetch of an RGBA32F plane (index.js:660-664)
   DEV float4 tex2d(const float4 *__restrict__ t, float u, float v) {
 #pragma clang fp contract(off)
@@ -1486,7 +1496,7 @@ struct Integrator {
     int x1 = min(max(x0 + 1, 0), P.width - 1), y1 = min(max(y0 + 1, 0), P.height - 1);
     x0 = min(max(x0, 0), P.width - 1);
     y0 = min(max(y0, 0), P.height - 1);
-    if (P.halo_miss && (y0 < P.valid_lo || y1 >= P.valid_hi)) atomicAdd(P.halo_miss, 1u);
+    if (P.halo_miss && !(row_local(y0) && row_local(y1))) atomicAdd(P.halo_miss, 1u);
     float4 t00 = t[(size_t)y0 * P.width + x0], t10 = t[(size_t)y0 * P.width + x1];
     float4 t01 = t[(size_t)y1 * P.width + x0], t11 = t[(size_t)y1 * P.width + x1];
     return bil_lerp(t00, t10, t01, t11, a, b);
@@ -1520,7 +1530,7 @@ struct Integrator {
     int x1 = min(max(x0 + 1, 0), P.width - 1), y1 = min(max(y0 + 1, 0), P.height - 1);
     x0 = min(max(x0, 0), P.width - 1);
     y0 = min(max(y0, 0), P.height - 1);
-    if (count && P.halo_miss && (y0 < P.valid_lo || y1 >= P.valid_hi)) atomicAdd(P.halo_miss, 1u);
+    if (count && P.halo_miss && !(row_local(y0) && row_local(y1))) atomicAdd(P.halo_miss, 1u);
     r.i00 = (uint32_t)(y0 * P.width + x0);
     r.i10 = (uint32_t)(y0 * P.width + x1);
     r.i01 = (uint32_t)(y1 * P.width + x0);

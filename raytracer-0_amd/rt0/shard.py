@@ -119,13 +119,17 @@ class BandGather:
 # ------------------------------------------------------------- sharded ReSTIR
 # ReSTIR's spatial pass reads the previous pass's reservoirs up to ~16 px away
 # (raytracer.glsl:1726-1760) and the temporal pass reads the history at a
-# reprojected position (1485-1523), so a ReSTIR shard owns ONE contiguous row
-# block (band_rows = block height) and, after every pass, swaps `halo` rows of
-# the newest reservoir planes with the shards above and below: one point-to-
-# point exchange per pass, 2 x halo x W x 32 B per neighbour.  The
-# history planes are earlier "newest" planes, so their halos are already in
-# place.  librt0 counts any fetch outside block + halo (Renderer.halo_misses):
-# zero means the sharded render equals the unsharded one bit for bit.
+# reprojected position (1485-1523).  A ReSTIR shard owns the row bands b with
+# b % world == rank: ONE contiguous block when band = block_band(H, world), or
+# several bands dealt round-robin (interleaved_band) so that the expensive
+# rows of a scene are spread over all ranks.  After every pass each band
+# boundary between two ranks swaps `halo` rows of the newest reservoir planes
+# (halo <= band, so a halo reaches into the neighbouring band only): one
+# batched point-to-point exchange per pass, 2 x halo x W x 32 B per boundary
+# (SURVEY 8e).  The history planes are earlier "newest" planes, so their halos
+# are already in place.  librt0 counts any fetch outside the own bands + halo
+# (Renderer.halo_misses): zero means the sharded render equals the unsharded
+# one bit for bit.
 
 def block_band(height, world):
     """Rows per shard for contiguous blocks: ceil(H / world) rounded up to the
@@ -133,30 +137,52 @@ def block_band(height, world):
     return ((height + world - 1) // world + 15) // 16 * 16
 
 
+def interleaved_band(height, world, per_rank=2, halo=24):
+    """Band height for `per_rank` round-robin bands per shard: the load balance
+    of a scene whose cost varies by row (sky vs geometry) against one halo
+    exchange per band boundary.  At least 2 x `halo` rows (the halos of a
+    band's two boundaries stay within the neighbouring band and do not
+    overlap) and a multiple of 16."""
+    b = block_band(height, world * per_rank)
+    return max(b, (2 * halo + 15) // 16 * 16)
+
+
 def block_rows(rank, band, height):
+    """Rows of the contiguous block of `rank` (band = block_band)."""
     lo = min(height, rank * band)
     return lo, min(height, lo + band)
 
 
+def owned_band_rows(rank, world, band, height):
+    """[(lo, hi)] of the bands of `rank`, top to bottom in row order."""
+    nb = (height + band - 1) // band
+    return [(b * band, min(height, (b + 1) * band)) for b in range(rank, nb, world)]
+
+
 def halo_plan(rank, world, band, height, halo):
     """Point-to-point transfers of one halo exchange for `rank`:
-    [("send"|"recv", peer, row0, row1)].  Every send has the matching recv on
-    the peer with the same row count."""
-    lo, hi = block_rows(rank, band, height)
-    if lo >= hi or halo <= 0:
+    [("send"|"recv", peer, row0, row1)], band boundaries in row order, so that
+    the transfers between any two ranks are posted in the same order on both
+    sides.  Every send has the matching recv on the peer with the same rows."""
+    if halo <= 0 or world <= 1:
         return []
     if halo > band:
-        raise ValueError("halo (%d rows) larger than a shard's block (%d rows)" % (halo, band))
+        raise ValueError("halo (%d rows) larger than a shard's band (%d rows)" % (halo, band))
+    nb = (height + band - 1) // band
     plan = []
-    if rank > 0:
-        plo, phi = block_rows(rank - 1, band, height)
-        plan.append(("send", rank - 1, lo, lo + min(halo, hi - lo)))
-        plan.append(("recv", rank - 1, lo - min(halo, phi - plo), lo))
-    if rank < world - 1:
-        nlo, nhi = block_rows(rank + 1, band, height)
-        if nlo < nhi:
-            plan.append(("send", rank + 1, hi - min(halo, hi - lo), hi))
-            plan.append(("recv", rank + 1, hi, hi + min(halo, nhi - nlo)))
+    for b in range(nb - 1):  # the boundary between bands b and b + 1, at row y
+        lower, upper = b % world, (b + 1) % world
+        if lower == upper or rank not in (lower, upper):
+            continue
+        y = (b + 1) * band
+        below = min(halo, band)  # rows of band b next to y
+        above = min(halo, min(height, y + band) - y)  # rows of band b + 1 next to y
+        if rank == lower:
+            plan.append(("send", upper, y - below, y))
+            plan.append(("recv", upper, y, y + above))
+        else:
+            plan.append(("recv", lower, y - below, y))
+            plan.append(("send", lower, y, y + above))
     return plan
 
 
@@ -192,11 +218,11 @@ class RestirShard:
     """One rank's sharded ReSTIR renderer state: torch-owned reservoir planes
     handed to librt0, so that the halo rows can be exchanged as tensors."""
 
-    def __init__(self, renderer, rank, world, height, width, device, halo=24):
+    def __init__(self, renderer, rank, world, height, width, device, halo=24, band=None):
         import torch
         self.r = renderer
         self.rank, self.world, self.halo = rank, world, halo
-        self.band = block_band(height, world)
+        self.band = band or block_band(height, world)  # default: one contiguous block
         self.planes = torch.zeros((8, height, width, 4), dtype=torch.float32, device=device)
         renderer.set_restir_buffers([self.planes[i].data_ptr() for i in range(8)])
         self.by_ptr = {self.planes[i].data_ptr(): i for i in range(8)}

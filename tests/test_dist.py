@@ -83,51 +83,71 @@ def test_gather_pads_a_partial_last_band():
     assert torch.equal(img, full)
 
 
-def test_halo_plan_pairs_sends_with_recvs():
+def _halo_cases():
+    """(H, world, band, halo): contiguous blocks (band = block_band) and
+    round-robin bands (interleaved_band, several per rank)."""
     for H, world, halo in ((96, 3, 24), (1080, 8, 24), (40, 3, 16), (64, 8, 16)):
-        band = shard.block_band(H, world)
+        yield H, world, shard.block_band(H, world), halo
+    for H, world, halo in ((192, 2, 24), (1080, 8, 24), (4096, 8, 24), (200, 3, 16), (1080, 3, 24)):
+        yield H, world, shard.interleaved_band(H, world, halo=halo), halo
+
+
+def test_halo_plan_pairs_sends_with_recvs():
+    for H, world, band, halo in _halo_cases():
         plans = {r: shard.halo_plan(r, world, band, H, min(halo, band)) for r in range(world)}
         for r, plan in plans.items():
+            own = shard.owned_band_rows(r, world, band, H)
             for kind, peer, r0, r1 in plan:
                 other = "recv" if kind == "send" else "send"
-                match = [p for p in plans[peer] if p[0] == other and p[1] == r]
-                assert len(match) == 1 and match[0][3] - match[0][2] == r1 - r0
-                lo, hi = shard.block_rows(r, band, H)
+                # the transfers between two ranks pair up in posting order
+                mine = [p[2:] for p in plan if p[0] == kind and p[1] == peer]
+                theirs = [p[2:] for p in plans[peer] if p[0] == other and p[1] == r]
+                assert mine == theirs
+                inside = [lo <= r0 < r1 <= hi for lo, hi in own]
                 if kind == "send":
-                    assert lo <= r0 < r1 <= hi  # only own rows leave a rank
+                    assert any(inside)  # only own rows leave a rank
                 else:
-                    assert r1 <= lo or r0 >= hi  # received rows are outside the own block
+                    assert all(r1 <= lo or r0 >= hi for lo, hi in own)  # received rows are not own rows
+            # every row within `halo` of an own band is own or received
+            got = set(y for lo, hi in own for y in range(lo, hi))
+            got |= set(y for k, _, r0, r1 in plan if k == "recv" for y in range(r0, r1))
+            need = set(y for lo, hi in own for y in range(max(0, lo - halo), min(H, hi + halo)))
+            assert need <= got, (H, world, band, halo, r)
 
 
-def _halo_worker(rank, world, port, H, W, halo, q):
+def _halo_worker(rank, world, port, H, W, halo, q, band=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        band = shard.block_band(H, world)
-        lo, hi = shard.block_rows(rank, band, H)
+        band = band or shard.block_band(H, world)
+        own = shard.owned_band_rows(rank, world, band, H)
         full = [_expected(H, W, band) + k * 1e6 for k in range(2)]
         planes = [torch.full_like(f, -1.0) for f in full]
         for p, f in zip(planes, full):
-            p[lo:hi] = f[lo:hi]
+            for lo, hi in own:
+                p[lo:hi] = f[lo:hi]
         shard.exchange_halo(planes, rank, world, band, halo)
-        vlo, vhi = max(0, lo - halo), min(H, hi + halo)
-        ok = all(torch.equal(p[vlo:vhi], f[vlo:vhi]) for p, f in zip(planes, full))
-        # rows beyond the halo are untouched
-        ok = ok and all(bool((p[:vlo] == -1).all()) and bool((p[vhi:] == -1).all()) for p in planes)
+        valid = torch.zeros(H, dtype=torch.bool)
+        for lo, hi in own:
+            valid[max(0, lo - halo):min(H, hi + halo)] = True
+        ok = all(torch.equal(p[valid], f[valid]) for p, f in zip(planes, full))
+        # rows beyond the halos are untouched
+        ok = ok and all(bool((p[~valid] == -1).all()) for p in planes)
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,H,halo", [(2, 64, 16), (3, 96, 24)])
-def test_restir_halo_exchange_over_gloo(world, H, halo):
+@pytest.mark.parametrize("world,H,halo,band", [(2, 64, 16, None), (3, 96, 24, None), (2, 192, 24, 48), (3, 200, 16, 32)])
+def test_restir_halo_exchange_over_gloo(world, H, halo, band):
     """The point-to-point halo exchange of sharded ReSTIR (the RCCL code path
-    on GPUs) delivers exactly the neighbours' rows on every rank."""
+    on GPUs) delivers exactly the neighbours' rows on every rank: contiguous
+    blocks (band None) and round-robin bands."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, H, 12, halo, q)) for r in range(world)]
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, H, 12, halo, q, band)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -199,10 +199,10 @@ def test_counters_feed_flop_model(cfgs, gpu_required):
     assert ok.mean() >= 0.99, ok.mean()
 
 
-def _restir_shards(cfgs, cfg, W, H, world, halo):
+def _restir_shards(cfgs, cfg, W, H, world, halo, band=None):
     import torch
     import rt0.shard as shard
-    band = shard.block_band(H, world)
+    band = band or shard.block_band(H, world)
     out = []
     for rank in range(world):
         r = rt0.Renderer(W, H)
@@ -252,6 +252,47 @@ def test_sharded_restir_matches_whole_image(cfgs, gpu_required, world, halo):
         assert r.halo_misses() == 0
     assert np.array_equal(img, ref)
     assert np.array_equal(main, ref_main)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_restir_round_robin_bands_match_whole_image(cfgs, gpu_required, world):
+    """ReSTIR over several round-robin row bands per shard (the bench's
+    load-balanced split, shard.interleaved_band) + the per-boundary halo
+    exchange == the unsharded render, bit for bit, through temporal passes."""
+    import torch
+    import rt0.shard as shard
+    cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
+    W, H, F, halo, band = 48, 192, 5, 24, 48
+    whole = rt0.Renderer(W, H)
+    rt0.configure(whole, cfg, cfgs)
+    for k in range(1, F + 1):
+        whole.render(k, 1)
+    ref = whole.read_accum()
+    ref_main, ref_aux = whole.read_restir(0)
+    shards, band = _restir_shards(cfgs, cfg, W, H, world, halo, band)
+
+    def newest(s):
+        r, planes, by_ptr = s
+        m, a = r.device_restir(0)
+        return [planes[by_ptr[m]], planes[by_ptr[a]]]
+
+    for k in range(1, F + 1):
+        for r, _, _ in shards:
+            r.render(k, 1)
+        shard.exchange_halo_local([newest(s) for s in shards], band, halo)
+        torch.cuda.synchronize()
+    img = np.zeros_like(ref)
+    main, aux = np.zeros_like(ref_main), np.zeros_like(ref_aux)
+    for rank, (r, _, _) in enumerate(shards):
+        own = shard.owned_band_rows(rank, world, band, H)
+        assert len(own) >= 1 and (world == 3 or len(own) == 2)
+        acc, (m, a) = r.read_accum(), r.read_restir(0)
+        for lo, hi in own:
+            img[lo:hi], main[lo:hi], aux[lo:hi] = acc[lo:hi], m[lo:hi], a[lo:hi]
+        assert r.halo_misses() == 0
+    assert np.array_equal(img, ref)
+    assert np.array_equal(main, ref_main)
+    assert np.array_equal(aux, ref_aux)
 
 
 def test_sharded_restir_reports_a_too_small_halo(cfgs, gpu_required):
