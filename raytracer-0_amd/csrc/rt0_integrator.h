@@ -1483,7 +1483,7 @@ struct Integrator {
     const int b = y / P.band, off = y - b * P.band;
     const bool own = b % P.n_shards == P.shard;
     const bool below = b > 0 && (b - 1) % P.n_shards == P.shard && off < P.halo_rows;
-    const bool above = (b + 1) % P.n_shards == P.shard && off >= P.band - P.halo_rows;
+    const bool above = (b + 1) * P.band < P.height && (b + 1) % P.n_shards == P.shard && off >= P.band - P.halo_rows;
     return own || below || above;
   }
   // GL LINEAR + CLAMP_TO_EDGE fetch of an RGBA32F plane (index.js:660-664)

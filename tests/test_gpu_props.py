@@ -295,6 +295,17 @@ def test_sharded_restir_round_robin_bands_match_whole_image(cfgs, gpu_required, 
     assert np.array_equal(aux, ref_aux)
 
 
+def test_round_robin_restir_reports_a_too_small_halo(cfgs, gpu_required):
+    """The kernel's halo check over round-robin bands: a 2-row halo is too
+    small for the ~16 px spatial taps, and every shard reports misses."""
+    cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
+    shards, band = _restir_shards(cfgs, cfg, 48, 192, 2, 2, band=48)
+    for k in range(1, 3):
+        for r, _, _ in shards:
+            r.render(k, 1)
+    assert all(r.halo_misses() > 0 for r, _, _ in shards)
+
+
 def test_sharded_restir_reports_a_too_small_halo(cfgs, gpu_required):
     import rt0.shard as shard
     cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
