@@ -228,3 +228,43 @@ def test_block_gather_reassembles_image(world, H):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=10) is True
+
+
+def _restir_gather_worker(rank, world, port, H, W, q):
+    """bench.py's Restir gather at N > 1: the rank's round-robin bands of a
+    full-size (band-padded) accumulator packed with one index_select into a
+    send buffer of the gather's row count, then BandGather."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        band = shard.interleaved_band(H, world)
+        nb = (H + band - 1) // band
+        full = _expected(H, W, band)
+        acc = torch.full((nb * band, W, 4), -1.0)
+        own = shard.owned_band_rows(rank, world, band, H)
+        for lo, hi in own:
+            acc[lo:hi] = full[lo:hi]
+        g = shard.BandGather(H, W, rank, world, band, "cpu")
+        rows = torch.tensor([y for lo, _ in own for y in range(lo, lo + band)], dtype=torch.long)
+        send_buf = torch.zeros((g.rows, W, 4))
+        torch.index_select(acc, 0, rows, out=send_buf[:len(rows)])
+        img = g.gather(send_buf)
+        q.put((rank, True if rank != 0 else bool(torch.equal(img, full))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H", [(2, 200), (3, 1080), (4, 512)])
+def test_restir_round_robin_gather_over_gloo(world, H):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_restir_gather_worker, args=(r, world, port, H, 6, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert all(res.values()), res
