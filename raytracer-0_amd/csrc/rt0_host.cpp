@@ -589,6 +589,7 @@ int rt0_set_camera(rt0_ctx *c, const float pos[3], const float lookat[3], const 
 int rt0_set_shard(rt0_ctx *c, int shard, int n_shards, int band_rows) {
   if (!c || n_shards < 1 || shard < 0 || shard >= n_shards || band_rows < 1) return RT0_E_ARG;
   if (band_rows % 16) return fail(c, RT0_E_ARG, "band_rows must be a multiple of 16");
+  if ((c->n_shards > 1) != (n_shards > 1)) c->jit_dirty = true;  // the halo check is compiled in or out
   c->shard = shard;
   c->n_shards = n_shards;
   c->band = band_rows;
@@ -784,6 +785,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     if (c->jit_dirty || !c->jit_fn) {
       rt0h::JitKey key = rt0h::make_jit_key(c->cfg, c->n_sdfs);
       if (c->exec_compat) key.flags |= F_EXEC_GHOST;
+      key.halo_check = c->n_shards > 1 ? 1 : 0;
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0)
                           ? (key.bvh_wide ? c->bvh4_stack : c->bvh_depth) + 1
                           : 0;

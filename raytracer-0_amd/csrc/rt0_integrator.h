@@ -87,6 +87,13 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_OPQ
 #define RT0_OPQ 0
 #endif
+// The sharded-ReSTIR halo check of every reservoir tap (row_local).  The
+// scene-specialised kernels of unsharded renders are compiled without it
+// (rt0_jit.cpp): its integer divisions cost the one-device C3 kernel 0.643 vs
+// 0.614 ms per pass even behind the null test of P.halo_miss.
+#ifndef RT0_HALO_CHECK
+#define RT0_HALO_CHECK 1
+#endif
 // ReSTIR reservoir taps fetched per batch (temporal levels together, spatial
 // taps RT0_TAP_BATCH at a time); 1 = one tap at a time.  The scene-specialised
 // kernels of ReSTIR scenes without models use 2 (rt0_jit.cpp)
@@ -1496,7 +1503,7 @@ struct Integrator {
     int x1 = min(max(x0 + 1, 0), P.width - 1), y1 = min(max(y0 + 1, 0), P.height - 1);
     x0 = min(max(x0, 0), P.width - 1);
     y0 = min(max(y0, 0), P.height - 1);
-    if (P.halo_miss && !(row_local(y0) && row_local(y1))) atomicAdd(P.halo_miss, 1u);
+    if (RT0_HALO_CHECK && P.halo_miss && !(row_local(y0) && row_local(y1))) atomicAdd(P.halo_miss, 1u);
     float4 t00 = t[(size_t)y0 * P.width + x0], t10 = t[(size_t)y0 * P.width + x1];
     float4 t01 = t[(size_t)y1 * P.width + x0], t11 = t[(size_t)y1 * P.width + x1];
     return bil_lerp(t00, t10, t01, t11, a, b);
@@ -1530,7 +1537,7 @@ struct Integrator {
     int x1 = min(max(x0 + 1, 0), P.width - 1), y1 = min(max(y0 + 1, 0), P.height - 1);
     x0 = min(max(x0, 0), P.width - 1);
     y0 = min(max(y0, 0), P.height - 1);
-    if (count && P.halo_miss && !(row_local(y0) && row_local(y1))) atomicAdd(P.halo_miss, 1u);
+    if (RT0_HALO_CHECK && count && P.halo_miss && !(row_local(y0) && row_local(y1))) atomicAdd(P.halo_miss, 1u);
     r.i00 = (uint32_t)(y0 * P.width + x0);
     r.i10 = (uint32_t)(y0 * P.width + x1);
     r.i01 = (uint32_t)(y1 * P.width + x0);

@@ -19,6 +19,7 @@ struct JitKey {
   bool restir, vol, sdf, spectral;
   int bvh_stack = 0;  // LDS traversal stack entries (push bound + 1) when the scene has models
   int bvh_wide = 0;   // RT0_BVH_WIDE of the generated kernel (4-wide or binary walk)
+  int halo_check = 1;  // RT0_HALO_CHECK: sharded launches count reservoir fetches outside the halo
 };
 
 std::string jit_source(const SceneDev &s, const JitKey &k);
