@@ -19,12 +19,17 @@ runs under it; WORLD_SIZE must equal --gpus.  One process per GPU:
     straight into a band-packed torch buffer (rt0_set_accum_buffer_compact:
     the RCCL send buffer as it stands), and rank 0 gathers the bands over RCCL
     into one preallocated buffer and reorders them with one index_copy_;
-  * ReSTIR workloads (C3, C5): one contiguous row block per rank, a halo
-    exchange of the newest reservoir planes after every pass (RCCL
-    point-to-point, rt0/shard.py: RestirShard), the block gather at the end
-    of the step.
-Both gathers are inside the timed region ("strong" scaling: total work fixed);
-rank 0's gather time is reported separately.
+  * ReSTIR workloads (C3, C5): two round-robin row bands per rank
+    (shard.interleaved_band), a halo exchange of the newest reservoir planes
+    at every band boundary after every pass (RCCL point-to-point,
+    rt0/shard.py: RestirShard), the band gather at the end of the step.
+librt0 launches on its own stream; it is ordered against torch's stream (the
+accumulator zeroing, the exchanges, the gather) with events, so a step makes
+one host synchronisation, at its end.  Both gathers are inside the timed
+region ("strong" scaling: total work fixed); rank 0's gather time is reported
+separately.  `--dist-backend gloo` stages every transfer through host memory:
+the one-GPU rehearsal of the N>1 path (all ranks on one device with
+RT0_BENCH_DEVICE=0, tests/test_bench_dist.py).
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
 `roofline` (VALU FP32: algorithmic FLOP/sample from SURVEY 8d x counted events,
@@ -47,7 +52,9 @@ sys.path.insert(0, os.path.join(HERE, "raytracer-0_amd"))
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
-PROFILE_ROUND = "r02/final"  # profiles/<dir>/ holding the PMC summaries (pmc_<config>.json) of each workload
+# profiles/<dir>/ holding the PMC summaries (pmc_<config>.json) of each
+# workload, newest first (scripts/gpu_measure.sh writes them)
+PROFILE_ROUNDS = ("r03", "r02/final")
 BAND = 16
 
 
@@ -192,7 +199,7 @@ def cpu_baseline_c(wl, budget_s=8.0):
 class Progressive:
     """C1/C2/C4: 16-row bands round-robin, band-packed accumulators, one gather."""
 
-    def __init__(self, rt0, torch, wl, rank, world, local):
+    def __init__(self, rt0, torch, wl, rank, world, local, staged=False):
         import rt0.shard as shard
         from rt0 import workloads
         self.torch, self.world = torch, world
@@ -203,7 +210,7 @@ class Progressive:
         self.gather = None
         if world > 1:
             self.r.set_shard(rank, world, BAND)
-            self.gather = shard.BandGather(H, W, rank, world, BAND, "cuda:%d" % local)
+            self.gather = shard.BandGather(H, W, rank, world, BAND, "cuda:%d" % local, staged=staged)
             self.acc = self.gather.acc
             rows = self.r.set_accum_buffer_compact(self.acc.data_ptr())
             assert rows <= self.acc.shape[0], (rows, self.acc.shape)
@@ -212,20 +219,28 @@ class Progressive:
             self.acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
             self.r.set_accum_buffer(self.acc.data_ptr())
             self.samples_per_step = W * H * self.spp
-        self.kernel_ms, self.gather_s, self.launches = [], [], 0
+        self.order = shard.StreamOrder(self.r, "cuda:%d" % local)
+        self.kernel_ms, self.gather_ms, self.launches = [], [], 0
+        self.image = None
 
     def step(self, i):
-        self.acc.zero_()
-        self.torch.cuda.synchronize()
-        self.r.render(1, self.spp)  # synchronous: returns after the kernels finished
+        self.acc.zero_()  # torch's stream
+        self.order.rt0_after_torch()
+        self.r.render_async(1, self.spp)  # librt0's stream
+        self.order.torch_after_rt0()
+        if self.gather is not None:
+            ev = self.order.begin_timing()
+            self.image = self.gather.gather()  # RCCL gather of the HDR bands + one reorder on rank 0
+            self.order.end_timing(ev)
+        self.r.sync()  # the step's one host synchronisation (kernel time of this render call)
         ms, n = self.r.last_kernel_ms()
         self.kernel_ms.append(ms)
         self.launches = n
         if self.gather is not None:
-            t = time.perf_counter()
-            self.gather.gather()  # RCCL gather of the HDR bands + one reorder on rank 0
-            self.torch.cuda.synchronize()
-            self.gather_s.append(time.perf_counter() - t)
+            self.gather_ms.append(self.order.elapsed_ms())
+
+    def final_image(self):
+        return self.acc if self.world == 1 else self.image
 
 
 class Restir:
@@ -235,7 +250,7 @@ class Restir:
     2.2-2.3x the mean, scripts/restir_shard_sim.py) + per-pass halo exchange
     at each band boundary + band gather."""
 
-    def __init__(self, rt0, torch, wl, rank, world, local):
+    def __init__(self, rt0, torch, wl, rank, world, local, staged=False):
         import rt0.shard as shard
         from rt0 import workloads
         self.torch, self.world = torch, world
@@ -245,10 +260,11 @@ class Restir:
         self.spp = wl["spp"]
         self.sh, self.gather = None, None
         dev = "cuda:%d" % local
+        self.order = shard.StreamOrder(self.r, dev)
         if world > 1:
             band = shard.interleaved_band(H, world)
-            self.sh = shard.RestirShard(self.r, rank, world, H, W, dev, band=band)
-            self.gather = shard.BandGather(H, W, rank, world, band, dev)
+            self.sh = shard.RestirShard(self.r, rank, world, H, W, dev, band=band, staged=staged, order=self.order)
+            self.gather = shard.BandGather(H, W, rank, world, band, dev, staged=staged)
             # full-size accumulator padded to whole bands; this rank's bands are
             # packed into the gather's send buffer (one index_select per step,
             # into a preallocated buffer)
@@ -266,43 +282,64 @@ class Restir:
             self.acc = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
             self.r.set_accum_buffer(self.acc.data_ptr())
             self.samples_per_step = W * H * self.spp
-        self.kernel_ms, self.gather_s, self.launches = [], [], 0
+        self.kernel_ms, self.gather_ms, self.launches = [], [], 0
+        self.image = None
 
     def step(self, i):
         first = 1 + i * self.spp
         if self.sh is None:
-            self.r.render(first, self.spp)
+            self.r.render(first, self.spp)  # one call, spp launches, synchronous
             ms, n = self.r.last_kernel_ms()
         else:
-            ms, n = 0.0, 0
-            for k in range(first, first + self.spp):
-                self.sh.render(k, 1)
-                m, l = self.r.last_kernel_ms()
-                ms, n = ms + m, n + l
+            self.sh.render(first, self.spp)  # async passes, halo exchanges event-ordered
+            ev = self.order.begin_timing()
+            self.torch.index_select(self.acc, 0, self.rows, out=self.send)
+            self.image = self.gather.gather(self.send_buf)
+            self.order.end_timing(ev)
+            self.r.sync()
+            # the last pass's kernel time (the timing events of earlier async
+            # passes are overwritten): ReSTIR pass times are flat over frames
+            m, _ = self.r.last_kernel_ms()
+            ms, n = m * self.spp, self.spp
+            self.gather_ms.append(self.order.elapsed_ms())
         self.kernel_ms.append(ms)
         self.launches = n
-        if self.gather is not None:
-            t = time.perf_counter()
-            if self.sh is not None:
-                self.torch.index_select(self.acc, 0, self.rows, out=self.send)
-                self.gather.gather(self.send_buf)
-            else:
-                self.gather.gather(self.send)
-            self.torch.cuda.synchronize()
-            self.gather_s.append(time.perf_counter() - t)
+
+    def final_image(self):
+        return self.acc[:self.r.height] if self.world == 1 else self.image
 
 
-def count_events(rt0, wl, local):
-    """Event counts of the same workload (separate counting kernel instance, a
-    fresh whole-image renderer, outside the timed region)."""
+def count_events(rt0, wl, local, first_timed, compat=False):
+    """Event counts of the timed workload (separate counting kernel instance, a
+    fresh whole-image renderer, outside the timed region).  ReSTIR workloads
+    count the frames of the first timed step: the chain is rendered up to it
+    uncounted (temporal taps start at frame 3, spatial taps are halved below
+    frame 10, raytracer.glsl:1660, 1726), then the step's frames are counted."""
     from rt0 import workloads
     r = rt0.Renderer(wl["width"], wl["height"], device=local)
     workloads.configure(r, wl)
-    r.set_counting(True)
-    r.render(1, min(wl["spp"], 8) if workloads.restir(wl) else wl["spp"])
+    r.set_executor_compat(compat)
+    if workloads.restir(wl):
+        if first_timed > 1:
+            r.render(1, first_timed - 1)
+        r.set_counting(True)
+        r.render(first_timed, wl["spp"])
+    else:
+        r.set_counting(True)
+        r.render(1, wl["spp"])
     cnt = r.counters()
     r.close()
     return cnt
+
+
+def pmc_summary(config):
+    """(path, summary) of the newest committed rocprofv3 PMC passes of this
+    workload (scripts/gpu_measure.sh -> scripts/pmc_summary.py)."""
+    for rd in PROFILE_ROUNDS:
+        path = os.path.join(HERE, "profiles", rd, "pmc_%s.json" % config)
+        if os.path.exists(path):
+            return "profiles/%s/pmc_%s.json" % (rd, config), json.load(open(path))
+    return None, None
 
 
 def main():
@@ -314,6 +351,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--secondary", action="store_true", help="also time the MAX_DIFF_BOUNCES=4 variant of c2")
     ap.add_argument("--jit", type=int, default=1, help="1: scene-specialised kernels (default), 0: ahead-of-time")
+    ap.add_argument("--executor-compat", action="store_true",
+                    help="rt0_set_executor_compat(1): the reference executor's reservoir stores (ReSTIR workloads)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N>1: nccl = RCCL over xGMI; gloo = every transfer staged through host memory")
+    ap.add_argument("--save-image", default=None, help="rank 0: np.save the last step's HDR image (H x W x 4)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -322,7 +364,8 @@ def main():
     if world != args.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RT0_BENCH_DEVICE pins every rank to one device (the one-GPU rehearsal)
+    local = int(os.environ.get("RT0_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
     import numpy as np
     import torch
@@ -331,18 +374,20 @@ def main():
 
     wl = workloads.get(args.config)
     dist = None
+    staged = args.dist_backend == "gloo"
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL on ROCm
+        dist.init_process_group(args.dist_backend)  # "nccl" = RCCL on ROCm
     W, H = wl["width"], wl["height"]
 
-    job = (Restir if workloads.restir(wl) else Progressive)(rt0, torch, wl, rank, world, local)
+    job = (Restir if workloads.restir(wl) else Progressive)(rt0, torch, wl, rank, world, local, staged=staged)
     job.r.set_jit(bool(args.jit))
+    job.r.set_executor_compat(args.executor_compat)
     for i in range(args.warmup):
         job.step(i)
     job.kernel_ms.clear()
-    job.gather_s.clear()
+    job.gather_ms.clear()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -354,7 +399,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], device="cuda:%d" % local)
+        t = torch.tensor([dt], device="cuda:%d" % local) if not staged else torch.tensor([dt])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt * 1000.0 / args.steps
@@ -364,32 +409,46 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
+    if args.save_image:
+        np.save(args.save_image, job.final_image().cpu().numpy()[:H])
 
-    cnt = count_events(rt0, wl, local)
+    first_timed = 1 + args.warmup * wl["spp"]
+    cnt = count_events(rt0, wl, local, first_timed, args.executor_compat)
     fps = flop_per_sample(cnt, wl)
     kern_s = float(np.mean(job.kernel_ms)) / 1000.0  # all launches of one step on rank 0
     achieved_tflops = fps * job.samples_per_step / kern_s / 1e12
-    # HBM traffic per launch from the committed rocprofv3 PMC passes of this
-    # workload (scripts/gpu_pmc.sh -> scripts/pmc_traffic.py; FETCH_SIZE x2
-    # gfx950 correction); counters cannot be read from inside this process
-    traffic, pmc = None, None
-    pmc_path = os.path.join(HERE, "profiles", PROFILE_ROUND, "pmc_%s.json" % args.config)
-    if world == 1 and os.path.exists(pmc_path):
-        pmc = json.load(open(pmc_path))
-        traffic = pmc["traffic_bytes_per_launch"]
     per_launch = max(1, job.launches)
     kern_launch_s = kern_s / per_launch
+    # algorithmic HBM bytes per launch: one float4 accumulator read +
+    # write per pixel (32 B); a ReSTIR pass also writes the two reservoir MRTs
+    # and reads the six input planes once (+128 B)
+    # (a ReSTIR launch is one pass over the pixels, a progressive launch every
+    # pass of the step: either way pixels x bpp)
+    bpp = 160.0 if workloads.restir(wl) else 32.0
+    alg_bytes = bpp * job.samples_per_step / wl["spp"]
+    # HBM traffic per launch from the committed rocprofv3 PMC passes of this
+    # workload (FETCH_SIZE x2 gfx950 correction); counters cannot be read from
+    # inside this process
+    pmc_path, pmc = pmc_summary(args.config) if world == 1 else (None, None)
+    traffic = pmc["traffic_bytes_per_launch"] if pmc else None
     roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-            "traffic_unit": "bytes/launch",
-            "traffic_source": ("profiles/%s/pmc_%s.json" % (PROFILE_ROUND, args.config)) if pmc else None,
+            "traffic_unit": "bytes/launch", "traffic_source": pmc_path,
+            "algorithmic_bytes": alg_bytes,
+            "algorithmic_gbs": round(alg_bytes / kern_launch_s / 1e9, 1),
+            "hbm_gbs": round(traffic / kern_launch_s / 1e9, 1) if traffic else None,
+            "hbm_peak_gbs": PEAK_HBM_GBS,
+            "hbm_frac": round(traffic / kern_launch_s / 1e9 / PEAK_HBM_GBS, 4) if traffic else None,
             "flop_per_sample": round(fps, 1),
             "events_per_sample": {k: round(cnt[k] / max(1, cnt["samples"]), 3) for k in cnt if k != "samples"},
+            "events_window": ("frames %d..%d (the first timed step)" % (first_timed, first_timed + wl["spp"] - 1))
+            if workloads.restir(wl) else "frames 1..%d (every step)" % wl["spp"],
             "kernel_ms_per_step": round(kern_s * 1000.0, 3),
             "launches_per_step": job.launches,
             "kernel_ms_per_launch": round(kern_launch_s * 1000.0, 3),
             "note": "FP32 vector kernel (no MFMA): peak = MI355X FP32 vector 157.3 TF; FLOP model SURVEY 8d x "
-                    "counted events (counting instance, whole image); achieved over rank 0's kernel time"}
+                    "counted events (counting instance, whole image); achieved over rank 0's kernel time (HIP "
+                    "events on librt0's stream); hbm_gbs = PMC traffic per launch over the same kernel time"}
     if pmc and "valu" in pmc:
         roof["valu_lane_utilisation"] = round(pmc.get("valu_lane_utilisation", 0.0), 4)
         # wave64 VALU instruction = 2 SIMD cycles (transcendental 4,
@@ -415,12 +474,17 @@ def main():
         "config": {"workload": "%s (%s): %s" % (args.config, wl["fixture"], wl["doc"]),
                    "width": W, "height": H, "spp": wl["spp"], "max_diff_bounces": mdb,
                    "parallelism": ("row-band x%d (16-row bands)" % world) if not workloads.restir(wl)
-                   else ("row-block x%d + reservoir halo exchange" % world),
-                   "kernel": "scene-specialised (hipRTC JIT)" if args.jit else "ahead-of-time"},
+                   else ("round-robin row bands x%d + reservoir halo exchange" % world),
+                   "dist_backend": args.dist_backend if world > 1 else None,
+                   "kernel": "scene-specialised (hipRTC JIT)" if args.jit else "ahead-of-time",
+                   "executor_compat": bool(args.executor_compat)},
         "roofline": roof,
     }
-    if job.gather_s:
-        out["gather_ms_per_step"] = round(1000.0 * float(np.mean(job.gather_s)), 3)
+    if wl.get("baseline_spp") and wl["baseline_spp"] != wl["spp"]:
+        out["config"]["spp_note"] = ("BASELINE.md quotes this config at %d spp; one bench step renders %d passes "
+                                     "(Msamples/s is per sample either way)" % (wl["baseline_spp"], wl["spp"]))
+    if job.gather_ms:
+        out["gather_ms_per_step"] = round(float(np.mean(job.gather_ms)), 3)
     if args.secondary and args.config == "c2":
         sec = workloads.get("c2_refcaps")
         workloads.configure(job.r, sec)

@@ -580,13 +580,18 @@ static v3 cube_sample(const Oracle *o, v3 d) {
 }
 
 /* iTriangle, the reference's commented-out Moller-Trumbore (raytracer.glsl:
- * 864-892), evaluated as written (no FMA: -ffp-contract=off). */
+ * 864-892), evaluated as written (no FMA: -ffp-contract=off), except for the
+ * parallel-ray threshold: EPSILON * |e0| * |e1| instead of the absolute
+ * EPSILON (the determinant scales with the triangle's area; with the absolute
+ * test the C5 model's ~0.015-edge triangles are rejected at every angle).
+ * The product computes the same threshold per triangle (TriDev.eps). */
 static int iTriangle(const float *v, int cull, v3 o, v3 d, float tmin, float *t) {
   v3 v1 = V(v[0], v[1], v[2]), e0 = sub(V(v[3], v[4], v[5]), v1), e1 = sub(V(v[6], v[7], v[8]), v1);
   v3 h = cross(d, e1);
   float a = dot3(e0, h);
-  if (cull && a < EPSILON) return 0;
-  if (!cull && a > -EPSILON && a < EPSILON) return 0;
+  float eps = EPSILON * sqrtf(e0.x * e0.x + e0.y * e0.y + e0.z * e0.z) * sqrtf(e1.x * e1.x + e1.y * e1.y + e1.z * e1.z);
+  if (cull && a < eps) return 0;
+  if (!cull && a > -eps && a < eps) return 0;
   float f = 1.0f / a;
   v3 s = sub(o, v1);
   float u = f * dot3(s, h);

@@ -13,8 +13,7 @@
 //   4. k_refit    bottom-up boxes, one thread per leaf, the second thread to
 //                 reach a node (atomic counter) merges its children;
 //   5. k_pack     64-B BvhNodes (both child boxes in the parent: one fetch per
-//                 visited node tests two boxes), their 32-B binary16 copies
-//                 (boxes rounded outward) and 48-B TriDevs in leaf order;
+//                 visited node tests two boxes) and 48-B TriDevs in leaf order;
 //   6. k_depth    the deepest leaf, checked against the traversal stack.
 // All kernels are one pass over n elements: the build is HBM/latency bound and
 // takes well under a millisecond for 100k triangles.
@@ -128,22 +127,9 @@ __global__ void k_refit(int n, const float *__restrict__ v, const uint32_t *__re
   }
 }
 
-// binary16 bits of x rounded toward -inf (down) or +inf (up)
-__device__ uint32_t half_bits(float x, bool up) {
-  const _Float16 h = (_Float16)x;  // round to nearest even
-  uint32_t b = (uint32_t)__builtin_bit_cast(uint16_t, h);
-  const float back = (float)h;
-  if (!up && back > x) b = b == 0x0000u ? 0x8001u : ((b & 0x8000u) ? b + 1u : b - 1u);
-  if (up && back < x) b = b == 0x8000u ? 0x0001u : ((b & 0x8000u) ? b - 1u : b + 1u);
-  return b;
-}
-__device__ uint32_t half_pair(float lo, bool lo_up, float hi, bool hi_up) {
-  return half_bits(lo, lo_up) | (half_bits(hi, hi_up) << 16);
-}
-
 __global__ void k_pack(int n, const float *__restrict__ v, const int32_t *__restrict__ model,
                        const uint32_t *__restrict__ idx, const int2 *__restrict__ child, const Box *__restrict__ box,
-                       BvhNode *__restrict__ nodes, BvhNodeH *__restrict__ hnodes, TriDev *__restrict__ tris) {
+                       BvhNode *__restrict__ nodes, TriDev *__restrict__ tris) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   {  // triangle i in leaf order
@@ -161,18 +147,13 @@ __global__ void k_pack(int n, const float *__restrict__ v, const int32_t *__rest
     d.e1x = t[6] - t[0];
     d.e1y = t[7] - t[1];
     d.e1z = t[8] - t[2];
-    d.pad = 0.f;
+    d.eps = 0.001f * sqrtf(d.e0x * d.e0x + d.e0y * d.e0y + d.e0z * d.e0z) *
+            sqrtf(d.e1x * d.e1x + d.e1y * d.e1y + d.e1z * d.e1z);
     tris[i] = d;
   }
   if (n == 1 && i == 0) {  // a one-triangle tree: the root holds the leaf twice
     const Box b = box[0];
     nodes[0] = BvhNode{b.x0, b.y0, b.z0, b.x0, b.x1, b.y1, b.z1, b.y0, b.z0, b.x1, b.y1, b.z1, ~0, ~0, 0, 0};
-    BvhNodeH hd;
-    hd.u[0] = hd.u[3] = half_pair(b.x0, false, b.y0, false);
-    hd.u[1] = hd.u[4] = half_pair(b.z0, false, b.x1, true);
-    hd.u[2] = hd.u[5] = half_pair(b.y1, true, b.z1, true);
-    hd.left = hd.right = ~0;
-    hnodes[0] = hd;
     return;
   }
   if (i >= n - 1) return;
@@ -195,16 +176,6 @@ __global__ void k_pack(int n, const float *__restrict__ v, const int32_t *__rest
   nd.right = ch.y >= n - 1 ? ~(ch.y - (n - 1)) : ch.y;
   nd.pad0 = nd.pad1 = 0;
   nodes[i] = nd;
-  BvhNodeH hd;
-  hd.u[0] = half_pair(l.x0, false, l.y0, false);
-  hd.u[1] = half_pair(l.z0, false, l.x1, true);
-  hd.u[2] = half_pair(l.y1, true, l.z1, true);
-  hd.u[3] = half_pair(r.x0, false, r.y0, false);
-  hd.u[4] = half_pair(r.z0, false, r.x1, true);
-  hd.u[5] = half_pair(r.y1, true, r.z1, true);
-  hd.left = nd.left;
-  hd.right = nd.right;
-  hnodes[i] = hd;
 }
 
 __global__ void k_depth(int n, const int *__restrict__ parent, int *__restrict__ depth) {
@@ -221,11 +192,10 @@ __global__ void k_depth(int n, const int *__restrict__ parent, int *__restrict__
 }  // namespace
 
 // Build the LBVH of n world-space triangles (v: 9 floats each, model: owner
-// index) into caller-allocated nodes[max(1, n-1)] (and their binary16 copies
-// hnodes[max(1, n-1)]) and tris[n].  Returns the
+// index) into caller-allocated nodes[max(1, n-1)] and tris[n].  Returns the
 // tree depth (edges root -> deepest leaf) in *depth_out.
 extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_model, float3 lo, float3 hi,
-                                    BvhNode *d_nodes, BvhNodeH *d_hnodes, TriDev *d_tris, int *depth_out,
+                                    BvhNode *d_nodes, TriDev *d_tris, int *depth_out,
                                     hipStream_t s) {
   if (n <= 0) return hipErrorInvalidValue;
   const float3 ext = make_float3(hi.x - lo.x, hi.y - lo.y, hi.z - lo.z);
@@ -267,7 +237,7 @@ extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_mo
   hipLaunchKernelGGL(k_refit, dim3(G), dim3(B), 0, s, n, d_v, idx2, child, parent, box, flag);
   TRY(hipGetLastError());
   // (n == 1: leaf 0 and the root share combined index 0, so box[0] is the leaf box)
-  hipLaunchKernelGGL(k_pack, dim3(G), dim3(B), 0, s, n, d_v, d_model, idx2, child, box, d_nodes, d_hnodes, d_tris);
+  hipLaunchKernelGGL(k_pack, dim3(G), dim3(B), 0, s, n, d_v, d_model, idx2, child, box, d_nodes, d_tris);
   TRY(hipGetLastError());
   hipLaunchKernelGGL(k_depth, dim3(G), dim3(B), 0, s, n, parent, depth);
   TRY(hipGetLastError());

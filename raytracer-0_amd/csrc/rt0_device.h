@@ -54,7 +54,8 @@ struct TexRec {
 // reference's commented-out iTriangle, 864-892).  One LBVH over the triangles
 // of all models, built on the device (rt0_bvh.hip) in world space:
 //   TriDev  48 B: v0 + model index, e0 = v1 - v0, e1 = v2 - v0 (the three
-//           Moller-Trumbore operands), stored in Morton (leaf) order;
+//           Moller-Trumbore operands) + the determinant threshold, stored in
+//           leaf order;
 //   BvhNode 64 B: both children's boxes + child links (>= 0 internal node,
 //           < 0 leaf ~triangle), so one node fetch tests two boxes.
 struct TriDev {
@@ -62,7 +63,8 @@ struct TriDev {
   int32_t model;  // owner model k (scene entry n_meshes + n_sdfs + k)
   float e0x, e0y, e0z;
   int32_t cull;   // Material.opts[3]: back-face culling (iTriangle, 869-872)
-  float e1x, e1y, e1z, pad;
+  float e1x, e1y, e1z;
+  float eps;      // EPSILON * |e0| * |e1|: iTriangle's parallel-ray threshold, scale-invariant
 };
 #define RT0_TRI_CULL_BIT (1 << 30)  // set in the build's model ids for culling models
 struct BvhNode {
@@ -71,30 +73,6 @@ struct BvhNode {
   float rz0, rx1, ry1, rz1;
   int32_t left, right, pad0, pad1;
 };
-// BvhNodeH 32 B: the same node with both child boxes in binary16, rounded
-// outward (min corners toward -inf, max corners toward +inf), so a box only
-// grows and the walk finds the same closest hit (RT0_BVH_HALF).  u[0..5] hold
-// the halves lx0 ly0 | lz0 lx1 | ly1 lz1 | rx0 ry0 | rz0 rx1 | ry1 rz1 (low |
-// high 16 bits), then the two links.
-struct BvhNodeH {
-  uint32_t u[6];
-  int32_t left, right;
-};
-// Bvh4Node 128 B (one L2 line): the 4-wide tree the host collapses from the
-// binary LBVH (rt0_host.cpp: collapse_bvh4).  Child boxes as SoA over the four
-// slots (mn.x[k] .. mx.z[k]); link[k] >= 0 internal node, < 0 leaf =
-// ~(first | (count - 1) << RT0_LEAF_SHIFT): triangles [first, first + count)
-// of the leaf order.  An empty slot holds the box (+inf)^3..(+inf)^3, which
-// no slab test enters.
-struct Bvh4Node {
-  float mnx[4], mny[4], mnz[4], mxx[4], mxy[4], mxz[4];
-  int32_t link[4];
-  int32_t pad[4];
-};
-#define RT0_LEAF_SHIFT 27  // leaf first index < 2^27, count <= 16
-#ifndef RT0_BVH_WIDE
-#define RT0_BVH_WIDE 0  // 1: walk the 4-wide tree (measured slower on C5); built only when selected
-#endif
 #ifndef RT0_BVH_STACK
 #define RT0_BVH_STACK 48  // traversal stack entries per lane (LDS); the build checks the bound
 #endif
@@ -167,10 +145,6 @@ struct LaunchParams {
   // to the accumulator in frame order (the same sequential sum).  samples ==
   // null: one chunk, accumulated in registers.
   int32_t frame_chunk;
-  // ReSTIR passes (one sample per pixel per launch): each wave owns a pool of
-  // 64*refill pixels (refill 8x8 blocks stacked in y) and a lane whose path
-  // ended takes the pool's next pixel; 1 = one pixel per lane
-  int32_t refill;
   float4 *samples;
   // Asset textures: RGBA8 texels (R in the low byte), row 0 = t 0; null =
   // unbound unit.
@@ -182,8 +156,6 @@ struct LaunchParams {
   int32_t cube_size;
   // Triangle models: LBVH nodes (root 0) and triangles in leaf order; n_tris 0 = none.
   const BvhNode *bvh;
-  const Bvh4Node *bvh4;  // the same tree collapsed 4-wide (RT0_BVH_WIDE)
-  const BvhNodeH *bvh16;  // the same nodes with binary16 boxes (RT0_BVH_HALF)
   const TriDev *tris;
   int32_t n_tris;
   // RENDER_MODE 1 (F_ANIM): the accumulator is an EMA with weight ema_alpha =

@@ -25,7 +25,7 @@ extern "C" hipError_t rt0_launch_tonemap(const float4 *acc, uchar4 *out, int n, 
                                          hipStream_t stream);
 extern "C" hipError_t rt0_launch_sum(const LaunchParams *p, dim3 grid, hipStream_t stream);
 extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_model, float3 lo, float3 hi,
-                                    BvhNode *d_nodes, BvhNodeH *d_hnodes, TriDev *d_tris, int *depth_out,
+                                    BvhNode *d_nodes, TriDev *d_tris, int *depth_out,
                                     hipStream_t s);
 
 // A pass launch with fewer than kTargetWaves waves (16 per SIMD of the 1024
@@ -33,8 +33,6 @@ extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_mo
 // shard of the 1024^2 bench image: 0.96 / 0.95 / 0.91 of linear for 2 / 4 / 8
 // shards, against 0.89 / 0.78 / 0.61 unchunked).
 static const long kTargetWaves = 16384;
-// Pixels per lane of a ReSTIR pass (LaunchParams::refill); RT0_REFILL overrides.
-static const int kRestirRefill = 1;  // measured: C3 R=2 0.796 vs 0.636 ms, C5 R=4 -3.5%
 static const long kChunkWaves = 65536;
 
 enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
@@ -57,11 +55,8 @@ struct rt0_ctx {
   std::vector<Model> models;
   bool bvh_dirty = false;
   BvhNode *d_bvh = nullptr;
-  Bvh4Node *d_bvh4 = nullptr;  // the same tree collapsed 4-wide (collapse_bvh4)
-  BvhNodeH *d_bvh16 = nullptr;  // the binary nodes with binary16 boxes
   TriDev *d_tris = nullptr;
   int n_tris = 0, bvh_depth = 0;
-  int bvh4_stack = 0;  // pushes bound of the 4-wide walk along any root-to-leaf path
   SceneDev *d_scene = nullptr;
   float cam_pos[3] = {0.f, 0.f, 2.8f}, cam_look[3] = {0.f, 0.f, -1.f}, cam_params[3] = {50.f, 0.f, 3.5f};
   float4 *d_accum = nullptr;
@@ -194,8 +189,6 @@ void rt0_destroy(rt0_ctx *c) {
     if (t) (void)hipFree(t);
   if (c->d_cube) (void)hipFree(c->d_cube);
   if (c->d_bvh) (void)hipFree(c->d_bvh);
-  if (c->d_bvh4) (void)hipFree(c->d_bvh4);
-  if (c->d_bvh16) (void)hipFree(c->d_bvh16);
   if (c->d_tris) (void)hipFree(c->d_tris);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -378,119 +371,13 @@ int rt0_set_model(rt0_ctx *c, int model, const float *positions, int n_vertices,
 }
 
 // World-space triangles of every TRIANGLE entry (instance k uses model k) ->
-// device LBVH (rt0_bvh.hip).  Runs at the first render after a scene/model
-// change.
-// RT0_BVH_LEAF=k lets the collapse turn subtrees of <= k triangles into leaves
-// (RT0_BVH_WIDE=0 selects the binary walk: rt0_jit.cpp make_jit_key).
-static int bvh_leaf_max() {
-  static const int k = getenv("RT0_BVH_LEAF") ? std::min(16, std::max(1, atoi(getenv("RT0_BVH_LEAF")))) : 1;
-  return k;
+// one BVH: the binned-SAH tree built on the host (rt0_bvh_sah.cpp, default) or
+// the device LBVH (rt0_bvh.hip; RT0_BVH_BUILD=lbvh).  Runs at the first render
+// after a scene/model change.
+static bool bvh_builder_sah() {
+  static const bool sah = !(getenv("RT0_BVH_BUILD") && std::string(getenv("RT0_BVH_BUILD")) == "lbvh");
+  return sah;
 }
-
-// Collapse the binary LBVH into the 4-wide tree of Bvh4Node (host side, once
-// per build: ~n/3 nodes, a few ms for 100k triangles).  Each 4-wide node starts
-// from a binary node's two children and repeatedly opens the child subtree of
-// largest surface area until it holds four slots; an internal child of at most
-// leaf_max triangles becomes a leaf range (a Karras subtree covers a contiguous
-// run of the leaf order).  Sibling nodes are stored consecutively.  Returns the
-// push bound of the walk: along any root-to-leaf path, the sum over nodes of
-// (internal children - 1).
-namespace {
-struct Bvh4Collapse {
-  struct Ch {
-    int link;  // binary link: >= 0 internal, < 0 ~leaf
-    float lo[3], hi[3];
-  };
-  const std::vector<BvhNode> &bn;
-  int leaf_max;
-  std::vector<int> size, first, last;
-  std::vector<Bvh4Node> out;
-
-  static Ch left(const BvhNode &n) { return Ch{n.left, {n.lx0, n.ly0, n.lz0}, {n.lx1, n.ly1, n.lz1}}; }
-  static Ch right(const BvhNode &n) { return Ch{n.right, {n.rx0, n.ry0, n.rz0}, {n.rx1, n.ry1, n.rz1}}; }
-  static float half_area(const Ch &c) {
-    const float x = c.hi[0] - c.lo[0], y = c.hi[1] - c.lo[1], z = c.hi[2] - c.lo[2];
-    return x * y + y * z + z * x;
-  }
-  int sz(int l) const { return l < 0 ? 1 : size[l]; }
-  int lo_leaf(int l) const { return l < 0 ? ~l : first[l]; }
-  int hi_leaf(int l) const { return l < 0 ? ~l : last[l]; }
-  void ranges(int i) {  // post-order; depth < RT0_BVH_STACK (checked before)
-    for (int l : {bn[i].left, bn[i].right})
-      if (l >= 0) ranges(l);
-    size[i] = sz(bn[i].left) + sz(bn[i].right);
-    first[i] = std::min(lo_leaf(bn[i].left), lo_leaf(bn[i].right));
-    last[i] = std::max(hi_leaf(bn[i].left), hi_leaf(bn[i].right));
-  }
-  int emit(int slot, std::vector<Ch> ch) {
-    while (ch.size() < 4) {
-      int best = -1;
-      float ba = -1.f;
-      for (int k = 0; k < (int)ch.size(); k++)
-        if (ch[k].link >= 0 && half_area(ch[k]) > ba) {
-          ba = half_area(ch[k]);
-          best = k;
-        }
-      if (best < 0) break;
-      const BvhNode &nd = bn[ch[best].link];
-      ch[best] = left(nd);
-      ch.insert(ch.begin() + best + 1, right(nd));
-    }
-    Bvh4Node n;
-    for (int k = 0; k < 4; k++) {
-      n.mnx[k] = n.mny[k] = n.mnz[k] = n.mxx[k] = n.mxy[k] = n.mxz[k] = INFINITY;  // empty: never entered
-      n.link[k] = -1;
-      n.pad[k] = 0;
-    }
-    std::vector<int> inner;  // slots holding 4-wide child nodes
-    for (int k = 0; k < (int)ch.size(); k++) {
-      const Ch &c = ch[k];
-      n.mnx[k] = c.lo[0];
-      n.mny[k] = c.lo[1];
-      n.mnz[k] = c.lo[2];
-      n.mxx[k] = c.hi[0];
-      n.mxy[k] = c.hi[1];
-      n.mxz[k] = c.hi[2];
-      if (c.link < 0) {
-        n.link[k] = c.link;  // ~triangle: a one-triangle range
-      } else if (size[c.link] <= leaf_max && last[c.link] - first[c.link] + 1 == size[c.link]) {
-        n.link[k] = ~(first[c.link] | ((size[c.link] - 1) << RT0_LEAF_SHIFT));
-      } else {
-        inner.push_back(k);
-      }
-    }
-    const int base = (int)out.size();
-    for (size_t j = 0; j < inner.size(); j++) n.link[inner[j]] = base + (int)j;
-    out.resize(base + inner.size());
-    out[slot] = n;
-    int sub = 0;
-    for (size_t j = 0; j < inner.size(); j++) {
-      const BvhNode &nd = bn[ch[inner[j]].link];
-      sub = std::max(sub, emit(base + (int)j, {left(nd), right(nd)}));
-    }
-    return inner.empty() ? 0 : (int)inner.size() - 1 + sub;
-  }
-};
-}  // namespace
-
-static int collapse_bvh4(const std::vector<BvhNode> &bn, int n_tris, int leaf_max, std::vector<Bvh4Node> &out) {
-  Bvh4Collapse C{bn, leaf_max, {}, {}, {}, {}};
-  C.out.resize(1);
-  int bound = 0;
-  if (n_tris == 1) {
-    const Bvh4Collapse::Ch leaf = Bvh4Collapse::left(bn[0]);  // the root holds leaf 0 twice (rt0_bvh.hip)
-    C.emit(0, {leaf});
-  } else {
-    C.size.assign(n_tris - 1, 0);
-    C.first.assign(n_tris - 1, 0);
-    C.last.assign(n_tris - 1, 0);
-    C.ranges(0);
-    bound = C.emit(0, {Bvh4Collapse::left(bn[0]), Bvh4Collapse::right(bn[0])});
-  }
-  out.swap(C.out);
-  return bound;
-}
-
 static int build_bvh(rt0_ctx *c) {
   c->bvh_dirty = false;
   std::vector<float> v;
@@ -516,50 +403,38 @@ static int build_bvh(rt0_ctx *c) {
   }
   const int n = (int)owner.size();
   if (c->d_bvh) HIPCHK(c, hipFree(c->d_bvh));
-  if (c->d_bvh4) HIPCHK(c, hipFree(c->d_bvh4));
-  if (c->d_bvh16) HIPCHK(c, hipFree(c->d_bvh16));
   if (c->d_tris) HIPCHK(c, hipFree(c->d_tris));
   c->d_bvh = nullptr;
-  c->d_bvh4 = nullptr;
-  c->d_bvh16 = nullptr;
   c->d_tris = nullptr;
   c->n_tris = 0;
   c->bvh_depth = 0;
-  c->bvh4_stack = 0;
   if (n == 0) return RT0_OK;
-  float *d_v = nullptr;
-  int32_t *d_owner = nullptr;
-  HIPCHK(c, hipMalloc(&d_v, v.size() * sizeof(float)));
-  HIPCHK(c, hipMalloc(&d_owner, owner.size() * sizeof(int32_t)));
   HIPCHK(c, hipMalloc(&c->d_bvh, (size_t)std::max(1, n - 1) * sizeof(BvhNode)));
-  HIPCHK(c, hipMalloc(&c->d_bvh16, (size_t)std::max(1, n - 1) * sizeof(BvhNodeH)));
   HIPCHK(c, hipMalloc(&c->d_tris, (size_t)n * sizeof(TriDev)));
-  HIPCHK(c, hipMemcpyAsync(d_v, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d_owner, owner.data(), owner.size() * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   int depth = 0;
-  hipError_t e = rt0_bvh_build(n, d_v, d_owner, make_float3(lo[0], lo[1], lo[2]), make_float3(hi[0], hi[1], hi[2]),
-                               c->d_bvh, c->d_bvh16, c->d_tris, &depth, c->stream);
-  (void)hipFree(d_v);
-  (void)hipFree(d_owner);
-  if (e != hipSuccess) return fail(c, RT0_E_HIP, std::string("BVH build: ") + hipGetErrorString(e));
+  if (bvh_builder_sah()) {
+    std::vector<BvhNode> nodes;
+    std::vector<TriDev> tris;
+    depth = rt0h::bvh_build_sah(n, v.data(), owner.data(), nodes, tris);
+    HIPCHK(c, hipMemcpy(c->d_bvh, nodes.data(), nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_tris, tris.data(), tris.size() * sizeof(TriDev), hipMemcpyHostToDevice));
+  } else {
+    float *d_v = nullptr;
+    int32_t *d_owner = nullptr;
+    HIPCHK(c, hipMalloc(&d_v, v.size() * sizeof(float)));
+    HIPCHK(c, hipMalloc(&d_owner, owner.size() * sizeof(int32_t)));
+    HIPCHK(c, hipMemcpyAsync(d_v, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d_owner, owner.data(), owner.size() * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    hipError_t e = rt0_bvh_build(n, d_v, d_owner, make_float3(lo[0], lo[1], lo[2]), make_float3(hi[0], hi[1], hi[2]),
+                                 c->d_bvh, c->d_tris, &depth, c->stream);
+    (void)hipFree(d_v);
+    (void)hipFree(d_owner);
+    if (e != hipSuccess) return fail(c, RT0_E_HIP, std::string("BVH build: ") + hipGetErrorString(e));
+  }
   if (depth >= RT0_BVH_STACK)
     return fail(c, RT0_E_UNSUPPORTED, "BVH depth " + std::to_string(depth) + " exceeds the traversal stack");
-  if (n >= (1 << RT0_LEAF_SHIFT))
-    return fail(c, RT0_E_UNSUPPORTED, "more than 2^27 triangles");
-  if (rt0h::bvh_wide_selected()) {  // the 4-wide tree, collapsed on the host from the binary one
-    std::vector<BvhNode> bn((size_t)std::max(1, n - 1));
-    HIPCHK(c, hipMemcpy(bn.data(), c->d_bvh, bn.size() * sizeof(BvhNode), hipMemcpyDeviceToHost));
-    std::vector<Bvh4Node> w;
-    const int bound = collapse_bvh4(bn, n, bvh_leaf_max(), w);
-    if (bound >= RT0_BVH_STACK)
-      return fail(c, RT0_E_UNSUPPORTED, "4-wide BVH stack bound " + std::to_string(bound) + " exceeds the traversal stack");
-    HIPCHK(c, hipMalloc(&c->d_bvh4, w.size() * sizeof(Bvh4Node)));
-    HIPCHK(c, hipMemcpy(c->d_bvh4, w.data(), w.size() * sizeof(Bvh4Node), hipMemcpyHostToDevice));
-    c->bvh4_stack = bound;
-    if (getenv("RT0_BVH_DEBUG"))
-      fprintf(stderr, "rt0 bvh: %d triangles, binary depth %d, %zu 4-wide nodes, 4-wide push bound %d\n", n, depth,
-              w.size(), bound);
-  }
+  if (getenv("RT0_BVH_DEBUG"))
+    fprintf(stderr, "rt0 bvh: %s build, %d triangles, depth %d\n", bvh_builder_sah() ? "sah" : "lbvh", n, depth);
   c->n_tris = n;
   c->bvh_depth = depth;
   c->jit_dirty = true;  // the scene-specialised kernel's traversal stack follows the depth
@@ -692,8 +567,6 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.cube = c->d_cube;
   p.cube_size = c->cube_size;
   p.bvh = c->d_bvh;
-  p.bvh4 = c->d_bvh4;
-  p.bvh16 = c->d_bvh16;
   p.tris = c->d_tris;
   p.n_tris = c->n_tris;
   p.accum = c->acc();
@@ -709,7 +582,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   } else if (c->n_shards > 1) {  // several bands per shard, dealt round-robin
     p.valid_lo = 0;
     p.valid_hi = c->H;
-    p.halo_rows = std::max(1, c->halo);
+    p.halo_rows = c->halo;  // >= 1 (render_impl)
     p.halo_miss = c->d_halo_miss;
   } else {
     p.valid_lo = 0;
@@ -738,6 +611,11 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   if (restir && c->n_shards > 1 && (long)c->band * c->n_shards < c->H && c->halo > c->band)
     return fail(c, RT0_E_UNSUPPORTED, "ReSTIR sharding over round-robin bands needs halo <= band_rows (" +
                                           std::to_string(c->halo) + " > " + std::to_string(c->band) + ")");
+  // the kernel's round-robin halo check (row_local) treats halo_rows rows of
+  // each neighbouring band as local: with no exchanged rows a bilinear tap into
+  // a neighbour's edge row would go uncounted
+  if (restir && c->n_shards > 1 && (long)c->band * c->n_shards < c->H && c->halo < 1)
+    return fail(c, RT0_E_ARG, "ReSTIR sharding over round-robin bands needs halo >= 1 (rt0_set_halo)");
   if (restir && c->n_shards > 1 && n > 1)
     return fail(c, RT0_E_ARG, "sharded ReSTIR renders one pass per call (halo exchange between passes)");
   // a band-packed caller buffer holds exactly the rows of the shard it was set
@@ -770,14 +648,6 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     return RT0_OK;
   }
   dim3 grid((p.vp_x1 - p.vp_x0 + 15) / 16, (p.vp_y1 - p.vp_y0 + 15) / 16);
-  // ReSTIR passes refill finished lanes from a per-wave pixel pool (pass_body):
-  // a workgroup then covers 16 x 16*refill launch rows
-  p.refill = 1;
-  if (restir && !c->counting) {
-    static const int refill = getenv("RT0_REFILL") ? std::max(1, atoi(getenv("RT0_REFILL"))) : kRestirRefill;
-    p.refill = refill;
-    grid.y = (p.vp_y1 - p.vp_y0 + 16 * refill - 1) / (16 * refill);
-  }
   // scene-specialised kernel (compiled once per scene/config, cached); the
   // counting instance is always the ahead-of-time one
   void *jit_fn = nullptr;
@@ -786,9 +656,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       rt0h::JitKey key = rt0h::make_jit_key(c->cfg, c->n_sdfs);
       if (c->exec_compat) key.flags |= F_EXEC_GHOST;
       key.halo_check = c->n_shards > 1 ? 1 : 0;
-      key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0)
-                          ? (key.bvh_wide ? c->bvh4_stack : c->bvh_depth) + 1
-                          : 0;
+      key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
       int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit_fn, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
       c->jit_dirty = false;

@@ -75,18 +75,12 @@ DEV float flog(float x) { return __logf(x); }
 // ----------------------------------------------- non-contracted arithmetic
 // Every helper below is evaluated exactly as the reference writes it (no FMA):
 // the RNG seeds feed a bit-level hash, so one fused a*b+c changes the whole
-// random stream.  `#pragma clang fp contract(off)` alone is not enough: with
-// -ffp-contract=fast, or with the ROCm 7.0 hipRTC that PyTorch bundles (and
-// that a process importing torch binds to), the backend fuses across it.  An
-// empty asm on the product makes it opaque, so no compiler can fuse it.
-// RT0_OPQ 1 additionally hides every product from the compiler (empty asm).
-// Off by default: under -ffp-contract=fast-honor-pragmas with the pinned
-// hipRTC the contract(off) pragmas alone keep the products unfused (every GPU
-// parity test is green either way), and the asm costs a v_mov + s_nop each:
-// 5.66 vs 5.80 ms per 64-spp C2 launch (profiles/r02/ab_c2knobs).
-#ifndef RT0_OPQ
-#define RT0_OPQ 0
-#endif
+// random stream.  The library and the JIT compile with
+// -ffp-contract=fast-honor-pragmas, under which the backend keeps every
+// product of a `#pragma clang fp contract(off)` block unfused (checked on the
+// gfx950 ISA; plain `fast` ignores the pragma in the backend).  Round 1 also
+// hid each such product behind an empty asm; that cost a v_mov + s_nop each
+// (5.66 vs 5.80 ms per 64-spp C2 launch) and was dropped in round 2.
 // The sharded-ReSTIR halo check of every reservoir tap (row_local).  The
 // scene-specialised kernels of unsharded renders are compiled without it
 // (rt0_jit.cpp): its integer divisions cost the one-device C3 kernel 0.643 vs
@@ -100,31 +94,24 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_TAP_BATCH
 #define RT0_TAP_BATCH 1
 #endif
-DEV float opq(float x) {
-#if RT0_OPQ
-  asm("" : "+v"(x));
-#endif
-  return x;
-}
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
-  x = opq(x);
   return x - floorf(x);
 }
 // a + b*c, unfused
 DEV float nc_addmul(float a, float b, float c) {
 #pragma clang fp contract(off)
-  return a + opq(b * c);
+  return a + (b * c);
 }
 // ((s + a*f) + b) + c*d  (raytracer.glsl:1810, 1956, 1972, 2003, 2024, 2046)
 DEV float nc_seed4(float s, float a, float f, float b, float c, float d) {
 #pragma clang fp contract(off)
-  return ((s + opq(a * f)) + b) + opq(c * d);
+  return ((s + (a * f)) + b) + (c * d);
 }
 // (s + a*f) + c*d  (raytracer.glsl:1909/1943)
 DEV float nc_seed3(float s, float a, float f, float c, float d) {
 #pragma clang fp contract(off)
-  return (s + opq(a * f)) + opq(c * d);
+  return (s + (a * f)) + (c * d);
 }
 
 // ------------------------------------------------------------------- RNG
@@ -140,18 +127,18 @@ DEV float hash(float seed) {
 #pragma clang fp contract(off)
   uint32_t n = __float_as_uint(seed) * 747796405u + 2891336453u;
   n = ((n >> ((n >> 28u) + 4u)) ^ n) * 277803737u;
-  return opq(u2f((n >> 22u) ^ n) * 2.3283064365386963e-10f);
+  return (u2f((n >> 22u) ^ n) * 2.3283064365386963e-10f);
 }
 // raytracer.glsl:308-312
 DEV void hash2(float sx, float sy, float &ox, float &oy) {
 #pragma clang fp contract(off)
-  float x = opq(sx * 0.1031f), y = opq(sy * 0.1030f);
+  float x = (sx * 0.1031f), y = (sy * 0.1030f);
   x = x - floorf(x);
   y = y - floorf(y);
-  float d = opq(x * (y + 19.19f)) + opq(y * (x + 19.19f));
+  float d = (x * (y + 19.19f)) + (y * (x + 19.19f));
   x += d;
   y += d;
-  float a = opq((x + y) * x), b = opq((x + y) * y);
+  float a = ((x + y) * x), b = ((x + y) * y);
   ox = a - floorf(a);
   oy = b - floorf(b);
 }
@@ -319,24 +306,21 @@ DEV int axis_of(v3 n) {
 }
 
 
-// --------------------------------------------------- triangles + LBVH
+// --------------------------------------------------- triangles + BVH
 // iTriangle (the reference's commented-out Moller-Trumbore, raytracer.glsl:
-// 864-892) over the device-built LBVH of all TRIANGLE models (rt0_bvh.hip).
-// Same EPSILON tests as the reference: |a| < EPSILON rejects (a < EPSILON
-// with back-face culling, opts[3]), t must lie in (EPSILON, tmin).
-#ifndef RT0_TRI_RCP  // v_rcp for 1/a: measured no faster than the exact divide (C5 8.50 vs 8.46 ms)
-#define RT0_TRI_RCP 0
-#endif
+// 864-892) over the BVH of all TRIANGLE models (rt0_bvh_sah.cpp / rt0_bvh.hip).
+// t must lie in (EPSILON, tmin) as there.  Deviation: the
+// parallel-ray test compares the determinant a = d . (e1 x e0) with
+// T.eps = EPSILON*|e0|*|e1| instead of the absolute EPSILON -- a scales with
+// the triangle's area, and with the absolute threshold every triangle of the
+// C5 model (edges ~0.015, |a| <= 1.9e-4) was rejected at every angle.
+// |a| < eps rejects (a < eps with back-face culling, opts[3]).
 DEV bool tri_test(const TriDev &T, v3 o, v3 d, float tmin, float &t) {
   const v3 e0 = mk(T.e0x, T.e0y, T.e0z), e1 = mk(T.e1x, T.e1y, T.e1z);
   const v3 h = mk(d.y * e1.z - d.z * e1.y, d.z * e1.x - d.x * e1.z, d.x * e1.y - d.y * e1.x);
   const float a = dot(e0, h);
-  if (T.cull ? a < EPSILON : (a > -EPSILON && a < EPSILON)) return false;
-#if RT0_TRI_RCP
-  const float f = frcp(a);  // v_rcp (1 ulp) instead of the IEEE divide sequence
-#else
+  if (T.cull ? a < T.eps : (a > -T.eps && a < T.eps)) return false;
   const float f = 1.0f / a;
-#endif
   const v3 s = o - mk(T.v0x, T.v0y, T.v0z);
   const float u = f * dot(s, h);
   if (u < 0.0f || u > 1.0f) return false;
@@ -356,125 +340,36 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
   const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
   return (tn <= tf && tn < tmin) ? tn : F_INF;
 }
-#ifndef RT0_LEAF_UNIFIED
-#define RT0_LEAF_UNIFIED 1
-#endif
-#ifndef RT0_BVH_HALF  // walk the binary16 copies of the nodes (BvhNodeH)
-#define RT0_BVH_HALF 0
-#endif
-DEV float h16_lo(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xffffu)); }
-DEV float h16_hi(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)); }
-#ifndef RT0_LEAF_DEFER  // Aila-Laine style postponed leaf: A/B knob
-#define RT0_LEAF_DEFER 0
-#endif
-// closest triangle hit along (o, d) before tmin: depth-first, nearer child
-// first, the far child on a per-lane stack in LDS (stride = block size so the
-// 64 lanes of a wave hit 64 different banks).  Returns the leaf-order triangle
-// index or -1; tmin is updated.  ANY: stop at the first hit before tmin (an
-// occlusion query: whether some triangle lies in (EPSILON, tmin)).
 // The per-lane traversal stacks: ONE LDS array for every traversal of the
 // kernel (closest-hit and occlusion instances alike -- a __shared__ array
-// declared inside the template would be one array per instance).
+// declared inside the template would be one array per instance); stride =
+// block size, so the 64 lanes of a wave hit 64 different banks.
 DEV int32_t *bvh_stack_lds() {
   __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
   return stk_base + threadIdx.x;
 }
+// closest triangle hit along (o, d) before tmin: depth-first, nearer child
+// first, the far child on the per-lane LDS stack.  Returns the leaf-order
+// triangle index or -1; tmin is updated.  ANY: stop at the first hit before
+// tmin (an occlusion query: whether some triangle lies in (EPSILON, tmin)).
+// Leaves hold one triangle and are tested in place, left before right; the
+// first leaf test of every lane runs in one block whichever side it is on
+// (8.36-8.39 vs 8.57-8.59 ms at 1024^2).
 template <bool ANY = false>
-DEV int bvh2_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
+DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
   int32_t *stk = bvh_stack_lds();
   int sp = 0, node = 0, best = -1;
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
   const TriDev *__restrict__ tris = P.tris;
   // a ray visits each of the n-1 nodes at most once: the cap only guarantees
   // that every wave exits even on a corrupt tree
-#if RT0_LEAF_DEFER
-  // one leaf per lane may wait while the lane keeps walking inner nodes; the
-  // leaf tests run once every active lane has one (or a lane holds two, or
-  // its walk ends), so the 64 lanes test triangles together.  Same closest
-  // hit: only the order of the tests changes.
-  int pend = -1;
   for (int guard = 2 * P.n_tris + 8; guard > 0; --guard) {
     const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
     const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
     float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
     float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
     const int cl = lk.x, cr = lk.y;
-    int l0 = -1, l1 = -1;
-    if (tl != F_INF && cl < 0) {
-      l0 = ~cl;
-      tl = F_INF;
-    }
-    if (tr != F_INF && cr < 0) {
-      if (l0 < 0) l0 = ~cr;
-      else l1 = ~cr;
-      tr = F_INF;
-    }
-    bool done = false;
-    if (tl != F_INF && tr != F_INF) {
-      const bool lfirst = tl <= tr;
-      stk[256 * sp] = lfirst ? cr : cl;
-      sp = min(sp + 1, RT0_BVH_STACK - 1);
-      node = lfirst ? cl : cr;
-    } else if (tl != F_INF) {
-      node = cl;
-    } else if (tr != F_INF) {
-      node = cr;
-    } else if (sp == 0) {
-      done = true;
-    } else {
-      node = stk[256 * --sp];
-    }
-    const int nl = (pend >= 0) + (l0 >= 0) + (l1 >= 0);
-    const bool has = nl > 0;
-    const bool now = has && (done || nl >= 2 || __ballot(has) == __builtin_amdgcn_read_exec());
-    if (now) {
-#pragma unroll 1
-      for (int k = 0; k < 3; ++k) {
-        const int li = k == 0 ? pend : (k == 1 ? l0 : l1);
-        float t;
-        if (li >= 0 && tri_test(tris[li], o, d, tmin, t)) {
-          tmin = t;
-          best = li;
-        }
-      }
-      pend = -1;
-      if (ANY && best >= 0) break;
-    } else if (has && pend < 0) {
-      pend = l0 >= 0 ? l0 : l1;
-    }
-    if (done) break;
-  }
-  if (pend >= 0) {  // only on a guard exit
-    float t;
-    if (tri_test(tris[pend], o, d, tmin, t)) {
-      tmin = t;
-      best = pend;
-    }
-  }
-  return best;
-#endif
-  for (int guard = 2 * P.n_tris + 8; guard > 0; --guard) {
-#if RT0_BVH_HALF
-    // 32-B nodes with binary16 boxes rounded outward: half the bytes per
-    // visit, the same closest hit (a box only grows)
-    const uint4 *hn = reinterpret_cast<const uint4 *>(P.bvh16) + 2 * node;
-    const uint4 q0 = hn[0], q1 = hn[1];
-    float tl = box_enter(h16_lo(q0.x), h16_hi(q0.x), h16_lo(q0.y), h16_hi(q0.y), h16_lo(q0.z), h16_hi(q0.z), o, inv,
-                         tmin);
-    float tr = box_enter(h16_lo(q0.w), h16_hi(q0.w), h16_lo(q1.x), h16_hi(q1.x), h16_lo(q1.y), h16_hi(q1.y), o, inv,
-                         tmin);
-    int cl = (int)q1.z, cr = (int)q1.w;
-#else
-    const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
-    const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
-    float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
-    float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
-    int cl = lk.x, cr = lk.y;
-#endif
     if (cnt) ++cnt[0];  // counting instance: nodes visited (two child boxes each)
-#if RT0_LEAF_UNIFIED
-    // leaves are tested in place, left before right; the first leaf test of
-    // every lane runs in one block whichever side it is on
     int l0 = -1, l1 = -1;
     if (tl != F_INF && cl < 0) {
       l0 = ~cl;
@@ -498,25 +393,6 @@ DEV int bvh2_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, uns
       }
       if (ANY && best >= 0) break;
     }
-#else
-    if (tl != F_INF && cl < 0) {  // leaves are tested in place
-      float t;
-      if (tri_test(tris[~cl], o, d, tmin, t)) {
-        tmin = t;
-        best = ~cl;
-      }
-      tl = F_INF;
-    }
-    if (tr != F_INF && cr < 0) {
-      float t;
-      if (tri_test(tris[~cr], o, d, tmin, t)) {
-        tmin = t;
-        best = ~cr;
-      }
-      tr = F_INF;
-    }
-    if (ANY && best >= 0) break;
-#endif
     if (tl != F_INF && tr != F_INF) {
       const bool lfirst = tl <= tr;
       stk[256 * sp] = lfirst ? cr : cl;
@@ -532,107 +408,6 @@ DEV int bvh2_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, uns
     }
   }
   return best;
-}
-
-// (t, link) compare-exchange: the nearer child first
-DEV void cx_near(float &ta, int &ca, float &tb, int &cb) {
-  const bool s = tb < ta;
-  const float t = s ? tb : ta;
-  const int c = s ? cb : ca;
-  tb = s ? ta : tb;
-  cb = s ? ca : cb;
-  ta = t;
-  ca = c;
-}
-// The same query over the 4-wide tree (Bvh4Node): one 128-B node fetch tests
-// four child boxes, so a ray makes about half the dependent node fetches of
-// the binary walk.  Hit leaves are tested first, in slot order, through one
-// triangle-test site (a lane walks the triangles of all its hit leaves in one
-// loop); the internal children still entered before the updated tmin are
-// sorted by entry distance (5-exchange network), the nearest is visited next
-// and the others are pushed far to near.  The build bounds the pushes along
-// any root-to-leaf path by RT0_BVH_STACK - 1.
-template <bool ANY = false>
-DEV int bvh4_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
-  int32_t *stk = bvh_stack_lds();
-  int sp = 0, node = 0, best = -1;
-  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh4);
-  const TriDev *__restrict__ tris = P.tris;
-  // fewer than n_tris nodes, each visited at most once: the cap only
-  // guarantees that every wave exits even on a corrupt tree
-  for (int guard = P.n_tris + 8; guard > 0; --guard) {
-    const float4 *nd = nodes + 8 * node;
-    const float4 mnx = nd[0], mny = nd[1], mnz = nd[2], mxx = nd[3], mxy = nd[4], mxz = nd[5];
-    const int4 lk = reinterpret_cast<const int4 *>(nd)[6];
-    float t0 = box_enter(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, tmin);
-    float t1 = box_enter(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, tmin);
-    float t2 = box_enter(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, tmin);
-    float t3 = box_enter(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, tmin);
-    int c0 = lk.x, c1 = lk.y, c2 = lk.z, c3 = lk.w;
-    if (cnt) cnt[0] += 2;  // counted in the binary node's unit: pairs of slab tests
-    unsigned lm = (t0 != F_INF && c0 < 0 ? 1u : 0u) | (t1 != F_INF && c1 < 0 ? 2u : 0u) |
-                  (t2 != F_INF && c2 < 0 ? 4u : 0u) | (t3 != F_INF && c3 < 0 ? 8u : 0u);
-    if (lm) {
-      int cur = 0, end = 0;
-      for (;;) {
-        if (cur == end) {
-          if (lm == 0) break;
-          const int k = __builtin_ctz(lm);
-          lm &= lm - 1;
-          const int e = ~(k == 0 ? c0 : (k == 1 ? c1 : (k == 2 ? c2 : c3)));
-          cur = e & ((1 << RT0_LEAF_SHIFT) - 1);
-          end = cur + (e >> RT0_LEAF_SHIFT) + 1;
-        }
-        float t;
-        if (cnt) ++cnt[1];  // triangle tests
-        if (tri_test(tris[cur], o, d, tmin, t)) {
-          tmin = t;
-          best = cur;
-        }
-        ++cur;
-        if (ANY && best >= 0) break;
-      }
-      if (ANY && best >= 0) break;
-    }
-    // internal children still entered before tmin (leaves are done)
-    t0 = (c0 < 0 || !(t0 < tmin)) ? F_INF : t0;
-    t1 = (c1 < 0 || !(t1 < tmin)) ? F_INF : t1;
-    t2 = (c2 < 0 || !(t2 < tmin)) ? F_INF : t2;
-    t3 = (c3 < 0 || !(t3 < tmin)) ? F_INF : t3;
-    cx_near(t0, c0, t1, c1);
-    cx_near(t2, c2, t3, c3);
-    cx_near(t0, c0, t2, c2);
-    cx_near(t1, c1, t3, c3);
-    cx_near(t1, c1, t2, c2);
-    if (t0 == F_INF) {
-      if (sp == 0) break;
-      node = stk[256 * --sp];
-      continue;
-    }
-    node = c0;
-    if (t3 != F_INF) {
-      stk[256 * sp] = c3;
-      sp = min(sp + 1, RT0_BVH_STACK - 1);
-    }
-    if (t2 != F_INF) {
-      stk[256 * sp] = c2;
-      sp = min(sp + 1, RT0_BVH_STACK - 1);
-    }
-    if (t1 != F_INF) {
-      stk[256 * sp] = c1;
-      sp = min(sp + 1, RT0_BVH_STACK - 1);
-    }
-  }
-  return best;
-}
-
-template <bool ANY = false>
-DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
-#if RT0_BVH_WIDE
-  return bvh4_closest<ANY>(P, o, d, inv, tmin, cnt);
-#else
-  return bvh2_closest<ANY>(P, o, d, inv, tmin, cnt);
-#endif
 }
 
 // getAnimatedPosition(meshes[i].pos, i, u_time) (raytracer.glsl:263-298),
@@ -1273,17 +1048,17 @@ DEV float pack_alpha(float age, float M, int idx, int nlights) {
   float na = fminf(fmaxf(age / 30.0f, 0.0f), 1.0f);
   float nM = fminf(fmaxf(M / 100.0f, 0.0f), 1.0f);
   float nli = (float)(idx + 1) / (float)(nlights > 1 ? nlights : 1);
-  return (opq(na * 0.33f) + opq(nM * 0.33f)) + opq(nli * 0.34f);
+  return ((na * 0.33f) + (nM * 0.33f)) + (nli * 0.34f);
 }
 // unpackReservoirEnhanced alpha decode, 1448-1457 (unfused)
 DEV void unpack_alpha(float pa, int nlights, float &age, float &M, int &idx) {
 #pragma clang fp contract(off)
-  float nli = opq(pa * 2.94f);
+  float nli = (pa * 2.94f);
   nli = nli - floorf(nli);
-  float temp = pa - opq(nli * 0.34f);
-  float nM = opq(temp * 3.03f);
+  float temp = pa - (nli * 0.34f);
+  float nM = (temp * 3.03f);
   nM = nM - floorf(nM);
-  float nage = (temp - opq(nM * 0.33f)) * 3.03f;
+  float nage = (temp - (nM * 0.33f)) * 3.03f;
   age = nage * 30.0f;
   M = nM * 100.0f;
   int len1 = nlights > 1 ? nlights : 1;
@@ -1496,7 +1271,7 @@ struct Integrator {
   // GL LINEAR + CLAMP_TO_EDGE fetch of an RGBA32F plane (index.js:660-664)
   DEV float4 tex2d(const float4 *__restrict__ t, float u, float v) {
 #pragma clang fp contract(off)
-    float x = opq(u * P.res_x) - 0.5f, y = opq(v * P.res_y) - 0.5f;
+    float x = (u * P.res_x) - 0.5f, y = (v * P.res_y) - 0.5f;
     float fx0 = floorf(x), fy0 = floorf(y);
     float a = x - fx0, b = y - fy0;
     int x0 = (int)fx0, y0 = (int)fy0;
@@ -1512,10 +1287,10 @@ struct Integrator {
 #pragma clang fp contract(off)
     float4 r;
     float top, bot;
-    top = t00.x + opq(a * (t10.x - t00.x)); bot = t01.x + opq(a * (t11.x - t01.x)); r.x = top + opq(b * (bot - top));
-    top = t00.y + opq(a * (t10.y - t00.y)); bot = t01.y + opq(a * (t11.y - t01.y)); r.y = top + opq(b * (bot - top));
-    top = t00.z + opq(a * (t10.z - t00.z)); bot = t01.z + opq(a * (t11.z - t01.z)); r.z = top + opq(b * (bot - top));
-    top = t00.w + opq(a * (t10.w - t00.w)); bot = t01.w + opq(a * (t11.w - t01.w)); r.w = top + opq(b * (bot - top));
+    top = t00.x + (a * (t10.x - t00.x)); bot = t01.x + (a * (t11.x - t01.x)); r.x = top + (b * (bot - top));
+    top = t00.y + (a * (t10.y - t00.y)); bot = t01.y + (a * (t11.y - t01.y)); r.y = top + (b * (bot - top));
+    top = t00.z + (a * (t10.z - t00.z)); bot = t01.z + (a * (t11.z - t01.z)); r.z = top + (b * (bot - top));
+    top = t00.w + (a * (t10.w - t00.w)); bot = t01.w + (a * (t11.w - t01.w)); r.w = top + (b * (bot - top));
     return r;
   }
   // tex2d split in two so that several taps' loads can be issued before any
@@ -1528,7 +1303,7 @@ struct Integrator {
   };
   DEV Bil bil_at(float u, float v, bool count) {
 #pragma clang fp contract(off)
-    float x = opq(u * P.res_x) - 0.5f, y = opq(v * P.res_y) - 0.5f;
+    float x = (u * P.res_x) - 0.5f, y = (v * P.res_y) - 0.5f;
     float fx0 = floorf(x), fy0 = floorf(y);
     Bil r;
     r.a = x - fx0;
@@ -2317,7 +2092,7 @@ struct Integrator {
     float seed;
     {
 #pragma clang fp contract(off)
-      seed = hash((opq(fcx * 12.9898f) + opq(fcy * 78.233f)) + opq(1113.1f * (float)frame));
+      seed = hash(((fcx * 12.9898f) + (fcy * 78.233f)) + (1113.1f * (float)frame));
     }
     hero = 550.0f;
     if constexpr (SPECTRAL) {
@@ -2387,9 +2162,9 @@ DEV void accumulate(const It &it, const LaunchParams &P, float4 &a, v3 s) {
     a.z = mixf(a.z, s.z, P.ema_alpha);
   } else {
 #pragma clang fp contract(off)
-    a.x += opq(s.x);
-    a.y += opq(s.y);
-    a.z += opq(s.z);
+    a.x += (s.x);
+    a.y += (s.y);
+    a.z += (s.z);
   }
 }
 
@@ -2402,103 +2177,9 @@ DEV size_t sample_index(const LaunchParams &P, int px, int r) {
 
 // The pass kernel body: 16x16 pixel tile per 256-thread workgroup (four 8x8
 // wave tiles); each lane accumulates its pixel's passes in registers.
-// XCD-aware tile order.  Workgroups are dealt round-robin over the 8 XCDs
-// (blocks b and b+8 share one, MI355X_MICROARCH.md "Workgroup dispatch"),
-// and each XCD has its own 4 MiB L2: mapping the blocks of one XCD onto one
-// contiguous run of tiles (row-major) keeps the spatial/temporal reservoir
-// taps and the BVH nodes of neighbouring tiles in the same L2.  A bijection
-// on the grid's (x, y) blocks, so it changes no result.
-//   RT0_XCD_REMAP 1: one contiguous run per XCD (whole bands of the image);
-//   RT0_XCD_REMAP c > 1: runs of c consecutive tiles per XCD, interleaved
-//   (8c tiles per round), keeping the work of the XCDs balanced.
-#ifndef RT0_XCD_REMAP
-#define RT0_XCD_REMAP 0
-#endif
-DEV void block_tile(int &bx, int &by) {
-#if RT0_XCD_REMAP == 1
-  const int gx = (int)gridDim.x, n = (int)(gridDim.x * gridDim.y);
-  const int L = (int)blockIdx.x + (int)blockIdx.y * gx;
-  const int q = n >> 3, rem = n & 7, k = L & 7, j = L >> 3;
-  const int t = k * q + min(k, rem) + j;
-  bx = t % gx;
-  by = t / gx;
-#elif RT0_XCD_REMAP > 1
-  const int gx = (int)gridDim.x, n = (int)(gridDim.x * gridDim.y);
-  const int L = (int)blockIdx.x + (int)blockIdx.y * gx;
-  constexpr int c = RT0_XCD_REMAP;
-  const int base = (L / (8 * c)) * (8 * c);
-  int t = base + (L & 7) * c + ((L >> 3) % c);
-  if (base + 8 * c > n) t = L;  // ragged last round: identity
-  bx = t % gx;
-  by = t / gx;
-#else
-  bx = (int)blockIdx.x;
-  by = (int)blockIdx.y;
-#endif
-}
-
-// ReSTIR pass with lane refill: the wave owns 64*P.refill pixels -- P.refill
-// 8x8 blocks stacked in y -- and a lane whose path has ended writes its pixel
-// (accumulator + reservoir MRTs) and takes the pool's next pixel, so lanes
-// whose ray left for the sky do not idle while their neighbours bounce.  The
-// pixels of one pass are independent (they read only the previous passes'
-// reservoirs), so the result is the same as one pixel per lane.
-template <class It, class Scene, class Cfg>
-DEV void restir_refill_body(const LaunchParams &P, It &it, const Scene &sc, const Cfg &cfg) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int R = P.refill, pool = 64 * R;
-  int bx, by;
-  block_tile(bx, by);
-  const int x0 = P.vp_x0 + bx * 16 + ((wave & 1) << 3);
-  const int r0 = P.vp_y0 + by * 16 * R + (wave >> 1) * 8 * R;
-  const unsigned long long below = (1ull << lane) - 1ull;
-  typename It::Path ps;
-  int pi = lane, next = 64;
-  bool have = true, alive = false, valid = false;
-  int px = 0, py = 0;
-  auto start = [&]() {
-    px = x0 + (pi & 7);
-    const int r = r0 + ((pi >> 6) << 3) + ((pi >> 3) & 7);
-    py = (px < P.vp_x1 && r < P.vp_y1) ? image_row(P, r) : P.height;
-    valid = py < P.height;
-    alive = false;
-    if (valid) {
-      it.frame = P.frame0;
-      it.begin(ps, px, py);
-      alive = cfg.max_bounces() > 0;
-    }
-  };
-  start();
-  while (true) {
-    if (alive) alive = it.step(ps);
-    const bool done = have && !alive;
-    if (done && valid) {
-      const size_t pix = (size_t)py * P.width + px;
-      float4 a = P.accum[pix];
-      accumulate(it, P, a, it.finish(ps));
-      P.accum[pix] = a;
-      if (P.rout_main != nullptr && P.rout_aux != nullptr) {
-        if (it.flag(F_RESTIR_DEF)) {
-          const Res &q = it.fin;
-          P.rout_main[pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
-          P.rout_aux[pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
-        } else {
-          P.rout_main[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
-          P.rout_aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-      }
-      valid = false;
-    }
-    const unsigned long long fin = __ballot(done);
-    if (done) {
-      pi = next + __popcll(fin & below);
-      if (pi < pool) start();
-      else have = false;
-    }
-    next += __popcll(fin);
-    if (__ballot(have) == 0ull) break;
-  }
-}
+// (XCD-aware tile orders -- whole bands or interleaved runs of tiles per XCD
+// -- were measured and lost or tied, DESIGN 4.7: blockIdx maps straight to
+// the tile.)
 
 // Path regeneration: the lane runs its pixel's passes back to back as ONE
 // loop of bounce steps; when its path ends it accumulates the sample and
@@ -2532,21 +2213,11 @@ DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int 
 
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
-  if constexpr (Scene::kStatic) Scene::stage();  // LDS copy of the scene records (before any early exit)
-  if constexpr (RESTIR && !COUNT) {
-    if (P.refill > 1) {
-      Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT> it(P, sc, cfg);
-      restir_refill_body(P, it, sc, cfg);
-      return;
-    }
-  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
   const int ly = (lane >> 3) + ((wave >> 1) << 3);
-  int bx, by;
-  block_tile(bx, by);
-  const int px = P.vp_x0 + bx * 16 + lx;
-  const int r = P.vp_y0 + by * 16 + ly;
+  const int px = P.vp_x0 + (int)blockIdx.x * 16 + lx;
+  const int r = P.vp_y0 + (int)blockIdx.y * 16 + ly;
   if (px >= P.vp_x1 || r >= P.vp_y1) return;
   const int py = image_row(P, r);
   if (py >= P.height) return;

@@ -7,6 +7,9 @@
 
 #include "../../include/rt0.h"
 
+struct BvhNode;
+struct TriDev;
+
 namespace rt0h {
 int lookup_material(const std::string &name, rt0_mesh &m);
 int parse_scene_glsl(const char *text, const char *const *sdf, int n_sdf, std::vector<rt0_mesh> &meshes,
@@ -15,6 +18,10 @@ int parse_scene_glsl(const char *text, const char *const *sdf, int n_sdf, std::v
 // are fan-triangulated, negative (relative) indices resolved
 int parse_obj(const char *text, size_t len, std::vector<float> &pos, std::vector<int32_t> &tris, std::string &err);
 void default_config(rt0_config &c);
+// binned-SAH BVH (rt0_bvh_sah.cpp) of n triangles (v: 9 floats each, model:
+// owner tags with RT0_TRI_CULL_BIT) -> pre-order inner nodes + leaf-order
+// triangles; returns the depth (edges root -> deepest leaf), -1 for n <= 0
+int bvh_build_sah(int n, const float *v, const int32_t *model, std::vector<BvhNode> &nodes, std::vector<TriDev> &tris);
 int parse_config(const char *const *defines, int nd, const char *const *constants, int nc, rt0_config &c,
                  std::string &err);
 }  // namespace rt0h

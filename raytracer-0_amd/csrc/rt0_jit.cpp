@@ -63,7 +63,6 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // 8) instead of the ahead-of-time kernels' 48: 48 x 256 lanes x 4 B = 48 KiB
   // per workgroup would cap a CU at three workgroups
   if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
-  o << "#define RT0_BVH_WIDE " << k.bvh_wide << "\n";
   o << "#define RT0_HALO_CHECK " << k.halo_check << "\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
@@ -101,18 +100,6 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   for (int i = 0; i < s.n_lights; i++) o << s.light_index[i] << ",";
   if (s.n_lights == 0) o << "-1";
   o << "};\n";
-  // Optional LDS copies of the records for lookups by a per-lane index (the
-  // mesh a ray hit): ds_read with broadcast instead of a vector-memory gather
-  // from the constant segment.  Constant indices (the unrolled mesh/light loops) still
-  // fold to immediates (__builtin_constant_p is resolved after inlining).
-  const int ntl = nt > 0 ? nt : 1;
-  // measured on the bench scene: 5.86 ms with the LDS copies vs 5.75 ms without
-  // (more code, 65 VGPRs = one wave less per SIMD), so off by default
-  static const bool lds = getenv("RT0_JIT_LDS") ? atoi(getenv("RT0_JIT_LDS")) != 0 : false;  // A/B knob
-  // RT0_LDS_IDX(i): this lookup goes to the LDS copy (never when staging is off)
-  o << (lds ? "#define RT0_LDS_IDX(i) (!__builtin_constant_p(i))\n" : "#define RT0_LDS_IDX(i) false\n");
-  o << "__shared__ GeomRec sJitGeom[" << ntl << "];\n__shared__ MatRec sJitMat[" << ntl << "];\n";
-  if (s.any_tex) o << "__shared__ TexRec sJitTex[" << ntl << "];\n";
   o << "struct JitScene {\n"
        "  static constexpr bool kStatic = true;\n"
        "  static constexpr int kMeshes = "
@@ -123,22 +110,12 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
        "  __device__ static constexpr int n_sdfs() { return kSdfs; }\n"
        "  __device__ static constexpr int n_models() { return kModels; }\n"
        "  __device__ static constexpr int n_lights() { return kLights; }\n"
-       "  __device__ static GeomRec geom(int i) { return RT0_LDS_IDX(i) ? sJitGeom[i] : kJitGeom[i]; }\n"
-       "  __device__ static MatRec mat(int i) { return RT0_LDS_IDX(i) ? sJitMat[i] : kJitMat[i]; }\n"
+       "  __device__ static GeomRec geom(int i) { return kJitGeom[i]; }\n"
+       "  __device__ static MatRec mat(int i) { return kJitMat[i]; }\n"
        "  __device__ static float j3(int i) { return kJitJ3[i]; }\n"
        "  __device__ static int sdf_kind(int i) { return kJitSdfKind[i]; }\n"
        "  __device__ static int light(int i) { return kJitLights[i]; }\n"
-    << (s.any_tex ? "  __device__ static TexRec tex(int i) { return RT0_LDS_IDX(i) ? sJitTex[i] : kJitTex[i]; }\n"
-                  : "  __device__ static TexRec tex(int i) { return kJitTex[i]; }\n")
-    << "  __device__ static void stage() {\n";
-  if (lds)
-    o << "    for (int k = threadIdx.x; k < " << ntl << "; k += blockDim.x) {\n"
-         "      sJitGeom[k] = kJitGeom[k];\n"
-         "      sJitMat[k] = kJitMat[k];\n"
-      << (s.any_tex ? "      sJitTex[k] = kJitTex[k];\n" : "")
-      << "    }\n"
-         "    __syncthreads();\n";
-  o << "  }\n"
+    << "  __device__ static TexRec tex(int i) { return kJitTex[i]; }\n"
        "  __device__ static constexpr bool any_tex() { return "
     << (s.any_tex ? "true" : "false") << "; }\n"
        "};\n";
@@ -335,15 +312,8 @@ uint32_t flags_from_config(const rt0_config &g) {
   return f;
 }
 
-bool bvh_wide_selected() {
-  static const bool w = getenv("RT0_BVH_WIDE") && atoi(getenv("RT0_BVH_WIDE")) != 0;
-  return w;
-}
-
 JitKey make_jit_key(const rt0_config &g, int n_sdfs) {
   JitKey k;
-  // RT0_BVH_WIDE=1: the 4-wide walk instead of the binary one (A/B knob)
-  k.bvh_wide = bvh_wide_selected() ? 1 : 0;
   k.flags = flags_from_config(g);
   k.max_bounces = g.max_bounces;
   k.max_diff = g.max_diff_bounces;

@@ -18,7 +18,6 @@ struct JitKey {
   float fudge;
   bool restir, vol, sdf, spectral;
   int bvh_stack = 0;  // LDS traversal stack entries (push bound + 1) when the scene has models
-  int bvh_wide = 0;   // RT0_BVH_WIDE of the generated kernel (4-wide or binary walk)
   int halo_check = 1;  // RT0_HALO_CHECK: sharded launches count reservoir fetches outside the halo
 };
 
@@ -26,10 +25,6 @@ std::string jit_source(const SceneDev &s, const JitKey &k);
 int jit_compile(const std::string &src, std::vector<char> &code, std::string &err);
 // runtime feature flags (F_*) of a config, and the JIT key of (config, scene)
 uint32_t flags_from_config(const rt0_config &c);
-// RT0_BVH_WIDE=1 in the environment: the host builds the 4-wide tree and the
-// scene-specialised kernels walk it (A/B knob; the ahead-of-time kernels keep
-// the binary walk)
-bool bvh_wide_selected();
 JitKey make_jit_key(const rt0_config &c, int n_sdfs);
 // flatten validated mesh records into the device scene layout
 SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, int nm, const int32_t *li, int nl);

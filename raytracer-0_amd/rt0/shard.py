@@ -70,6 +70,44 @@ def gather_image(acc, rank, world, band, image=None, bufs=None):
     return None
 
 
+class StreamOrder:
+    """Orders librt0's stream (rt0_device_accum) against torch's current stream
+    with events, so that a producer on one and a consumer on the other need no
+    host synchronisation: torch_after_rt0() before torch work that reads what
+    librt0 wrote (exchanges, gathers), rt0_after_torch() before a librt0
+    launch that reads what torch wrote (a zeroed accumulator, received halo
+    rows).  Also times a torch-stream interval (begin/end_timing)."""
+
+    def __init__(self, renderer, device):
+        import torch
+        _, stream = renderer.device_accum()
+        self.torch = torch
+        self.ext = torch.cuda.ExternalStream(stream, device=device)
+        self.ev_rt0 = torch.cuda.Event()
+        self.ev_torch = torch.cuda.Event()
+        self.t0 = torch.cuda.Event(enable_timing=True)
+        self.t1 = torch.cuda.Event(enable_timing=True)
+
+    def torch_after_rt0(self):
+        self.ev_rt0.record(self.ext)
+        self.torch.cuda.current_stream().wait_event(self.ev_rt0)
+
+    def rt0_after_torch(self):
+        self.ev_torch.record(self.torch.cuda.current_stream())
+        self.ext.wait_event(self.ev_torch)
+
+    def begin_timing(self):
+        self.t0.record()
+        return self.t0
+
+    def end_timing(self, ev=None):
+        self.t1.record()
+
+    def elapsed_ms(self):
+        """t0 -> t1 on torch's stream (after a synchronisation)."""
+        return self.t0.elapsed_time(self.t1)
+
+
 class BandGather:
     """The per-step gather for band-packed accumulators (rt0_set_accum_buffer_compact):
     every rank renders straight into a [rows, W, 4] buffer holding only its
@@ -80,11 +118,17 @@ class BandGather:
     host->device index upload.
 
     With band = block_band(H, world) every rank owns one contiguous row block
-    (sharded ReSTIR); `send` then passes that block of a full-size accumulator."""
+    (sharded ReSTIR); `send` then passes that block of a full-size accumulator.
 
-    def __init__(self, H, W, rank, world, band, device, channels=4):
+    staged=True (a gloo process group, which moves host tensors only): the
+    send buffer is copied to host memory, gathered there, and rank 0 copies
+    the received buffers back to the device -- the same layout and reorder,
+    so the assembled image is identical."""
+
+    def __init__(self, H, W, rank, world, band, device, channels=4, staged=False):
         import torch
         self.H, self.W, self.rank, self.world, self.band = H, W, rank, world, band
+        self.staged = staged
         self.nb = (H + band - 1) // band
         self.max_owned = (self.nb + world - 1) // world
         self.rows = self.max_owned * band  # every rank's buffer has this many rows (RCCL needs equal sizes)
@@ -100,16 +144,25 @@ class BandGather:
             self.src = torch.tensor(src_slot, device=device)
             self.dst = torch.tensor(dst_band, device=device)
             self.image = torch.zeros((self.nb * band, W, channels), dtype=torch.float32, device=device)
+            if staged:
+                self.recv_host = torch.empty((world, self.rows, W, channels), dtype=torch.float32)
+                self.bufs_host = list(self.recv_host.unbind(0))
 
     def gather(self, send=None):
         """Collective; rank 0 returns the assembled [H, W, 4] image (a view of a
         persistent buffer), the other ranks None.  send defaults to self.acc."""
         import torch.distributed as dist
         send = self.acc if send is None else send
+        if self.staged:
+            send = send.cpu()
         if self.rank != 0:
             dist.gather(send, None, dst=0)
             return None
-        dist.gather(send, self.bufs, dst=0)
+        if self.staged:
+            dist.gather(send, self.bufs_host, dst=0)
+            self.recv.copy_(self.recv_host)
+        else:
+            dist.gather(send, self.bufs, dst=0)
         bands = self.recv.view(self.world * self.max_owned, self.band, self.W, -1)
         img = self.image.view(self.nb, self.band, self.W, -1)
         img.index_copy_(0, self.dst, bands.index_select(0, self.src))
@@ -186,20 +239,30 @@ def halo_plan(rank, world, band, height, halo):
     return plan
 
 
-def exchange_halo(planes, rank, world, band, halo):
+def exchange_halo(planes, rank, world, band, halo, staged=False):
     """Collective over torch.distributed (RCCL on GPUs, gloo on CPU): planes is
     a list of [H, W, 4] tensors, fresh in this rank's block; afterwards the
-    halo rows hold the neighbours' rows."""
+    halo rows hold the neighbours' rows.  staged=True (gloo with device
+    planes): sent rows are copied to host buffers first and received rows
+    copied back to the device afterwards."""
     import torch.distributed as dist
     height = planes[0].shape[0]
-    ops = []
+    ops, back = [], []
     for p in planes:
         for kind, peer, r0, r1 in halo_plan(rank, world, band, height, halo):
+            rows = p[r0:r1]
+            if staged and rows.is_cuda:
+                host = rows.cpu() if kind == "send" else rows.new_empty(rows.shape, device="cpu")
+                if kind == "recv":
+                    back.append((rows, host))
+                rows = host
             fn = dist.isend if kind == "send" else dist.irecv
-            ops.append(dist.P2POp(fn, p[r0:r1], peer))
+            ops.append(dist.P2POp(fn, rows, peer))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    for dev_rows, host in back:
+        dev_rows.copy_(host)
 
 
 def exchange_halo_local(planes_by_rank, band, halo):
@@ -218,10 +281,11 @@ class RestirShard:
     """One rank's sharded ReSTIR renderer state: torch-owned reservoir planes
     handed to librt0, so that the halo rows can be exchanged as tensors."""
 
-    def __init__(self, renderer, rank, world, height, width, device, halo=24, band=None):
+    def __init__(self, renderer, rank, world, height, width, device, halo=24, band=None, staged=False, order=None):
         import torch
         self.r = renderer
-        self.rank, self.world, self.halo = rank, world, halo
+        self.rank, self.world, self.halo, self.staged = rank, world, halo, staged
+        self.order = order or StreamOrder(renderer, device)
         self.band = band or block_band(height, world)  # default: one contiguous block
         self.planes = torch.zeros((8, height, width, 4), dtype=torch.float32, device=device)
         renderer.set_restir_buffers([self.planes[i].data_ptr() for i in range(8)])
@@ -237,17 +301,18 @@ class RestirShard:
     def render(self, first, n, exchange=None):
         """Passes first..first+n-1, one launch each, halo exchange after each
         (exchange(planes) defaults to exchange_halo over torch.distributed).
-        Raises if any fetch fell outside block + halo."""
-        import torch
+        The launches are asynchronous on librt0's stream; each exchange waits
+        for its pass and the next pass for the exchange through events (no host
+        synchronisation per pass).  Raises if any fetch fell outside block + halo."""
         for k in range(first, first + n):
-            self.r.render(k, 1)
+            self.r.render_async(k, 1)
             planes = self.newest()
+            self.order.torch_after_rt0()
             if exchange is None:
-                exchange_halo(planes, self.rank, self.world, self.band, self.halo)
+                exchange_halo(planes, self.rank, self.world, self.band, self.halo, staged=self.staged)
             else:
                 exchange(planes)
-            # librt0 launches on its own stream: the collective's writes must land first
-            torch.cuda.synchronize(self.planes.device)
+            self.order.rt0_after_torch()
         miss = self.r.halo_misses()
         if miss:
             raise RuntimeError("sharded ReSTIR: %d reservoir fetches fell outside the %d-row halo; "

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 --pmc passes of one workload (scripts/gpu_measure.sh)
+into per-launch figures of the scene-specialised pass kernel (rt0_jit_pass).
+
+    pmc_summary.py OUT.json W H BYTES_PER_PIXEL SKIP PASS_DIR [PASS_DIR ...]
+
+Per dispatch of rt0_jit_pass (the counting instance bench.py launches
+afterwards is a different kernel and is excluded), dropping the first SKIP
+dispatches (the warm-up step), averaged over the rest:
+  * HBM traffic: FETCH_SIZE x 2 (MI355X_MICROARCH.md: gfx950 reports half the
+    bytes of a 16-B/lane streaming read; scripts/fetch_calib.hip measures the
+    factor for the 64-B gathers and bilinear taps of the ReSTIR/BVH kernels)
+    + WRITE_SIZE (exact for 16-B/lane stores); counters in KiB;
+  * VALU: SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32, SQ_ACTIVE_INST_VALU,
+    SQ_THREAD_CYCLES_VALU -> lane utilisation (active lanes per issued VALU
+    instruction / 64);
+  * clock: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 / dispatch duration
+    = the effective shader clock under load (DVFS give-back);
+  * stall split: SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY as shares of
+    SQ_WAVE_CYCLES.
+The algorithmic bytes per launch = W x H x BYTES_PER_PIXEL (32: one float4
+accumulator read + write; 160 for a ReSTIR pass: + two reservoir MRT writes
+and the six reservoir planes read once).
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+KERNEL = "rt0_jit_pass"
+
+
+def dispatches(d):
+    """{dispatch id: {counter: value}} and {dispatch id: duration ns} of the
+    pass kernel in one pass directory."""
+    vals = defaultdict(lambda: defaultdict(float))
+    for fn in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(fn)):
+            if KERNEL in r["Kernel_Name"]:
+                vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    dur = {}
+    for fn in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(fn)):
+            if KERNEL in r["Kernel_Name"]:
+                dur[int(r["Dispatch_Id"])] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    return vals, dur
+
+
+def main():
+    out, W, H, bpp, skip = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), float(sys.argv[4]), int(sys.argv[5])
+    per = {}  # counter -> mean over the kept dispatches
+    n_kept = {}
+    clock = []
+    for d in sys.argv[6:]:
+        vals, dur = dispatches(d)
+        ids = sorted(vals)[skip:]
+        if not ids:
+            continue
+        names = set().union(*(vals[i].keys() for i in ids))
+        for c in names:
+            per[c] = sum(vals[i].get(c, 0.0) for i in ids) / len(ids)
+            n_kept[c] = len(ids)
+        if "GRBM_GUI_ACTIVE" in names:
+            for i in ids:
+                if dur.get(i):
+                    clock.append(vals[i]["GRBM_GUI_ACTIVE"] / 8.0 / dur[i])  # cycles per ns = GHz
+    res = {"kernel": KERNEL, "skipped_dispatches": skip, "dispatches_kept": n_kept, "counters": per,
+           "algorithmic_bytes_per_launch": W * H * bpp}
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        res["fetch_bytes_per_launch"] = 2.0 * per["FETCH_SIZE"] * 1024.0
+        res["write_bytes_per_launch"] = per["WRITE_SIZE"] * 1024.0
+        res["traffic_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
+        res["note"] = "FETCH_SIZE x2 (gfx950 16-B/lane read correction), WRITE_SIZE as reported; KiB -> bytes"
+    if "SQ_THREAD_CYCLES_VALU" in per:
+        res["valu"] = {c: per[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_ACTIVE_INST_VALU",
+                                           "SQ_THREAD_CYCLES_VALU") if c in per}
+        res["valu_lane_utilisation"] = per["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * per["SQ_ACTIVE_INST_VALU"])
+    if clock:
+        clock.sort()
+        res["clock_ghz_median"] = clock[len(clock) // 2]
+    if "SQ_WAVE_CYCLES" in per:
+        w = per["SQ_WAVE_CYCLES"] or 1.0
+        res["stall_share"] = {c: per[c] / w for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                                      "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_BUSY_CYCLES")
+                              if c in per}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "counters"}))
+
+
+if __name__ == "__main__":
+    main()
