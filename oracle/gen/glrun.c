@@ -85,6 +85,7 @@ typedef intptr_t GLsizeiptr;
 #define GL_STATIC_DRAW 0x88E4
 #define GL_TRIANGLES 0x0004
 #define GL_READ_FRAMEBUFFER 0x8CA8
+#define GL_SCISSOR_TEST 0x0C11
 
 #define F(ret, name, args) static ret(*p_##name) args;
 F(EGLDisplay, eglGetDisplay, (void *))
@@ -130,6 +131,8 @@ F(void, glBufferData, (GLenum, GLsizeiptr, const void *, GLenum))
 F(void, glEnableVertexAttribArray, (GLuint))
 F(void, glVertexAttribPointer, (GLuint, GLint, GLenum, GLboolean, GLsizei, const void *))
 F(void, glViewport, (GLint, GLint, GLsizei, GLsizei))
+F(void, glScissor, (GLint, GLint, GLsizei, GLsizei))
+F(void, glEnable, (GLenum))
 F(void, glDrawArrays, (GLenum, GLint, GLsizei))
 F(void, glReadPixels, (GLint, GLint, GLsizei, GLsizei, GLenum, GLenum, void *))
 F(void, glFinish, (void))
@@ -177,7 +180,7 @@ static void load(void) {
   L(gles, glCheckFramebufferStatus) L(gles, glDrawBuffers) L(gles, glReadBuffer)
   L(gles, glGenBuffers) L(gles, glBindBuffer) L(gles, glBufferData)
   L(gles, glEnableVertexAttribArray) L(gles, glVertexAttribPointer)
-  L(gles, glViewport) L(gles, glDrawArrays) L(gles, glReadPixels)
+  L(gles, glViewport) L(gles, glScissor) L(gles, glEnable) L(gles, glDrawArrays) L(gles, glReadPixels)
   L(gles, glFinish) L(gles, glGetError) L(gles, glPixelStorei)
 #undef L
 }
@@ -292,6 +295,7 @@ int main(int argc, char **argv) {
   const char *cube_file = NULL;
   int cube_size = 0;
   int temporal_frames = 5; /* index.js:258 default temporalFrames */
+  int sc[4] = {0, 0, 0, 0}; /* --scissor x y w h: only these fragments run (w = 0: all) */
   for (int i = 1; i < argc; i++) {
     if (!strcmp(argv[i], "--frag")) frag = argv[++i];
     else if (!strcmp(argv[i], "--out")) prefix = argv[++i];
@@ -312,6 +316,9 @@ int main(int argc, char **argv) {
     } else if (!strcmp(argv[i], "--cube")) { /* --cube SIZE file.rgb8 */
       cube_size = atoi(argv[++i]);
       cube_file = argv[++i];
+    }
+    else if (!strcmp(argv[i], "--scissor")) {
+      for (int k = 0; k < 4; k++) sc[k] = atoi(argv[++i]);
     }
     else if (!strcmp(argv[i], "--cam")) {
       for (int k = 0; k < 9; k++) cam[k] = (float)atof(argv[++i]);
@@ -402,6 +409,13 @@ int main(int argc, char **argv) {
   GLint time_loc = p_glGetUniformLocation(prog, "u_time");
   GLint tf_loc = p_glGetUniformLocation(prog, "u_temporalFrames");
   p_glViewport(0, 0, w, h);
+  /* A scissored tile: the same uniforms and fragment coordinates as the full
+   * image, only the tile's fragments are shaded (the executor does not finish
+   * some fragments of the volumetric shaders: one glrun per tile isolates them) */
+  if (sc[2] > 0 && sc[3] > 0) {
+    p_glEnable(GL_SCISSOR_TEST);
+    p_glScissor(sc[0], sc[1], sc[2], sc[3]);
+  }
 
   for (int pass = 1; pass <= frames; pass++) {
     p_glUseProgram(prog);

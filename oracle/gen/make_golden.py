@@ -23,6 +23,8 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -93,6 +95,8 @@ def run_config(glrun, cfgs, cfg):
         np.ascontiguousarray(img, np.uint8).tofile(fn)
         cmd += ["--tex", str(unit + 1), str(img.shape[1]), str(img.shape[0]), fn]
     skipped = []
+    if cfg.get("tiles"):
+        return run_tiled(cfg, cmd, prefix, W, H, restir, defs, consts)
     if cfg.get("frame_timeout"):
         # Per-frame mode (volumetric configs): SwiftShader 4.1 does not finish
         # some passes of these shaders (a pass of 8x8 pixels either renders in
@@ -130,6 +134,94 @@ def run_config(glrun, cfgs, cfg):
     return {"defines": defs, "constants": consts, "frames": ids, "skipped_frames": skipped, "width": W, "height": H,
             "restir": restir, "nan_pixels": nan,
             "mean_rgb": [float(x) for x in np.nanmean(out["samples"][..., :3], axis=(0, 1, 2))]}
+
+
+def swiftshader_dir(threads):
+    """A working directory whose SwiftShader.ini pins the executor's thread
+    count ([Processor] ThreadCount): SwiftShader reads it from the current
+    directory.  Default (no ini) = one thread per core."""
+    d = tempfile.mkdtemp(prefix="rt0_ss%d_" % threads)
+    with open(os.path.join(d, "SwiftShader.ini"), "w") as f:
+        f.write("[Processor]\nThreadCount=%d\n" % threads)
+    return d
+
+
+def run_tiled(cfg, cmd, prefix, W, H, restir, defs, consts):
+    """Tiled mode (deep volumetric configs): every (u_frame, tile) is its own
+    glrun call with glScissor on the tile and a time limit, run once per
+    SwiftShader thread count of cfg["thread_counts"].  A pixel is `valid` when
+    its tile finished in every run with the same value: the executor does not
+    finish some fragments of these shaders (a tile either renders in ~2 s or
+    runs for minutes), and in some branches it reads registers another quad
+    left behind, so a full-image render depends on the thread count (measured
+    on vol_cornell_2 u_frame 6: ThreadCount 2 changes pixel (x 2, y 6); 1, 3,
+    8 and 16 agree).  One 2x2 quad per call shares no registers with another."""
+    tw, th = cfg["tiles"]
+    frames = int(cfg["frames"])
+    tcs = cfg.get("thread_counts", [1, 3])
+    dirs = {t: swiftshader_dir(t) for t in tcs}
+    jobs = [(k, x, y) for k in range(1, frames + 1) for y in range(0, H, th) for x in range(0, W, tw)]
+
+    def run(k, x, y, t):
+        out = "%s_k%d_x%d_y%d_t%d" % (prefix, k, x, y, t)
+        try:
+            subprocess.run(cmd + ["--frames", "1", "--frame0", str(k), "--scissor", str(x), str(y), str(tw), str(th),
+                                  "--out", out], check=True, capture_output=True, cwd=dirs[t],
+                           timeout=float(cfg["tile_timeout"]))
+        except subprocess.TimeoutExpired:
+            return None
+        img = {"c": np.fromfile("%s_f%d_c.bin" % (out, k), dtype=np.float32).reshape(H, W, 4)}
+        if restir:
+            for tag in "ra":
+                img[tag] = np.fromfile("%s_f%d_%s.bin" % (out, k, tag), dtype=np.float32).reshape(H, W, 4)
+        for f in os.listdir(os.path.dirname(out)):
+            if f.startswith(os.path.basename(out) + "_"):
+                os.remove(os.path.join(os.path.dirname(out), f))
+        return img
+
+    def one(job):
+        """The tile under every thread count (stopping at the first run that
+        does not finish: one quad per call renders the same either way)."""
+        imgs = []
+        for t in tcs:
+            img = run(*job, t)
+            if img is None:
+                return job, None
+            imgs.append(img)
+        return job, imgs
+
+    workers = int(os.environ.get("RT0_GOLDEN_WORKERS", "6"))
+    with ThreadPoolExecutor(workers) as ex:
+        results = list(ex.map(one, jobs))
+    samples = np.zeros((frames, H, W, 4), np.float32)
+    valid = np.zeros((frames, H, W), bool)
+    aux = {tag: np.zeros((frames, H, W, 4), np.float32) for tag in ("ra" if restir else "")}
+    timed_out = 0
+    for (k, x, y), imgs in results:
+        sl = (k - 1, slice(y, y + th), slice(x, x + tw))
+        if imgs is None:
+            timed_out += 1
+            continue
+        tile = imgs[0]["c"][y:y + th, x:x + tw]
+        same = np.ones(tile.shape[:2], bool)
+        for other in imgs[1:]:
+            o = other["c"][y:y + th, x:x + tw]
+            same &= (o == tile).all(-1) | (np.isnan(o).all(-1) & np.isnan(tile).all(-1))
+        samples[sl] = tile
+        valid[sl] = same
+        for tag in aux:
+            aux[tag][sl] = imgs[0][tag][y:y + th, x:x + tw]
+    out = {"samples": samples, "valid": valid, "frames": np.arange(1, frames + 1, dtype=np.int32)}
+    if restir:
+        out["restir_main"], out["restir_aux"] = aux["r"], aux["a"]
+    name = cfg["name"]
+    np.savez_compressed(os.path.join(GOLD, name + ".npz"), **out)
+    v = samples[..., :3][valid]
+    return {"defines": defs, "constants": consts, "frames": list(range(1, frames + 1)), "width": W, "height": H,
+            "restir": restir, "tiles": [tw, th], "thread_counts": tcs, "tiles_timed_out": timed_out,
+            "tile_jobs": len(jobs), "valid_pixel_samples": int(valid.sum()),
+            "nan_pixels": int(np.isnan(v).any(-1).sum()) if v.size else 0,
+            "mean_rgb": [float(x) for x in (np.nanmean(v, axis=0) if v.size else [0, 0, 0])]}
 
 
 def run_kat(glrun, cfgs):

@@ -13,10 +13,12 @@
 #   BENCH=1|0         plain bench line per config
 #   PROFILE=1|0       rocprofv3 --kernel-trace of a bench run -> steady-state kernel time
 #   PMC=1|0           counter passes: FETCH_SIZE | WRITE_SIZE | VALU + GRBM clock | SQ stall split
+#                     (MIX=1 adds the VALU instruction-mix pass: ADD/MUL/FMA/TRANS/INT32/CVT)
 #   AB="name:VAR=val VAR2=val;name2:VAR=val"  bench every config under each
 #                     variant (env assignments), ROUNDS interleaved rounds, plus
 #                     the default ("base") in every round; AB_CONFIGS overrides CONFIGS
-#   CALIB=1           scripts/fetch_calib under rocprofv3 --pmc FETCH_SIZE
+#   CALIB=1           scripts/fetch_calib under rocprofv3 --pmc FETCH_SIZE, and
+#                     scripts/valu_peak (measured scalar / packed FP32 FMA peaks)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${OUT:-measure}
 mkdir -p "$O"
@@ -42,6 +44,9 @@ if [ "${CALIB:-0}" = "1" ]; then
     ./scripts/fetch_calib > "$O/calib.log" 2>&1
   rc=$?; echo "calib rc=$rc"; tail -2 "$O/calib.log"; stop_if_bad $rc
   python3 scripts/fetch_calib.py "$O/calib" "$O/calib.log" > "$O/calib.json"; cat "$O/calib.json"
+  # measured FP32 VALU peaks: scalar v_fma_f32 vs packed v_pk_fma_f32
+  timeout -k 10 60 ./scripts/valu_peak > "$O/valu_peak.json" 2>&1
+  rc=$?; echo "valu peak rc=$rc"; cat "$O/valu_peak.json"; stop_if_bad $rc
 fi
 
 for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do
@@ -65,7 +70,8 @@ for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do
     i=0; dirs=""
     for pass in "FETCH_SIZE" "WRITE_SIZE" \
         "SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
-        "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INSTS_SALU"; do
+        "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INSTS_SALU" \
+        ${MIX:+"SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU SQ_INSTS_SMEM"}; do
       i=$((i+1))
       timeout -s KILL 240 rocprofv3 --pmc $pass --kernel-trace --output-format csv -d "$O/pmc_${cfg}_$i" -o run -- $CMD > "$O/pmc_${cfg}_$i.log" 2>&1
       rc=$?; echo "pmc $cfg pass $i: rc=$rc"

@@ -84,6 +84,14 @@ def main():
         res["stall_share"] = {c: per[c] / w for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
                                                       "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_BUSY_CYCLES")
                               if c in per}
+    if "SQ_INSTS_VALU_FMA_F32" in per:
+        tot = per.get("SQ_INSTS_VALU") or 1.0
+        res["valu_mix"] = {c[len("SQ_INSTS_VALU_"):].lower(): per[c] / tot for c in per
+                           if c.startswith("SQ_INSTS_VALU_")}
+        # wave-level FP32 operations the hardware executed (FMA = 2): the
+        # ceiling the algorithmic FLOP model is compared against
+        res["hw_flop_wave_instr"] = 2.0 * per["SQ_INSTS_VALU_FMA_F32"] + per["SQ_INSTS_VALU_ADD_F32"] + \
+            per["SQ_INSTS_VALU_MUL_F32"]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "counters"}))
 

@@ -28,7 +28,9 @@ def run_bench(tmp_path, config, gpus, extra=()):
            "--warmup", "0", "--no-cpu-baseline", "--save-image", str(img)] + list(extra)
     env = dict(os.environ, RT0_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
+    if r.returncode != 0:  # the ranks' own tracebacks, not torch.distributed.run's summary
+        lines = [l for l in r.stderr.splitlines() if l.startswith("[rank") or "Error" in l]
+        raise AssertionError("bench.py --gpus %d failed:\n%s" % (gpus, "\n".join(lines[-40:]) or r.stderr[-3000:]))
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     return json.loads(line), np.load(img)
 
