@@ -104,7 +104,8 @@ class StreamOrder:
         self.t1.record()
 
     def elapsed_ms(self):
-        """t0 -> t1 on torch's stream (after a synchronisation)."""
+        """t0 -> t1 on torch's stream (waits for t1)."""
+        self.t1.synchronize()
         return self.t0.elapsed_time(self.t1)
 
 

@@ -83,7 +83,8 @@ NON_RESTIR = ["c1_cornell_cos", "c2_cornell_mis_refcaps", "c2_cornell_mis_8", "c
               "mis_demo_sdfbox", "menger_coat", "thinlens_glass", "c4_mandelbulb_vol", "spectral_vol_1l",
               "tex_sdf_metal", "tex_light_sphere", "tex_check_test", "cube_spheres", "cube_sdf_metal",
               "sdf_triprism", "sdf_cone", "spectral_cornell", "vol_cornell_2",
-              "page_scene0_slabfirst", "tex_check_assets", "page_scene1", "cube_spheres_assets"]
+              "page_scene0_slabfirst", "tex_check_assets", "page_scene1", "cube_spheres_assets",
+              "c4_mandelbulb_deep"]
 
 
 @pytest.mark.parametrize("name", NON_RESTIR)
@@ -97,11 +98,14 @@ def test_gpu_matches_reference_fixture(name, cfgs, gpu_required):
     frames = G["frames"] if "frames" in G else range(1, F + 1)
     r = make(cfgs, name, W, H)
     got = np.stack([single(r, int(k)) for k in frames])
+    # tiled fixtures: the pixels whose tile the executor finished, stable
+    # under two thread counts (oracle/gen/make_golden.py run_tiled)
+    valid = G["valid"] if "valid" in G else np.ones(gold.shape[:3], bool)
     ok, nan = pixel_match(got[..., :3], gold[..., :3])
-    bad = 1.0 - ok.mean()
+    bad = 1.0 - ok[valid].mean()
     assert bad <= BAD_FRAC.get(name, BAD_FRAC["default"]), "%s: %.4f of pixels differ" % (name, bad)
     assert not np.isnan(got).any()
-    m = ~nan
+    m = ~nan & valid
     g, s = gold[..., :3][m], got[..., :3][m]
     assert abs(s.mean() - g.mean()) <= MEAN_TOL.get(name, 5e-3) * max(1.0, abs(g.mean()))
 
