@@ -36,6 +36,28 @@ these rules):
      differently with their SDF statements swapped.
 The summary (per-pixel outputs of every case) is tests/golden/mask_kat.json.
 
+DEPARTURES (json key "departures"; run with SwiftShader ThreadCount=1, the
+executor being thread-count dependent): shaders whose GLSL ES
+3.00 result is known in closed form, recorded with it:
+  8. a `continue` in a loop whose body has a `break` AFTER it (the reference's
+     volumetric bounce loop: continue at raytracer.glsl:2050, breaks at 2057,
+     2065, 2089, 2101) retires the lane: continue_then_break renders 1 where
+     GLSL semantics give 31, on every pixel; the same loop without the later
+     break (continue_no_break) or with the break before the continue
+     (break_then_continue) is executed correctly.  How many lanes of the
+     reference's own loop the executor retires depends on the generated code
+     (in reference-shaped loops it varied with a compile-time constant), so
+     the restatement does not model it: volumetric scenes deeper than one
+     bounce are darker in the reference than under GLSL semantics
+     (c4_mandelbulb_deep: -9% mean radiance; the medium-free
+     c4_mandelbulb_deep_novol agrees to 0.1%);
+  9. the two-light in-scatter construct (raytracer.glsl:2011-2044 as
+     make_shader.js rewrites it, a light loop over the const light_index array
+     calling an intersection() with a mesh loop, inside radiance()'s loop with
+     lanes breaking at different iterations) is executed correctly
+     (inscatter_two_lights): the two-light departure is rule 8 (a scatter's
+     `continue` precedes every in-scatter loop of a later bounce).
+
 usage: python3 oracle/gen/mask_kat.py
 """
 import json
@@ -277,13 +299,113 @@ void main() {
 }
 
 
-def run_case(name, body):
+# rule 8/9 cases: name -> (body, GLSL ES 3.00 value of o0 per pixel (x, y))
+LOOP_FN = """
+float f() {
+  float acc = 0.0;
+  for (int d = 0; d < 5; ++d) {
+    int code = d == 0 ? 0 : ((d == 4) ? 3 : 1);
+    %s
+  }
+  return acc;
+}
+void main() {
+  g0 = 0.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = 0;
+  float loc = f();
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+"""
+INSCATTER = """
+struct Hit2 { int index; float t; };
+struct M { vec3 pos; float r; int t; };
+M meshes[3];
+const lowp int LIDX[2] = int[](1, 2);
+float isect(vec3 o, vec3 d, out Hit2 h) {
+  h.index = 0; float tmin = 1e4;
+  for (int i = 0; i < 3; i++) {
+    vec3 oc = o - meshes[i].pos; float b = dot(oc, d); float c = dot(oc, oc) - meshes[i].r * meshes[i].r;
+    float disc = b * b - c;
+    if (disc < 0.0) continue;
+    float t = -b - sqrt(disc);
+    if (t > 0.001 && t < tmin) { tmin = t; h.index = i; }
+  }
+  return tmin;
+}
+float radiance(vec3 p, int stop) {
+  float loc = 0.0;
+  for (int d = 0; d < 6; ++d) {
+    if (d == stop) break;
+    int num = int(LIDX.length());
+    for (int li = 0; li < num; ++li) {
+      int light_idx = int(LIDX[li]);
+      if (!(light_idx < 0)) {
+        M lm = meshes[light_idx];
+        if (!(lm.t != 0)) {
+          vec3 dir = normalize(lm.pos - p);
+          Hit2 sh;
+          float ts = isect(p, dir, sh);
+          if (!(sh.index != light_idx)) { loc += float(light_idx) * (float(d) * 10.0 + 1.0); }
+        }
+      }
+    }
+  }
+  return loc;
+}
+void main() {
+  meshes[0] = M(vec3(0.0, 0.0, 0.0), 1.0, 1);
+  meshes[1] = M(vec3(-3.0, 3.0, 0.0), 0.5, 0);
+  meshes[2] = M(vec3(3.0, 3.0, 0.0), 0.5, 0);
+  g0 = 0.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  int stop = stopOf(ivec2(gl_FragCoord.xy));
+  vec3 p = vec3(floor(gl_FragCoord.x) - 3.5, -2.0, floor(gl_FragCoord.y) - 3.5);
+  float loc = radiance(p, stop);
+  float o0 = loc, o1 = 0.0, o2 = 0.0, o3 = 0.0;
+"""
+
+
+def _inscatter_glsl(x, y):
+    """GLSL value of INSCATTER's o0 (float64 geometry: the visibility decisions are far from grazing)."""
+    ms = [(np.array([0.0, 0, 0]), 1.0), (np.array([-3.0, 3, 0]), 0.5), (np.array([3.0, 3, 0]), 0.5)]
+    p = np.array([x - 3.5, -2.0, y - 3.5])
+    lane, quad = (x & 1) + 2 * (y & 1), ((x >> 1) + (y >> 1)) & 3
+    stop = (lane * 3 + quad) % 5
+    per = 0
+    for L in (1, 2):
+        d = ms[L][0] - p
+        d /= np.linalg.norm(d)
+        tmin, idx = 1e4, 0
+        for i, (c, r) in enumerate(ms):
+            oc = p - c
+            b, cc = oc @ d, oc @ oc - r * r
+            if b * b - cc < 0:
+                continue
+            t = -b - np.sqrt(b * b - cc)
+            if 0.001 < t < tmin:
+                tmin, idx = t, i
+        per += L if idx == L else 0
+    return float(sum(per * (d * 10 + 1) for d in range(stop)))
+
+
+DEPARTURES = {
+    # rule 8: continue at d = 0, a break later in the body (taken at d = 4): GLSL 1 + 10 + 10 + 10 = 31
+    "continue_then_break": (LOOP_FN % "if (code == 0) { acc += 1.0; continue; }\n    if (code == 3) break;\n    acc += 10.0;",
+                            lambda x, y: 31.0),
+    # controls: no later break (41), the break before the continue (41)
+    "continue_no_break": (LOOP_FN % "if (code == 0) { acc += 1.0; continue; }\n    acc += 10.0;", lambda x, y: 41.0),
+    "break_then_continue": (LOOP_FN % "if (code == 0) { acc += 1.0; if (acc > 100.0) break; continue; }\n    acc += 10.0;",
+                            lambda x, y: 41.0),
+    # rule 9: the two-light in-scatter construct
+    "inscatter_two_lights": (INSCATTER, _inscatter_glsl),
+}
+
+
+def run_case(name, body, cwd=None):
     frag = os.path.join(GEN, name + ".frag")
     with open(frag, "w") as f:
         f.write(HEAD + body + EPILOGUE)
     prefix = os.path.join(GEN, name)
     subprocess.run([GLRUN, "--frag", frag, "--w", str(W), "--h", str(H), "--frames", "1", "--single",
-                    "--restir-out", "--out", prefix], check=True, capture_output=True, text=True)
+                    "--restir-out", "--out", prefix], check=True, capture_output=True, text=True, cwd=cwd)
 
     def load(tag):
         return np.fromfile("%s_f1_%s.bin" % (prefix, tag), dtype=np.float32).reshape(H, W, 4)
@@ -304,6 +426,18 @@ def main():
         print(name)
         for r in rows[:4]:
             print("   x=%d y=%d stop=%d g=%s o=%s" % (r["x"], r["y"], r["stop"], r["g"], r["o"]))
+    # departures from GLSL semantics, one executor thread (deterministic)
+    t1 = os.path.join(GEN, "threads1")
+    os.makedirs(t1, exist_ok=True)
+    with open(os.path.join(t1, "SwiftShader.ini"), "w") as f:
+        f.write("[Processor]\nThreadCount=1\n")
+    out["departures"] = {}
+    for name, (body, glsl) in DEPARTURES.items():
+        rows = run_case(name, body, cwd=t1)
+        out["departures"][name] = [{"x": r["x"], "y": r["y"], "exec": r["o"][0], "glsl": glsl(r["x"], r["y"])}
+                                   for r in rows]
+        bad = sum(1 for r in out["departures"][name] if r["exec"] != r["glsl"])
+        print("%s: %d of %d pixels depart from GLSL semantics" % (name, bad, len(rows)))
     with open(os.path.join(REPO, "tests", "golden", "mask_kat.json"), "w") as f:
         json.dump(out, f, separators=(",", ":"))
 

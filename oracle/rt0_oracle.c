@@ -184,6 +184,7 @@ typedef struct {
   int temporal_frames;
   /* 1 = model SwiftShader 4.1's masked-execution quirk (see radiance()) */
   int ghost;
+  int scatter0_exit; /* SWIFTSHADER_SCATTER0_EXIT: the executor's first-iteration `continue` (see radiance) */
   /* camera uniforms (index.js:421-423) */
   v3 cam_pos, cam_look, cam_params;
   /* asset textures (index.js:256-296): 0..3 u_tex0..3, 4 u_rnd_tex; RGBA8 */
@@ -1315,6 +1316,15 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         int stop = (F->scat_ev >= o->max_scatter || vmaxc(mask) < 0.01f);
         if (o->ghost) ghost_brdf(F, &regs, seed);
         if (stop) break;
+        /* SWIFTSHADER_SCATTER0_EXIT: the reference executor (SwiftShader 4.1)
+         * leaves the bounce loop at this `continue` (raytracer.glsl:2050) when
+         * it is executed in the loop's first iteration: the loop body has
+         * `break`s after it (2057, 2065, 2089, 2101) and the executor's
+         * continue mask then also retires the lane.  Pinned by
+         * oracle/gen/mask_kat.py case continue_then_break (a lane that
+         * continues at iteration 0 ends with one iteration's contribution;
+         * at later iterations the same continue is honoured). */
+        if (o->scatter0_exit && depth == 0) break;
         continue;
       }
     }
@@ -1601,6 +1611,7 @@ int or_set_constant(void *h, const char *name, double v) {
   else if (!strcmp(name, "RESTIR_SAMPLES")) o->restir_samples = iv;
   else if (!strcmp(name, "LIGHT_PATH_LENGTH")) { /* unused by the shader */ }
   else if (!strcmp(name, "SWIFTSHADER_GHOST")) o->ghost = iv;
+  else if (!strcmp(name, "SWIFTSHADER_SCATTER0_EXIT")) o->scatter0_exit = iv;
   else if (!strcmp(name, "RENDER_MODE")) {
     o->render_mode = iv;
     if (iv != 0 && iv != 1) { snprintf(o->err, sizeof o->err, "RENDER_MODE must be 0 or 1"); return -1; }

@@ -77,6 +77,23 @@ struct BvhNode {
 #define RT0_BVH_STACK 48  // traversal stack entries per lane (LDS); the build checks the bound
 #endif
 
+// Deferred light sampling (ReSTIR scenes, scene-specialised kernels): the
+// pass kernel appends one NeeRec per sampleLightsReSTIR call instead of
+// running it (its result only adds to the path's radiance; the path's next
+// direction does not depend on it), rt0_jit_nee evaluates the records densely
+// -- every lane has one -- and rt0_jit_resolve adds them to the pixel's
+// sample in bounce order.  64 B, appended per wave (contiguous, coalesced).
+struct NeeRec {
+  float x, y, z;     // the shading point (hit.pos)
+  float nx, ny, nz;  // nl
+  float sx, sy;      // sampleLightsReSTIR's two seeds (raytracer.glsl:1909/1943)
+  float mr, mg, mb;  // the path's mask at the call
+  int32_t pix;       // image pixel (y * W + x)
+  int32_t mat;       // the hit mesh (material of the shading point)
+  int32_t k;         // the call's index along the path (0-based)
+  int32_t pad;
+};
+
 struct SceneDev {
   int32_t n_meshes, n_sdfs, n_lights, n_total;
   int32_t n_models;  // TRIANGLE entries: geom/mat[n_meshes + n_sdfs + k]
@@ -163,5 +180,14 @@ struct LaunchParams {
   // getAnimatedPosition(meshes[i].pos, i, u_time) (263-298), evaluated once
   // per launch on the host (it is uniform over the image).  Unused otherwise.
   float ema_alpha;
+  // deferred light sampling (NeeRec): defer != 0 routes sampleLightsReSTIR
+  // calls into nee_rec[*nee_count++] (capacity nee_cap); results go to
+  // nee_out[k * width * height + pix]; nee_partial[pix] = (the path's radiance
+  // without them, hero wavelength), nee_n[pix] = its number of calls
+  int32_t defer, nee_cap;
+  NeeRec *nee_rec;
+  uint32_t *nee_count;
+  float4 *nee_out, *nee_partial;
+  int32_t *nee_n;
   float4 apos[RT0_MAX_MESH];
 };

@@ -97,8 +97,18 @@ struct rt0_ctx {
   bool exec_compat = false;  // rt0_set_executor_compat: F_EXEC_GHOST
   // the scene-specialised kernel of the current (scene, config): looked up once
   // per change instead of regenerating and hashing its source on every render
-  void *jit_fn = nullptr;
+  rt0h::JitFns jit;
   bool jit_dirty = true;
+  // deferred ReSTIR light sampling (RT0_DEFER_NEE, default on): the calls one
+  // pass appends (NeeRec), their results (one float4 plane per call index),
+  // the paths' own radiance + hero wavelength, and the calls per pixel
+  bool defer_nee = true;
+  NeeRec *d_nee_rec = nullptr;
+  uint32_t *d_nee_count = nullptr;
+  float4 *d_nee_out = nullptr, *d_nee_partial = nullptr;
+  int32_t *d_nee_n = nullptr;
+  size_t nee_slots = 0;  // records d_nee_rec holds (W x H x calls per pixel)
+  size_t nee_pixels = 0;
   std::string jit_err;
   std::string err;
 };
@@ -157,6 +167,7 @@ int rt0_create(int width, int height, int device, rt0_ctx **out) {
   rt0_ctx *c = new rt0_ctx();
   c->device = device;
   if (const char *e = getenv("RT0_JIT")) c->use_jit = atoi(e) != 0;
+  if (const char *e = getenv("RT0_DEFER_NEE")) c->defer_nee = atoi(e) != 0;
   rt0h::default_config(c->cfg);
   int rc;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -185,6 +196,9 @@ void rt0_destroy(rt0_ctx *c) {
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_halo_miss) (void)hipFree(c->d_halo_miss);
   if (c->d_samples) (void)hipFree(c->d_samples);
+  for (void *q : {(void *)c->d_nee_rec, (void *)c->d_nee_count, (void *)c->d_nee_out, (void *)c->d_nee_partial,
+                  (void *)c->d_nee_n})
+    if (q) (void)hipFree(q);
   for (auto &t : c->d_tex)
     if (t) (void)hipFree(t);
   if (c->d_cube) (void)hipFree(c->d_cube);
@@ -651,17 +665,54 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   // scene-specialised kernel (compiled once per scene/config, cached); the
   // counting instance is always the ahead-of-time one
   void *jit_fn = nullptr;
+  // ReSTIR light sampling in its own kernel over the pass's appended calls
+  // (rt0_integrator.h nee_body): scene-specialised kernels only; the executor
+  // ghost (F_EXEC_GHOST) keeps the inline calls
+  const bool defer = restir && c->use_jit && !c->counting && !c->exec_compat && c->defer_nee && p.max_bounces > 0;
   if (c->use_jit && !c->counting) {
-    if (c->jit_dirty || !c->jit_fn) {
+    if (c->jit_dirty || !c->jit.pass || (defer != (c->jit.nee != nullptr))) {
       rt0h::JitKey key = rt0h::make_jit_key(c->cfg, c->n_sdfs);
       if (c->exec_compat) key.flags |= F_EXEC_GHOST;
       key.halo_check = c->n_shards > 1 ? 1 : 0;
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
-      int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit_fn, c->jit_err);
+      key.defer = defer ? 1 : 0;
+      int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
       c->jit_dirty = false;
     }
-    jit_fn = c->jit_fn;
+    jit_fn = c->jit.pass;
+  }
+  unsigned nee_grid = 0;
+  if (defer) {
+    // one record per (pixel, call): a path makes at most one light-sampling
+    // call per bounce (rt0_integrator.h step)
+    const size_t pixels = (size_t)c->W * c->H, slots = pixels * (size_t)p.max_bounces;
+    if (slots > 0x7fffffffu) return fail(c, RT0_E_UNSUPPORTED, "deferred light sampling: too many records");
+    if (slots > c->nee_slots || pixels != c->nee_pixels) {
+      for (void **q : {(void **)&c->d_nee_rec, (void **)&c->d_nee_out, (void **)&c->d_nee_partial,
+                       (void **)&c->d_nee_n}) {
+        if (*q) HIPCHK(c, hipFree(*q));
+        *q = nullptr;
+      }
+      c->nee_slots = c->nee_pixels = 0;
+      HIPCHK(c, hipMalloc(&c->d_nee_rec, slots * sizeof(NeeRec)));
+      HIPCHK(c, hipMalloc(&c->d_nee_out, slots * sizeof(float4)));
+      HIPCHK(c, hipMalloc(&c->d_nee_partial, pixels * sizeof(float4)));
+      HIPCHK(c, hipMalloc(&c->d_nee_n, pixels * sizeof(int32_t)));
+      if (!c->d_nee_count) HIPCHK(c, hipMalloc(&c->d_nee_count, sizeof(uint32_t)));
+      c->nee_slots = slots;
+      c->nee_pixels = pixels;
+    }
+    p.defer = 1;
+    p.nee_cap = (int32_t)slots;
+    p.nee_rec = c->d_nee_rec;
+    p.nee_count = c->d_nee_count;
+    p.nee_out = c->d_nee_out;
+    p.nee_partial = c->d_nee_partial;
+    p.nee_n = c->d_nee_n;
+    // grid-stride over the records: ~16 waves per SIMD whatever the count
+    const size_t lanes = (size_t)(p.vp_x1 - p.vp_x0) * (p.vp_y1 - p.vp_y0) * 2;
+    nee_grid = (unsigned)std::max<size_t>(1, std::min<size_t>(4096, (lanes + 255) / 256));
   }
   auto launch = [&](const LaunchParams &lp, unsigned gz, dim3 g) -> hipError_t {
     if (jit_fn) return rt0h::jit_launch(jit_fn, &lp, g.x, g.y, gz, c->stream) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
@@ -682,8 +733,19 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       p.rin[5] = c->d_restir[R_H2A];
       p.rout_main = c->d_restir[R_OUT_MAIN];
       p.rout_aux = c->d_restir[R_OUT_AUX];
-      HIPCHK(c, launch(p, 1, grid));
-      launches++;
+      if (defer) {
+        HIPCHK(c, hipMemsetAsync(c->d_nee_count, 0, sizeof(uint32_t), c->stream));
+        HIPCHK(c, launch(p, 1, grid));
+        HIPCHK(c, rt0h::jit_launch(c->jit.nee, &p, nee_grid, 1, 1, c->stream) == RT0_OK ? hipSuccess
+                                                                                            : hipErrorLaunchFailure);
+        HIPCHK(c, rt0h::jit_launch(c->jit.resolve, &p, grid.x, grid.y, 1, c->stream) == RT0_OK
+                      ? hipSuccess
+                      : hipErrorLaunchFailure);
+        launches += 3;
+      } else {
+        HIPCHK(c, launch(p, 1, grid));
+        launches++;
+      }
       // swapReSTIRBuffers, index.js:795-820
       float4 **R = c->d_restir;
       float4 *o2 = R[R_H2], *o2a = R[R_H2A];

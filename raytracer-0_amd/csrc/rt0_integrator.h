@@ -88,6 +88,11 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_HALO_CHECK
 #define RT0_HALO_CHECK 1
 #endif
+// Deferred light sampling for ReSTIR scenes (NeeRec, rt0_device.h): the
+// scene-specialised kernels of ReSTIR scenes are compiled with 1 (rt0_jit.cpp)
+#ifndef RT0_DEFER_NEE
+#define RT0_DEFER_NEE 0
+#endif
 // ReSTIR reservoir taps fetched per batch (temporal levels together, spatial
 // taps RT0_TAP_BATCH at a time); 1 = one tap at a time.  The scene-specialised
 // kernels of ReSTIR scenes without models use 2 (rt0_jit.cpp)
@@ -1081,6 +1086,9 @@ struct Integrator {
   // spatial taps, BVH nodes / triangle tests (rt0_read_counters_n [5..10])
   unsigned long long n_restir = 0, n_cand = 0, n_ttap = 0, n_stap = 0, n_bvh[2] = {0, 0};
   Res fin;  // g_final_reservoir (raytracer.glsl:1616)
+  // deferred light sampling (P.defer): this sample's image pixel and the
+  // number of sampleLightsReSTIR calls it has deferred so far
+  int32_t nee_pix = 0, nee_k = 0;
   // F_EXEC_GHOST: brdf()'s parameter registers as the lane's last live call
   // left them (see ghost_brdf)
   v3 gr_x, gr_nl, gr_rd;
@@ -1595,6 +1603,50 @@ struct Integrator {
     return mk(0.f, 0.f, 0.f);
   }
 
+  // Does sample_lights() route this call to sampleLightsReSTIR (raytracer.
+  // glsl:1900-1946)?  use_restir without use_mis, or use_mis with more than 8
+  // lights; never in the counting instance (its event counts stay inline)
+  DEV bool restir_routed() const {
+    if constexpr (!RESTIR || COUNT) return false;
+    if (!flag(F_RESTIR) || !flag(F_RESTIR_DEF)) return false;
+    return !flag(F_MIS) || sc.n_lights() > 8;
+  }
+  // P.defer: append the call as a NeeRec (one atomic per wave: the active
+  // lanes take consecutive slots) instead of running it; rt0_jit_nee runs it
+  // with the same arguments and rt0_jit_resolve adds result * mask to the
+  // sample.  The seeds are the ones sample_lights() passes (1909/1943).
+  DEV void defer_nee(v3 x, v3 nl, int mi, float seed, float bounce, v3 mask) {
+    const float fr = (float)frame;
+    const unsigned long long act = __ballot(1);
+    const int lane = (int)(threadIdx.x & 63u);
+    const int leader = __ffsll((long long)act) - 1;
+    const int rank = __popcll(act & ((1ull << lane) - 1ull));
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(P.nee_count, (uint32_t)__popcll(act));
+    base = __shfl(base, leader);
+    const uint32_t i = base + (uint32_t)rank;
+    if (i < (uint32_t)P.nee_cap) {  // the host sizes nee_cap for MAX_DIFF_BOUNCES calls per pixel
+      NeeRec r;
+      r.x = x.x;
+      r.y = x.y;
+      r.z = x.z;
+      r.nx = nl.x;
+      r.ny = nl.y;
+      r.nz = nl.z;
+      r.sx = nc_seed3(seed, 8652.1f, fr, bounce, 7895.13f);
+      r.sy = nc_seed3(seed, 1234.567f, fr, bounce, 9876.54f);
+      r.mr = mask.x;
+      r.mg = mask.y;
+      r.mb = mask.z;
+      r.pix = nee_pix;
+      r.mat = mi;
+      r.k = nee_k;
+      r.pad = 0;
+      P.nee_rec[i] = r;
+    }
+    ++nee_k;
+  }
+
   // Non-specular light sampling dispatch, raytracer.glsl:1899-1976
   DEV v3 sample_lights(v3 x, v3 nl, const MatRec &mat, float seed, float bounce) {
     const float fr = (float)frame;
@@ -2055,7 +2107,14 @@ struct Integrator {
       }
       return end ? false : ++ps.depth < C.max_bounces();
     }
-    if (!spec && flag(F_SAMPLE_LIGHTS)) acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;
+    if (!spec && flag(F_SAMPLE_LIGHTS)) {
+      if constexpr (RT0_DEFER_NEE && RESTIR && !COUNT) {
+        if (restir_routed()) defer_nee(x, nl, hit.index, seed, bounce, mask);
+        else acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;
+      } else {
+        acc = acc + sample_lights(x, nl, mt, seed, bounce) * mask;
+      }
+    }
     // ---- end brdf
     if (ghost_on()) {
       gr_have = true;
@@ -2122,6 +2181,7 @@ struct Integrator {
     if (RESTIR) {
       fin = empty_res();
       gr_have = false;
+      nee_k = 0;
     }
     ps = Path{ro, rd, mk(0.f, 0.f, 0.f), mk(1.f, 1.f, 1.f), mk(0.f, 1.f, 0.f), seed, 0, true};
   }
@@ -2235,6 +2295,19 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     }
   } else if constexpr (!RESTIR && !COUNT) {
     regen_pixel(P, it, cfg, px, py, apix);
+  } else if constexpr (RT0_DEFER_NEE && RESTIR && !COUNT) {
+    // the path without its deferred sampleLightsReSTIR calls; rt0_jit_resolve
+    // completes the sample and accumulates it
+    it.frame = P.frame0;
+    it.nee_pix = (int32_t)pix;
+    typename decltype(it)::Path ps;
+    it.begin(ps, px, py);
+    if (cfg.max_bounces() > 0)
+      while (it.step(ps)) {
+      }
+    P.nee_partial[pix] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, it.hero);
+    P.nee_n[pix] = it.nee_k;
+    if (it.nee_k > 0) return;  // g_final_reservoir is the last deferred call's: rt0_jit_nee writes it
   } else {
     float4 a = P.accum[apix];
     for (int f = 0; f < P.nframes; ++f) {
@@ -2267,6 +2340,74 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     atomicAdd(&P.counters[9], it.n_bvh[0]);
     atomicAdd(&P.counters[10], it.n_bvh[1]);
   }
+}
+
+// The deferred sampleLightsReSTIR calls of one pass (rt0_jit_nee): every lane
+// takes records off the list the pass kernel appended (grid-stride), so the
+// candidates, reservoir taps and visibility rays run on full waves whatever
+// the paths' lengths.  Same arguments, same arithmetic as the inline call;
+// the last call of a pixel writes its reservoir MRTs (g_final_reservoir,
+// raytracer.glsl:2171-2174).
+template <class Scene, class Cfg, bool VOL, bool SDF, bool SPECTRAL>
+DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  const uint32_t n = min(*P.nee_count, (uint32_t)P.nee_cap);
+  const size_t plane = (size_t)P.width * P.height;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const NeeRec r = P.nee_rec[i];
+    Integrator<Scene, Cfg, true, VOL, SDF, SPECTRAL, false> it(P, sc, cfg);
+    it.frame = P.frame0;
+    const int py = r.pix / P.width, px = r.pix - py * P.width;
+    it.fcx = (float)px + 0.5f;
+    it.fcy = (float)py + 0.5f;
+    it.fin = empty_res();
+    it.gr_have = false;
+    const v3 c = it.restir(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), sc.mat(r.mat), r.sx, r.sy);
+    P.nee_out[(size_t)r.k * plane + r.pix] = make_float4(c.x * r.mr, c.y * r.mg, c.z * r.mb, 0.f);
+    if (r.k == P.nee_n[r.pix] - 1 && P.rout_main != nullptr && P.rout_aux != nullptr) {
+      const Res &q = it.fin;
+      P.rout_main[r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
+      P.rout_aux[r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+    }
+  }
+}
+
+// Completes the samples of a deferred pass (rt0_jit_resolve): the path's own
+// radiance plus its light-sampling results in call order, main()'s spectral
+// weighting (2152-2155), then the accumulator (2157-2169).  Same tile grid as
+// pass_body.
+template <class Scene, class Cfg, bool SPECTRAL>
+DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int px = P.vp_x0 + (int)blockIdx.x * 16 + (lane & 7) + ((wave & 1) << 3);
+  const int r = P.vp_y0 + (int)blockIdx.y * 16 + (lane >> 3) + ((wave >> 1) << 3);
+  if (px >= P.vp_x1 || r >= P.vp_y1) return;
+  const int py = image_row(P, r);
+  if (py >= P.height) return;
+  const size_t pix = (size_t)py * P.width + px;
+  const size_t apix = P.compact ? (size_t)r * P.width + px : pix;
+  const size_t plane = (size_t)P.width * P.height;
+  const float4 part = P.nee_partial[pix];
+  const int n = P.nee_n[pix];
+  v3 col = mk(part.x, part.y, part.z);
+  for (int k = 0; k < n; ++k) {
+    const float4 o = P.nee_out[(size_t)k * plane + pix];
+    col = col + mk(o.x, o.y, o.z);
+  }
+  if constexpr (SPECTRAL) {
+    if (cfg.flags() & F_SPECTRAL) col = col * wavelength_to_rgb(part.w);
+  }
+  float4 a = P.accum[apix];
+  if (cfg.flags() & F_ANIM) {
+    a.x = mixf(a.x, col.x, P.ema_alpha);
+    a.y = mixf(a.y, col.y, P.ema_alpha);
+    a.z = mixf(a.z, col.z, P.ema_alpha);
+  } else {
+#pragma clang fp contract(off)
+    a.x += col.x;
+    a.y += col.y;
+    a.z += col.z;
+  }
+  P.accum[apix] = a;
 }
 
 // Frame-chunked launches: accumulator += samples of frames 0..nframes-1 in

@@ -64,6 +64,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // per workgroup would cap a CU at three workgroups
   if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
   o << "#define RT0_HALO_CHECK " << k.halo_check << "\n";
+  if (k.defer) o << "#define RT0_DEFER_NEE 1\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
   // occupancy target below); with a BVH the extra registers cost more than
@@ -130,30 +131,49 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     << "; }\n  __device__ static constexpr int restir_samples() { return " << k.restir_samples
     << "; }\n  __device__ static constexpr float fudge() { return " << fl(k.fudge) << "; }\n};\n";
   o << "}  // namespace rt0\n";
+  const char *rt = k.restir ? "true" : "false", *vol = k.vol ? "true" : "false", *sdf = k.sdf ? "true" : "false",
+             *spc = k.spectral ? "true" : "false";
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
-  if (const char *w = getenv("RT0_JIT_WAVES_PER_EU"))  // tuning knob: occupancy target
-    o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w) << "))) ";
   // occupancy targets measured per kernel family (scripts/ab_configs.sh, ab_c5.sh,
   // gpu_ab_taps.sh): BVH traversal is load-latency bound -- C5 4096^2 129.9 ms
   // (3 waves/SIMD: 131 VGPRs and a 48-entry LDS stack) -> 78.3 ms at 6; the
   // ReSTIR kernel with batched taps at 4 (128 VGPRs; at 5 it spills: C3 0.85
   // ms per pass, at 3 0.65, at 4 0.60); the quadric/SDF kernels already sit at
-  // <= 64 VGPRs (8 waves) and are left alone
+  // <= 64 VGPRs (8 waves) and are left alone.  A deferred ReSTIR pass kernel
+  // holds no reservoir code and is left to the compiler unless it walks a BVH;
+  // its light-sampling kernel takes the ReSTIR targets.
+  const char *w_env = getenv("RT0_JIT_WAVES_PER_EU");  // tuning knobs: occupancy targets
+  const char *wn_env = getenv("RT0_JIT_NEE_WAVES_PER_EU");
+  if (w_env)
+    o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w_env) << "))) ";
   else if (s.n_models > 0)
     o << "__attribute__((amdgpu_waves_per_eu(6))) ";
-  else if (k.restir)
+  else if (k.restir && !k.defer)
     o << "__attribute__((amdgpu_waves_per_eu(4))) ";
   o << "void rt0_jit_pass(const LaunchParams P) {\n"
        "  rt0::pass_body<rt0::JitScene, rt0::JitCfg, "
-    << (k.restir ? "true" : "false") << ", " << (k.vol ? "true" : "false") << ", " << (k.sdf ? "true" : "false")
-    << ", " << (k.spectral ? "true" : "false")
-    << ", false>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    << rt << ", " << vol << ", " << sdf << ", " << spc << ", false>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+  if (k.defer) {
+    o << "extern \"C\" __global__ __launch_bounds__(256) ";
+    if (wn_env)
+      o << "__attribute__((amdgpu_waves_per_eu(" << atoi(wn_env) << "))) ";
+    else if (s.n_models > 0)
+      o << "__attribute__((amdgpu_waves_per_eu(6))) ";
+    else
+      o << "__attribute__((amdgpu_waves_per_eu(4))) ";
+    o << "void rt0_jit_nee(const LaunchParams P) {\n"
+         "  rt0::nee_body<rt0::JitScene, rt0::JitCfg, "
+      << vol << ", " << sdf << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_resolve(const LaunchParams P) {\n"
+         "  rt0::resolve_body<rt0::JitScene, rt0::JitCfg, "
+      << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+  }
   return o.str();
 }
 
 struct CacheEntry {
   hipModule_t mod = nullptr;
-  hipFunction_t fn = nullptr;
+  JitFns fns;
 };
 static std::mutex g_mu;
 static std::map<std::pair<uint64_t, int>, CacheEntry> g_cache;
@@ -264,26 +284,34 @@ int jit_compile(const std::string &src, std::vector<char> &code, std::string &er
   return RT0_OK;
 }
 
-int jit_get(const SceneDev &s, const JitKey &k, int device, void **fn_out, std::string &err) {
+int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::string &err) {
   std::string src = jit_source(s, k);
   uint64_t h = fnv1a(src);
   std::lock_guard<std::mutex> lock(g_mu);
   auto it = g_cache.find({h, device});
   if (it != g_cache.end()) {
-    *fn_out = (void *)it->second.fn;
+    *fns = it->second.fns;
     return RT0_OK;
   }
   std::vector<char> code;
   int rc = jit_compile(src, code, err);
   if (rc != RT0_OK) return rc;
   CacheEntry e;
-  if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess ||
-      hipModuleGetFunction(&e.fn, e.mod, "rt0_jit_pass") != hipSuccess) {
+  hipFunction_t f[3] = {};
+  bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess &&
+            hipModuleGetFunction(&f[0], e.mod, "rt0_jit_pass") == hipSuccess;
+  if (ok && k.defer)
+    ok = hipModuleGetFunction(&f[1], e.mod, "rt0_jit_nee") == hipSuccess &&
+         hipModuleGetFunction(&f[2], e.mod, "rt0_jit_resolve") == hipSuccess;
+  if (!ok) {
     err = "hipModuleLoadData/GetFunction failed for the JIT module";
     return RT0_E_HIP;
   }
+  e.fns.pass = (void *)f[0];
+  e.fns.nee = (void *)f[1];
+  e.fns.resolve = (void *)f[2];
   g_cache[{h, device}] = e;
-  *fn_out = (void *)e.fn;
+  *fns = e.fns;
   return RT0_OK;
 }
 
@@ -400,7 +428,11 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
   std::vector<char> code;
   if (rc == RT0_OK) {
     SceneDev s = rt0h::make_scene_dev(m.data(), ne, ns, nm, l.data(), (int)l.size());
-    rc = rt0h::jit_compile(rt0h::jit_source(s, rt0h::make_jit_key(*cfg, ns)), code, e);
+    rt0h::JitKey key = rt0h::make_jit_key(*cfg, ns);
+    // the kernels rt0_render launches: deferred light sampling for ReSTIR (rt0_host.cpp)
+    const char *d = getenv("RT0_DEFER_NEE");
+    key.defer = key.restir && key.max_bounces > 0 && (!d || atoi(d) != 0);
+    rc = rt0h::jit_compile(rt0h::jit_source(s, key), code, e);
   }
   if (code_size) *code_size = code.size();
   if (err && err_len) {

@@ -19,6 +19,13 @@ struct JitKey {
   bool restir, vol, sdf, spectral;
   int bvh_stack = 0;  // LDS traversal stack entries (push bound + 1) when the scene has models
   int halo_check = 1;  // RT0_HALO_CHECK: sharded launches count reservoir fetches outside the halo
+  int defer = 0;       // RT0_DEFER_NEE: ReSTIR light sampling in its own kernel (rt0_jit_nee + rt0_jit_resolve)
+};
+
+// The kernels of one compiled module: the pass kernel and, for a deferred
+// ReSTIR key, the light-sampling and resolve kernels (hipFunction_t each).
+struct JitFns {
+  void *pass = nullptr, *nee = nullptr, *resolve = nullptr;
 };
 
 std::string jit_source(const SceneDev &s, const JitKey &k);
@@ -29,8 +36,8 @@ JitKey make_jit_key(const rt0_config &c, int n_sdfs);
 // flatten validated mesh records into the device scene layout
 SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, int nm, const int32_t *li, int nl);
 // Compile (or fetch from the process cache) the kernel for this scene/config on
-// `device`; *fn receives a hipFunction_t.
-int jit_get(const SceneDev &s, const JitKey &k, int device, void **fn, std::string &err);
+// `device`.
+int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::string &err);
 int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, unsigned gz, void *stream);
 
 }  // namespace rt0h

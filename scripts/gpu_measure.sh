@@ -8,7 +8,7 @@
 #
 # Env (all optional):
 #   OUT=name          results under gpurun_out/<name>/
-#   TESTS=1|0         python -m pytest tests -m gpu (PYTEST_ARGS appended)
+#   TESTS=1|0         python -m pytest tests -m gpu (PYTEST_K = a -k expression)
 #   CONFIGS="c2 c1 c3 c4 c5"   STEPS=5 WARMUP=2
 #   BENCH=1|0         plain bench line per config
 #   PROFILE=1|0       rocprofv3 --kernel-trace of a bench run -> steady-state kernel time
@@ -35,7 +35,7 @@ declare -A LPS=([c1]=1 [c2]=1 [c2_refcaps]=1 [c3]=16 [c4]=1 [c5]=4)  # pass laun
 
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider \
-    ${PYTEST_ARGS:-} > "$O/pytest_gpu.log" 2>&1
+    ${PYTEST_K:+-k "$PYTEST_K"} > "$O/pytest_gpu.log" 2>&1
   rc=$?; tail -25 "$O/pytest_gpu.log"; stop_if_bad $rc
 fi
 

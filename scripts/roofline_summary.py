@@ -1,67 +1,127 @@
-"""Per-workload roofline table from a profile directory written by
-scripts/gpu_round2.sh (bench_<c>.json, kernel_stats_<c>.csv from
-rocprofv3 --kernel-trace --stats, pmc_<c>.json from scripts/pmc_traffic.py).
+#!/usr/bin/env python3
+"""Per-workload roofline table from the files scripts/gpu_measure.sh writes
+(profiles/r03/: bench_<c>.json, kt_<c>.json, prof_<c>.json, pmc_<c>.json,
+calib.json, valu_peak.json).
 
-frac is recomputed from the rocprof average duration of the scene-specialised
-pass kernel (rt0_jit_pass), not from bench.py's live HIP-event time:
-  achieved = FLOP/sample (bench.py's model x counted events) x samples per
-             launch / rocprof average launch duration
-VALU issue utilisation = (SQ_INSTS_VALU x 2 + SQ_INSTS_VALU_TRANS_F32 x 2) SIMD
-cycles / (1024 SIMDs x launch duration x 2.4 GHz) (wave64 VALU = 2 passes on a
-SIMD32-wide datapath; transcendentals quarter rate -> 4 cycles).
-usage: python scripts/roofline_summary.py profiles/r02/s2 > profiles/r02/s2/roofline.md
+    python3 scripts/roofline_summary.py profiles/r03 > profiles/r03/roofline.md
+
+For every workload:
+  * kernel time: the MEDIAN rocprofv3 duration of rt0_jit_pass over the timed
+    steps of a profiled bench run (warm-up launches dropped: kt_summary.py),
+    cross-checked against that run's own ms_per_step (kernel ms x launches per
+    step must not exceed it) and against the plain run's HIP-event time;
+  * achieved = FLOP/sample (bench.py: SURVEY 8d model x counted events of the
+    timed frame window) x samples per launch / median kernel time; frac against
+    the 157.3 TF spec (packed v_pk_fma_f32) and against the MEASURED scalar
+    v_fma_f32 peak of scripts/valu_peak (the compiler emits scalar FMA for this
+    kernel: -fno-slp-vectorize);
+  * VALU issue utilisation at the MEASURED clock (GRBM_GUI_ACTIVE / 8 / time):
+    (2 x SQ_INSTS_VALU + 2 x SQ_INSTS_VALU_TRANS_F32) SIMD cycles / (1024 SIMDs
+    x kernel cycles);
+  * HBM traffic: FETCH_SIZE x 1024 B x the calibrated factor of the access
+    shape (scripts/fetch_calib: 16-B/lane stream x2, 64-B gathers x1, bilinear
+    2x2 RGBA32F taps x0.5) + WRITE_SIZE.  A kernel that mixes shapes gets its
+    accumulator stream at x2 and the rest at the factor of its dominant shape
+    (ReSTIR taps x0.5 for C3; C5: reported as the range x0.5 .. x2), over the
+    median kernel time -> GB/s and the fraction of 8 TB/s.
 """
-import csv
 import json
 import os
 import sys
 
-PEAK = 157.3
+PEAK_SPEC = 157.3
 D = sys.argv[1]
+
+
+def load(name):
+    p = os.path.join(D, name)
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+calib = load("calib.json") or {}
+fac = {k: (v["factor"][-1] if v.get("factor") else None) for k, v in calib.items()}
+vp = {}
+if os.path.exists(os.path.join(D, "valu_peak.json")):
+    for line in open(os.path.join(D, "valu_peak.json")):
+        if line.startswith("{"):
+            d = json.loads(line)
+            vp[d["kernel"]] = d["tflops"]
+PEAK_SCALAR = vp.get("v_fma_f32", 78.6)
+
 rows = []
 for c in ("c1", "c2", "c3", "c4", "c5"):
-    try:
-        b = json.load(open(os.path.join(D, "bench_%s.json" % c)))
-    except FileNotFoundError:
+    b, kt, pr, pmc = load("bench_%s.json" % c), load("kt_%s.json" % c), load("prof_%s.json" % c), load("pmc_%s.json" % c)
+    if not (b and kt):
         continue
-    ks = {}
-    with open(os.path.join(D, "kernel_stats_%s.csv" % c)) as f:
-        for r in csv.DictReader(f):
-            ks[r["Name"]] = r
-    k = ks.get("rt0_jit_pass")
-    avg_ns = float(k["AverageNs"]) if k else float("nan")
+    R = b["roofline"]
     cfg = b["config"]
-    # pass-kernel launches per step: the profiled command runs 1 warm-up + 2
-    # steps (scripts/gpu_round2.sh); a frame-chunked launch adds a sum kernel
-    # that is not a pass
-    per_step = int(k["Calls"]) / 3.0 if k else b["roofline"]["launches_per_step"]
-    spl = cfg["width"] * cfg["height"] * cfg["spp"] / per_step
-    fps = b["roofline"]["flop_per_sample"]
-    ach = fps * spl / (avg_ns * 1e-9) / 1e12
-    pmc = {}
-    try:
-        pmc = json.load(open(os.path.join(D, "pmc_%s.json" % c)))
-    except FileNotFoundError:
-        pass
-    v = pmc.get("valu", {})
-    issue = float("nan")
-    if v:
-        cyc = 2.0 * (v["SQ_INSTS_VALU"] - v["SQ_INSTS_VALU_TRANS_F32"]) + 4.0 * v["SQ_INSTS_VALU_TRANS_F32"]
-        issue = cyc / (1024 * avg_ns * 1e-9 * 2.4e9)  # counters are per dispatch (pmc_traffic.py)
-    rows.append(dict(config=c, workload=cfg["workload"], msamples_s=b["value"], flop_per_sample=fps,
-                     samples_per_launch=spl, rocprof_avg_ms=avg_ns / 1e6, achieved_tflops=ach, frac=ach / PEAK,
-                     bench_frac=b["roofline"]["frac"], lane_util=pmc.get("valu_lane_utilisation"),
-                     valu_issue_util=issue, traffic_bytes=pmc.get("traffic_bytes_per_launch"),
-                     algorithmic_bytes=pmc.get("algorithmic_bytes_per_launch"),
-                     events=b["roofline"].get("events_per_sample")))
-json.dump(rows, open(os.path.join(D, "roofline.json"), "w"), indent=1)
-print("| config | Msamples/s | FLOP/sample | rocprof ms/launch | TFLOP/s | frac (rocprof) | frac (bench) | "
-      "VALU lane util | VALU issue util | HBM bytes/launch (PMC / algorithmic) |")
-print("|---|---|---|---|---|---|---|---|---|---|")
+    lps = R["launches_per_step"]
+    pixels = cfg["width"] * cfg["height"]
+    spl = pixels * cfg["spp"] / lps  # samples per launch
+    med = kt["median_ms"]
+    ach = R["flop_per_sample"] * spl / (med * 1e-3) / 1e12
+    row = dict(config=c, msamples_s=b["value"], ms_per_step=b["ms_per_step"], flop_per_sample=R["flop_per_sample"],
+               launches_per_step=lps, rocprof_median_ms=med, rocprof_min_ms=kt["min_ms"], rocprof_max_ms=kt["max_ms"],
+               hip_event_ms=R["kernel_ms_per_launch"], achieved_tflops=ach, frac_spec=ach / PEAK_SPEC,
+               frac_scalar=ach / PEAK_SCALAR, bench_frac=R["frac"])
+    if pr:
+        row["profiled_ms_per_step"] = pr["ms_per_step"]
+        row["check_kernel_x_launches_le_step"] = med * lps <= pr["ms_per_step"] * 1.0001
+    if pmc:
+        clk = pmc.get("clock_ghz_median")
+        row["clock_ghz"] = clk
+        v = pmc.get("valu", {})
+        if v and clk:
+            cyc = 2.0 * v["SQ_INSTS_VALU"] + 2.0 * v["SQ_INSTS_VALU_TRANS_F32"]
+            row["valu_issue_util"] = cyc / (1024 * med * 1e-3 * clk * 1e9)
+        row["lane_util"] = pmc.get("valu_lane_utilisation")
+        row["stall_share"] = pmc.get("stall_share")
+        cnt = pmc.get("counters", {})
+        if "FETCH_SIZE" in cnt and "WRITE_SIZE" in cnt:
+            fetch = cnt["FETCH_SIZE"] * 1024.0  # counter bytes as reported
+            write = cnt["WRITE_SIZE"] * 1024.0
+            acc = 16.0 * pixels  # the accumulator read: a 16-B/lane stream
+            rest = max(0.0, fetch - acc / 2.0)  # counter bytes of everything else
+            if c in ("c1", "c2", "c4"):
+                lo = hi = est = 2.0 * fetch + write
+            elif c == "c3":  # bilinear reservoir taps dominate the rest
+                est = acc + rest * (fac.get("k_bilin") or 0.5) + write
+                lo, hi = acc + 0.5 * rest + write, acc + 2.0 * rest + write
+            else:  # c5: taps, 64-B node / 48-B triangle gathers and spills mixed
+                lo, hi = acc + 0.5 * rest + write, acc + 2.0 * rest + write
+                est = acc + rest * (fac.get("k_node64") or 1.0) + write
+            row.update(fetch_counter_bytes=fetch, write_bytes=write, traffic_est=est, traffic_lo=lo, traffic_hi=hi,
+                       hbm_gbs=est / (med * 1e-3) / 1e9, hbm_frac=est / (med * 1e-3) / 8e12,
+                       algorithmic_bytes=pmc.get("algorithmic_bytes_per_launch"))
+        if pmc.get("valu_mix"):
+            row["valu_mix"] = pmc["valu_mix"]
+    rows.append(row)
+json.dump({"rows": rows, "calibration": fac, "valu_peak_tflops": vp}, open(os.path.join(D, "roofline.json"), "w"),
+          indent=1)
+
+
+def f(x, fmt="%.3f"):
+    return "-" if x is None else fmt % x
+
+
+print("Measured peaks: scalar v_fma_f32 %s TF, packed v_pk_fma_f32 %s TF (scripts/valu_peak.hip; spec 157.3)."
+      % (f(vp.get("v_fma_f32"), "%.1f"), f(vp.get("v_pk_fma_f32"), "%.1f")))
+print("FETCH_SIZE calibration, true bytes / counter bytes (scripts/fetch_calib.hip): %s." %
+      ", ".join("%s x%s" % (k, v) for k, v in fac.items()))
+print()
+print("| config | Msamples/s | FLOP/sample | kernel ms/launch: rocprof median (min-max) / HIP events | launches x median <= "
+      "ms_per_step (profiled run) | TFLOP/s | frac of 157.3 | frac of scalar peak | clock GHz | VALU issue util | "
+      "lane util | HBM bytes/launch est. (range) / algorithmic | GB/s | frac of 8 TB/s |")
+print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
 for r in rows:
-    print("| %s | %.0f | %.0f | %.3f | %.1f | %.3f | %.3f | %s | %s | %s / %s |" % (
-        r["config"], r["msamples_s"], r["flop_per_sample"], r["rocprof_avg_ms"], r["achieved_tflops"], r["frac"],
-        r["bench_frac"], "%.2f" % r["lane_util"] if r["lane_util"] else "-",
-        "%.2f" % r["valu_issue_util"] if r["valu_issue_util"] == r["valu_issue_util"] else "-",
-        "%.3g" % r["traffic_bytes"] if r["traffic_bytes"] else "-",
-        "%.3g" % r["algorithmic_bytes"] if r["algorithmic_bytes"] else "-"))
+    chk = r.get("check_kernel_x_launches_le_step")
+    print("| %s | %.0f | %.0f | %.3f (%.3f-%.3f) / %.3f | %s %s | %.1f | %.3f | %.3f | %s | %s | %s | %s (%s-%s) / %s | %s | %s |" % (
+        r["config"], r["msamples_s"], r["flop_per_sample"], r["rocprof_median_ms"], r["rocprof_min_ms"],
+        r["rocprof_max_ms"], r["hip_event_ms"],
+        "%.2f x %d = %.2f <= %.2f" % (r["rocprof_median_ms"], r["launches_per_step"],
+                                      r["rocprof_median_ms"] * r["launches_per_step"], r.get("profiled_ms_per_step", 0)),
+        "ok" if chk else ("VIOLATED" if chk is not None else "-"),
+        r["achieved_tflops"], r["frac_spec"], r["frac_scalar"], f(r.get("clock_ghz"), "%.2f"),
+        f(r.get("valu_issue_util"), "%.2f"), f(r.get("lane_util"), "%.2f"), f(r.get("traffic_est"), "%.3g"),
+        f(r.get("traffic_lo"), "%.3g"), f(r.get("traffic_hi"), "%.3g"), f(r.get("algorithmic_bytes"), "%.3g"),
+        f(r.get("hbm_gbs"), "%.0f"), f(r.get("hbm_frac"), "%.3f")))
