@@ -82,7 +82,11 @@ struct BvhNode {
 // running it (its result only adds to the path's radiance; the path's next
 // direction does not depend on it), rt0_jit_nee evaluates the records densely
 // -- every lane has one -- and rt0_jit_resolve adds them to the pixel's
-// sample in bounce order.  64 B, appended per wave (contiguous, coalesced).
+// sample in bounce order.  64 B.  Each wave of the pass kernel owns a region
+// of nee_cap records (64 lanes x max_bounces calls) that it fills in call
+// order through an LDS counter -- no device-wide atomic, whose single address
+// serialises every wave of the chip -- and the NEE kernel gives each region to
+// one wave, so a wave's records are one 8x8 tile's calls (coherent taps).
 struct NeeRec {
   float x, y, z;     // the shading point (hit.pos)
   float nx, ny, nz;  // nl
@@ -181,7 +185,9 @@ struct LaunchParams {
   // per launch on the host (it is uniform over the image).  Unused otherwise.
   float ema_alpha;
   // deferred light sampling (NeeRec): defer != 0 routes sampleLightsReSTIR
-  // calls into nee_rec[*nee_count++] (capacity nee_cap); results go to
+  // calls into its region nee_rec[wave * nee_cap ...], nee_count[wave] = the
+  // records the wave wrote (wave = (blockIdx.y * gridDim.x + blockIdx.x) * 4
+  // + threadIdx.x / 64 of the pass grid); results go to
   // nee_out[k * width * height + pix]; nee_partial[pix] = (the path's radiance
   // without them, hero wavelength), nee_n[pix] = its number of calls
   int32_t defer, nee_cap;

@@ -104,10 +104,11 @@ struct rt0_ctx {
   // the paths' own radiance + hero wavelength, and the calls per pixel
   bool defer_nee = true;
   NeeRec *d_nee_rec = nullptr;
-  uint32_t *d_nee_count = nullptr;
+  uint32_t *d_nee_count = nullptr;  // records per pass wave
   float4 *d_nee_out = nullptr, *d_nee_partial = nullptr;
   int32_t *d_nee_n = nullptr;
-  size_t nee_slots = 0;  // records d_nee_rec holds (W x H x calls per pixel)
+  size_t nee_slots = 0;  // records d_nee_rec holds (pass waves x 64 x calls per lane)
+  size_t nee_waves = 0;  // entries of d_nee_count
   size_t nee_pixels = 0;
   std::string jit_err;
   std::string err;
@@ -682,37 +683,34 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     }
     jit_fn = c->jit.pass;
   }
-  unsigned nee_grid = 0;
+  const size_t pass_waves = (size_t)grid.x * grid.y * 4;
   if (defer) {
-    // one record per (pixel, call): a path makes at most one light-sampling
-    // call per bounce (rt0_integrator.h step)
-    const size_t pixels = (size_t)c->W * c->H, slots = pixels * (size_t)p.max_bounces;
-    if (slots > 0x7fffffffu) return fail(c, RT0_E_UNSUPPORTED, "deferred light sampling: too many records");
-    if (slots > c->nee_slots || pixels != c->nee_pixels) {
-      for (void **q : {(void **)&c->d_nee_rec, (void **)&c->d_nee_out, (void **)&c->d_nee_partial,
-                       (void **)&c->d_nee_n}) {
+    // a region of 64 lanes x max_bounces records per pass wave: a path makes
+    // at most one light-sampling call per bounce (rt0_integrator.h step)
+    const size_t pixels = (size_t)c->W * c->H, slots = pass_waves * 64 * (size_t)p.max_bounces;
+    if (slots > c->nee_slots || pass_waves > c->nee_waves || pixels != c->nee_pixels) {
+      for (void **q : {(void **)&c->d_nee_rec, (void **)&c->d_nee_count, (void **)&c->d_nee_out,
+                       (void **)&c->d_nee_partial, (void **)&c->d_nee_n}) {
         if (*q) HIPCHK(c, hipFree(*q));
         *q = nullptr;
       }
-      c->nee_slots = c->nee_pixels = 0;
+      c->nee_slots = c->nee_waves = c->nee_pixels = 0;
       HIPCHK(c, hipMalloc(&c->d_nee_rec, slots * sizeof(NeeRec)));
-      HIPCHK(c, hipMalloc(&c->d_nee_out, slots * sizeof(float4)));
+      HIPCHK(c, hipMalloc(&c->d_nee_count, pass_waves * sizeof(uint32_t)));
+      HIPCHK(c, hipMalloc(&c->d_nee_out, pixels * (size_t)p.max_bounces * sizeof(float4)));
       HIPCHK(c, hipMalloc(&c->d_nee_partial, pixels * sizeof(float4)));
       HIPCHK(c, hipMalloc(&c->d_nee_n, pixels * sizeof(int32_t)));
-      if (!c->d_nee_count) HIPCHK(c, hipMalloc(&c->d_nee_count, sizeof(uint32_t)));
       c->nee_slots = slots;
+      c->nee_waves = pass_waves;
       c->nee_pixels = pixels;
     }
     p.defer = 1;
-    p.nee_cap = (int32_t)slots;
+    p.nee_cap = 64 * p.max_bounces;
     p.nee_rec = c->d_nee_rec;
     p.nee_count = c->d_nee_count;
     p.nee_out = c->d_nee_out;
     p.nee_partial = c->d_nee_partial;
     p.nee_n = c->d_nee_n;
-    // grid-stride over the records: ~16 waves per SIMD whatever the count
-    const size_t lanes = (size_t)(p.vp_x1 - p.vp_x0) * (p.vp_y1 - p.vp_y0) * 2;
-    nee_grid = (unsigned)std::max<size_t>(1, std::min<size_t>(4096, (lanes + 255) / 256));
   }
   auto launch = [&](const LaunchParams &lp, unsigned gz, dim3 g) -> hipError_t {
     if (jit_fn) return rt0h::jit_launch(jit_fn, &lp, g.x, g.y, gz, c->stream) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
@@ -734,14 +732,17 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       p.rout_main = c->d_restir[R_OUT_MAIN];
       p.rout_aux = c->d_restir[R_OUT_AUX];
       if (defer) {
-        HIPCHK(c, hipMemsetAsync(c->d_nee_count, 0, sizeof(uint32_t), c->stream));
+        // waves wholly outside the viewport write no count
+        HIPCHK(c, hipMemsetAsync(c->d_nee_count, 0, pass_waves * sizeof(uint32_t), c->stream));
         HIPCHK(c, launch(p, 1, grid));
-        HIPCHK(c, rt0h::jit_launch(c->jit.nee, &p, nee_grid, 1, 1, c->stream) == RT0_OK ? hipSuccess
-                                                                                            : hipErrorLaunchFailure);
+        // one NEE wave per pass wave's region
+        HIPCHK(c, rt0h::jit_launch(c->jit.nee, &p, grid.x * grid.y, 1, 1, c->stream) == RT0_OK
+                      ? hipSuccess
+                      : hipErrorLaunchFailure);
         HIPCHK(c, rt0h::jit_launch(c->jit.resolve, &p, grid.x, grid.y, 1, c->stream) == RT0_OK
                       ? hipSuccess
                       : hipErrorLaunchFailure);
-        launches += 3;
+        launches++;  // one pass (rt0_last_kernel_ms)
       } else {
         HIPCHK(c, launch(p, 1, grid));
         launches++;

@@ -353,6 +353,11 @@ DEV int32_t *bvh_stack_lds() {
   __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
   return stk_base + threadIdx.x;
 }
+// the record counter of this wave's deferred light-sampling region
+DEV uint32_t *nee_wave_counter() {
+  __shared__ uint32_t cnt[4];
+  return cnt + (threadIdx.x >> 6);
+}
 // closest triangle hit along (o, d) before tmin: depth-first, nearer child
 // first, the far child on the per-lane LDS stack.  Returns the leaf-order
 // triangle index or -1; tmin is updated.  ANY: stop at the first hit before
@@ -1089,6 +1094,7 @@ struct Integrator {
   // deferred light sampling (P.defer): this sample's image pixel and the
   // number of sampleLightsReSTIR calls it has deferred so far
   int32_t nee_pix = 0, nee_k = 0;
+  uint32_t nee_wave = 0;  // the pass grid's wave index: the region defer_nee appends to
   // F_EXEC_GHOST: brdf()'s parameter registers as the lane's last live call
   // left them (see ghost_brdf)
   v3 gr_x, gr_nl, gr_rd;
@@ -1611,8 +1617,9 @@ struct Integrator {
     if (!flag(F_RESTIR) || !flag(F_RESTIR_DEF)) return false;
     return !flag(F_MIS) || sc.n_lights() > 8;
   }
-  // P.defer: append the call as a NeeRec (one atomic per wave: the active
-  // lanes take consecutive slots) instead of running it; rt0_jit_nee runs it
+  // RT0_DEFER_NEE: append the call as a NeeRec to the wave's region (one LDS
+  // add per wave: the active lanes take consecutive slots) instead of running
+  // it; rt0_jit_nee runs it
   // with the same arguments and rt0_jit_resolve adds result * mask to the
   // sample.  The seeds are the ones sample_lights() passes (1909/1943).
   DEV void defer_nee(v3 x, v3 nl, int mi, float seed, float bounce, v3 mask) {
@@ -1622,10 +1629,10 @@ struct Integrator {
     const int leader = __ffsll((long long)act) - 1;
     const int rank = __popcll(act & ((1ull << lane) - 1ull));
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(P.nee_count, (uint32_t)__popcll(act));
+    if (lane == leader) base = atomicAdd(nee_wave_counter(), (uint32_t)__popcll(act));
     base = __shfl(base, leader);
     const uint32_t i = base + (uint32_t)rank;
-    if (i < (uint32_t)P.nee_cap) {  // the host sizes nee_cap for MAX_DIFF_BOUNCES calls per pixel
+    if (i < (uint32_t)P.nee_cap) {  // nee_cap = 64 lanes x max_bounces calls: never exceeded
       NeeRec r;
       r.x = x.x;
       r.y = x.y;
@@ -1642,7 +1649,7 @@ struct Integrator {
       r.mat = mi;
       r.k = nee_k;
       r.pad = 0;
-      P.nee_rec[i] = r;
+      P.nee_rec[(size_t)nee_wave * (uint32_t)P.nee_cap + i] = r;
     }
     ++nee_k;
   }
@@ -2300,11 +2307,17 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     // completes the sample and accumulates it
     it.frame = P.frame0;
     it.nee_pix = (int32_t)pix;
+    it.nee_wave = (blockIdx.y * gridDim.x + blockIdx.x) * 4u + (uint32_t)wave;
+    volatile uint32_t *wc = nee_wave_counter();
+    *wc = 0u;  // every active lane stores the same 0 before the wave's first append
     typename decltype(it)::Path ps;
     it.begin(ps, px, py);
     if (cfg.max_bounces() > 0)
       while (it.step(ps)) {
       }
+    // the wave has reconverged: every append is in the counter
+    const uint32_t total = *wc;
+    if (lane == __ffsll((long long)__ballot(1)) - 1) P.nee_count[it.nee_wave] = total;
     P.nee_partial[pix] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, it.hero);
     P.nee_n[pix] = it.nee_k;
     if (it.nee_k > 0) return;  // g_final_reservoir is the last deferred call's: rt0_jit_nee writes it
@@ -2342,18 +2355,20 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   }
 }
 
-// The deferred sampleLightsReSTIR calls of one pass (rt0_jit_nee): every lane
-// takes records off the list the pass kernel appended (grid-stride), so the
-// candidates, reservoir taps and visibility rays run on full waves whatever
-// the paths' lengths.  Same arguments, same arithmetic as the inline call;
+// The deferred sampleLightsReSTIR calls of one pass (rt0_jit_nee): each wave
+// takes one pass wave's region 64 records at a time, so the candidates,
+// reservoir taps and visibility rays run on full waves whatever the paths'
+// lengths.  Same arguments, same arithmetic as the inline call;
 // the last call of a pixel writes its reservoir MRTs (g_final_reservoir,
 // raytracer.glsl:2171-2174).
 template <class Scene, class Cfg, bool VOL, bool SDF, bool SPECTRAL>
 DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
-  const uint32_t n = min(*P.nee_count, (uint32_t)P.nee_cap);
-  const size_t plane = (size_t)P.width * P.height;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const NeeRec r = P.nee_rec[i];
+  // one wave per region of the pass grid (host: gridDim.x = the pass grid's workgroups)
+  const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t n = min(P.nee_count[gw], (uint32_t)P.nee_cap);
+  const size_t plane = (size_t)P.width * P.height, base = (size_t)gw * (uint32_t)P.nee_cap;
+  for (uint32_t i = threadIdx.x & 63u; i < n; i += 64u) {
+    const NeeRec r = P.nee_rec[base + i];
     Integrator<Scene, Cfg, true, VOL, SDF, SPECTRAL, false> it(P, sc, cfg);
     it.frame = P.frame0;
     const int py = r.pix / P.width, px = r.pix - py * P.width;

@@ -7,7 +7,10 @@ run of bench.py (scripts/gpu_measure.sh).
 Keeps the rt0_jit_pass dispatches after the first SKIP (the warm-up step's
 launches) and reports their median / mean / min / max duration, plus the other
 kernels' totals (rocprofv3's own --stats table averages every dispatch,
-warm-up included).
+warm-up included).  A deferred ReSTIR pass is three dispatches (rt0_jit_pass,
+rt0_jit_nee, rt0_jit_resolve; rt0_integrator.h): their kept medians are
+reported per kernel and "median_ms" .. "max_ms" are then per pass, the three
+kernels' durations summed pass by pass.
 """
 import csv
 import glob
@@ -17,6 +20,7 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_resolve")
 
 
 def main():
@@ -25,16 +29,24 @@ def main():
     for fn in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
         rows += list(csv.DictReader(open(fn)))
     rows.sort(key=lambda r: float(r["Start_Timestamp"]))
-    pas = [float(r["End_Timestamp"]) - float(r["Start_Timestamp"]) for r in rows if KERNEL in r["Kernel_Name"]]
+    dur = {k: [float(r["End_Timestamp"]) - float(r["Start_Timestamp"]) for r in rows if r["Kernel_Name"].strip() == k]
+           for k in GROUP}
+    pas = dur[KERNEL]
+    per_kernel = {}
+    if dur["rt0_jit_nee"]:  # deferred passes: pass + nee + resolve, one of each per pass
+        n = min(len(v) for v in dur.values())
+        pas = [sum(dur[k][i] for k in GROUP) for i in range(n)]
+        per_kernel = {k: statistics.median(v[skip:]) / 1e6 for k, v in dur.items() if v[skip:]}
     kept = pas[skip:]
     other = defaultdict(list)
     for r in rows:
-        if KERNEL not in r["Kernel_Name"]:
+        if r["Kernel_Name"].strip() not in GROUP:
             other[r["Kernel_Name"][:80]].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     res = {"kernel": KERNEL, "dispatches": len(pas), "skipped": skip, "kept": len(kept),
            "median_ms": statistics.median(kept) / 1e6 if kept else None,
            "mean_ms": statistics.mean(kept) / 1e6 if kept else None,
            "min_ms": min(kept) / 1e6 if kept else None, "max_ms": max(kept) / 1e6 if kept else None,
+           "per_kernel_median_ms": per_kernel,
            "all_ms": [round(x / 1e6, 4) for x in pas],
            "other_kernels": {k: {"calls": len(v), "total_ms": sum(v) / 1e6} for k, v in other.items()}}
     json.dump(res, open(out, "w"), indent=1)

@@ -6,7 +6,9 @@ into per-launch figures of the scene-specialised pass kernel (rt0_jit_pass).
 
 Per dispatch of rt0_jit_pass (the counting instance bench.py launches
 afterwards is a different kernel and is excluded), dropping the first SKIP
-dispatches (the warm-up step), averaged over the rest:
+dispatches (the warm-up step), averaged over the rest -- for a deferred ReSTIR
+pass (rt0_jit_pass + rt0_jit_nee + rt0_jit_resolve) the three kernels' means
+summed, i.e. per pass:
   * HBM traffic: FETCH_SIZE x 2 (MI355X_MICROARCH.md: gfx950 reports half the
     bytes of a 16-B/lane streaming read; scripts/fetch_calib.hip measures the
     factor for the 64-B gathers and bilinear taps of the ReSTIR/BVH kernels)
@@ -29,20 +31,21 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_resolve")
 
 
-def dispatches(d):
-    """{dispatch id: {counter: value}} and {dispatch id: duration ns} of the
-    pass kernel in one pass directory."""
+def dispatches(d, kernel):
+    """{dispatch id: {counter: value}} and {dispatch id: duration ns} of one
+    kernel in one pass directory."""
     vals = defaultdict(lambda: defaultdict(float))
     for fn in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(fn)):
-            if KERNEL in r["Kernel_Name"]:
+            if r["Kernel_Name"].strip() == kernel:
                 vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     dur = {}
     for fn in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(fn)):
-            if KERNEL in r["Kernel_Name"]:
+            if r["Kernel_Name"].strip() == kernel:
                 dur[int(r["Dispatch_Id"])] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     return vals, dur
 
@@ -52,20 +55,24 @@ def main():
     per = {}  # counter -> mean over the kept dispatches
     n_kept = {}
     clock = []
+    kernels = []
     for d in sys.argv[6:]:
-        vals, dur = dispatches(d)
-        ids = sorted(vals)[skip:]
-        if not ids:
-            continue
-        names = set().union(*(vals[i].keys() for i in ids))
-        for c in names:
-            per[c] = sum(vals[i].get(c, 0.0) for i in ids) / len(ids)
-            n_kept[c] = len(ids)
-        if "GRBM_GUI_ACTIVE" in names:
-            for i in ids:
-                if dur.get(i):
-                    clock.append(vals[i]["GRBM_GUI_ACTIVE"] / 8.0 / dur[i])  # cycles per ns = GHz
-    res = {"kernel": KERNEL, "skipped_dispatches": skip, "dispatches_kept": n_kept, "counters": per,
+        for kernel in GROUP:
+            vals, dur = dispatches(d, kernel)
+            ids = sorted(vals)[skip:]
+            if not ids:
+                continue
+            if kernel not in kernels:
+                kernels.append(kernel)
+            names = set().union(*(vals[i].keys() for i in ids))
+            for c in names:  # per pass: the group's kernels summed
+                per[c] = per.get(c, 0.0) + sum(vals[i].get(c, 0.0) for i in ids) / len(ids)
+                n_kept[c] = len(ids)
+            if "GRBM_GUI_ACTIVE" in names and kernel == KERNEL:
+                for i in ids:
+                    if dur.get(i):
+                        clock.append(vals[i]["GRBM_GUI_ACTIVE"] / 8.0 / dur[i])  # cycles per ns = GHz
+    res = {"kernel": "+".join(kernels) or KERNEL, "skipped_dispatches": skip, "dispatches_kept": n_kept, "counters": per,
            "algorithmic_bytes_per_launch": W * H * bpp}
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
         res["fetch_bytes_per_launch"] = 2.0 * per["FETCH_SIZE"] * 1024.0
