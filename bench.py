@@ -342,6 +342,24 @@ def pmc_summary(config):
     return None, None
 
 
+def valu_rates():
+    """(ns per non-transcendental, ns per transcendental) wave64 VALU
+    instruction per SIMD, measured by scripts/valu_peak (16 independent chains
+    per lane at full occupancy; committed under profiles/), or None."""
+    for rd in PROFILE_ROUNDS:
+        path = os.path.join(HERE, "profiles", rd, "valu_peak.json")
+        if os.path.exists(path):
+            r = {}
+            for line in open(path):
+                if line.startswith("{"):
+                    d = json.loads(line)
+                    r[d["kernel"]] = d.get("wave_instr_per_simd_per_ns")
+            if all(r.get(k) for k in ("v_add_f32", "v_mul_f32", "v_fma_f32", "v_exp_f32")):
+                norm = 3.0 / (r["v_add_f32"] + r["v_mul_f32"] + r["v_fma_f32"])
+                return norm, 1.0 / r["v_exp_f32"], "profiles/%s/valu_peak.json" % rd
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -451,11 +469,17 @@ def main():
                     "events on librt0's stream); hbm_gbs = PMC traffic per launch over the same kernel time"}
     if pmc and "valu" in pmc:
         roof["valu_lane_utilisation"] = round(pmc.get("valu_lane_utilisation", 0.0), 4)
-        # wave64 VALU instruction = 2 SIMD cycles (transcendental 4,
-        # MI355X_MICROARCH.md constants), over 1024 SIMDs x the live kernel
-        # time of one launch at the nominal 2.4 GHz
-        roof["valu_issue_utilisation"] = round(2.0 * (pmc["valu"]["SQ_INSTS_VALU"] + pmc["valu"]["SQ_INSTS_VALU_TRANS_F32"])
-                                               / (1024 * kern_launch_s * 2.4e9), 4)
+        rates = valu_rates()
+        if rates:
+            # VALU busy: the launch's wave64 VALU instructions at the MEASURED
+            # issue time of their class (scripts/valu_peak: add/mul/fma ~0.9-1.1
+            # per SIMD per ns, a transcendental ~4.5 ns), over 1024 SIMDs x the
+            # live kernel time of one launch
+            v = pmc["valu"]
+            busy_ns = ((v["SQ_INSTS_VALU"] - v["SQ_INSTS_VALU_TRANS_F32"]) * rates[0]
+                       + v["SQ_INSTS_VALU_TRANS_F32"] * rates[1]) / 1024.0
+            roof["valu_busy"] = round(busy_ns / (kern_launch_s * 1e9), 4)
+            roof["valu_rates_source"] = rates[2]
     mdb = wl["constants"].get("MAX_DIFF_BOUNCES", 4)
     out = {
         "metric": "Msamples/sec (pixels x spp / s) at 1024^2 Cornell, 8 bounces" if args.config == "c2"

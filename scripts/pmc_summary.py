@@ -56,6 +56,7 @@ def main():
     n_kept = {}
     clock = []
     kernels = []
+    by_kernel = {}  # kernel -> {counter: mean per dispatch}
     for d in sys.argv[6:]:
         for kernel in GROUP:
             vals, dur = dispatches(d, kernel)
@@ -66,7 +67,9 @@ def main():
                 kernels.append(kernel)
             names = set().union(*(vals[i].keys() for i in ids))
             for c in names:  # per pass: the group's kernels summed
-                per[c] = per.get(c, 0.0) + sum(vals[i].get(c, 0.0) for i in ids) / len(ids)
+                m = sum(vals[i].get(c, 0.0) for i in ids) / len(ids)
+                per[c] = per.get(c, 0.0) + m
+                by_kernel.setdefault(kernel, {})[c] = m
                 n_kept[c] = len(ids)
             if "GRBM_GUI_ACTIVE" in names and kernel == KERNEL:
                 for i in ids:
@@ -83,6 +86,11 @@ def main():
         res["valu"] = {c: per[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_ACTIVE_INST_VALU",
                                            "SQ_THREAD_CYCLES_VALU") if c in per}
         res["valu_lane_utilisation"] = per["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * per["SQ_ACTIVE_INST_VALU"])
+    if len(by_kernel) > 1:
+        res["per_kernel"] = by_kernel
+        res["per_kernel_lane_utilisation"] = {
+            k: v["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * v["SQ_ACTIVE_INST_VALU"])
+            for k, v in by_kernel.items() if "SQ_THREAD_CYCLES_VALU" in v and "SQ_ACTIVE_INST_VALU" in v}
     if clock:
         clock.sort()
         res["clock_ghz_median"] = clock[len(clock) // 2]
@@ -100,7 +108,7 @@ def main():
         res["hw_flop_wave_instr"] = 2.0 * per["SQ_INSTS_VALU_FMA_F32"] + per["SQ_INSTS_VALU_ADD_F32"] + \
             per["SQ_INSTS_VALU_MUL_F32"]
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps({k: v for k, v in res.items() if k != "counters"}))
+    print(json.dumps({k: v for k, v in res.items() if k not in ("counters", "per_kernel")}))
 
 
 if __name__ == "__main__":

@@ -15,9 +15,10 @@ For every workload:
     the 157.3 TF spec (packed v_pk_fma_f32) and against the MEASURED scalar
     v_fma_f32 peak of scripts/valu_peak (the compiler emits scalar FMA for this
     kernel: -fno-slp-vectorize);
-  * VALU issue utilisation at the MEASURED clock (GRBM_GUI_ACTIVE / 8 / time):
-    (2 x SQ_INSTS_VALU + 2 x SQ_INSTS_VALU_TRANS_F32) SIMD cycles / (1024 SIMDs
-    x kernel cycles);
+  * VALU busy: the kernel's wave64 VALU instructions at the MEASURED issue
+    time of their class (scripts/valu_peak: non-transcendental = the mean of
+    v_add/v_mul/v_fma rates, transcendental = v_exp_f32's), per SIMD, over the
+    median kernel time -- the share of time the VALU pipe is occupied;
   * HBM traffic: FETCH_SIZE x 1024 B x the calibrated factor of the access
     shape (scripts/fetch_calib: 16-B/lane stream x2, 64-B gathers x1, bilinear
     2x2 RGBA32F taps x0.5) + WRITE_SIZE.  A kernel that mixes shapes gets its
@@ -40,13 +41,16 @@ def load(name):
 
 calib = load("calib.json") or {}
 fac = {k: (v["factor"][-1] if v.get("factor") else None) for k, v in calib.items()}
-vp = {}
+vp, rate = {}, {}
 if os.path.exists(os.path.join(D, "valu_peak.json")):
     for line in open(os.path.join(D, "valu_peak.json")):
         if line.startswith("{"):
             d = json.loads(line)
             vp[d["kernel"]] = d["tflops"]
+            rate[d["kernel"]] = d.get("wave_instr_per_simd_per_ns")
 PEAK_SCALAR = vp.get("v_fma_f32", 78.6)
+NS_NORM = 3.0 / (rate["v_add_f32"] + rate["v_mul_f32"] + rate["v_fma_f32"]) if rate.get("v_add_f32") else None
+NS_TRANS = 1.0 / rate["v_exp_f32"] if rate.get("v_exp_f32") else None
 
 rows = []
 for c in ("c1", "c2", "c3", "c4", "c5"):
@@ -71,9 +75,9 @@ for c in ("c1", "c2", "c3", "c4", "c5"):
         clk = pmc.get("clock_ghz_median")
         row["clock_ghz"] = clk
         v = pmc.get("valu", {})
-        if v and clk:
-            cyc = 2.0 * v["SQ_INSTS_VALU"] + 2.0 * v["SQ_INSTS_VALU_TRANS_F32"]
-            row["valu_issue_util"] = cyc / (1024 * med * 1e-3 * clk * 1e9)
+        if v and NS_NORM:
+            ns = (v["SQ_INSTS_VALU"] - v["SQ_INSTS_VALU_TRANS_F32"]) * NS_NORM + v["SQ_INSTS_VALU_TRANS_F32"] * NS_TRANS
+            row["valu_busy"] = ns / 1024.0 / (med * 1e6)
         row["lane_util"] = pmc.get("valu_lane_utilisation")
         row["stall_share"] = pmc.get("stall_share")
         cnt = pmc.get("counters", {})
@@ -110,7 +114,7 @@ print("FETCH_SIZE calibration, true bytes / counter bytes (scripts/fetch_calib.h
       ", ".join("%s x%s" % (k, v) for k, v in fac.items()))
 print()
 print("| config | Msamples/s | FLOP/sample | kernel ms/launch: rocprof median (min-max) / HIP events | launches x median <= "
-      "ms_per_step (profiled run) | TFLOP/s | frac of 157.3 | frac of scalar peak | clock GHz | VALU issue util | "
+      "ms_per_step (profiled run) | TFLOP/s | frac of 157.3 | frac of scalar peak | clock GHz | VALU busy | "
       "lane util | HBM bytes/launch est. (range) / algorithmic | GB/s | frac of 8 TB/s |")
 print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
 for r in rows:
@@ -122,6 +126,6 @@ for r in rows:
                                       r["rocprof_median_ms"] * r["launches_per_step"], r.get("profiled_ms_per_step", 0)),
         "ok" if chk else ("VIOLATED" if chk is not None else "-"),
         r["achieved_tflops"], r["frac_spec"], r["frac_scalar"], f(r.get("clock_ghz"), "%.2f"),
-        f(r.get("valu_issue_util"), "%.2f"), f(r.get("lane_util"), "%.2f"), f(r.get("traffic_est"), "%.3g"),
+        f(r.get("valu_busy"), "%.2f"), f(r.get("lane_util"), "%.2f"), f(r.get("traffic_est"), "%.3g"),
         f(r.get("traffic_lo"), "%.3g"), f(r.get("traffic_hi"), "%.3g"), f(r.get("algorithmic_bytes"), "%.3g"),
         f(r.get("hbm_gbs"), "%.0f"), f(r.get("hbm_frac"), "%.3f")))
