@@ -1267,6 +1267,19 @@ static void ghost_brdf(Frag *F, const BrdfRegs *g, float seed) {
   sampleLightsReSTIR(F, g->hit.pos, muls(g->hit.n, g->inside), mat, sx, sy, 1);
 }
 
+/* Diagnostics: RT0_ORACLE_TRACE="x,y" prints every bounce of that pixel's
+ * paths (ray, closest hit) to stderr, e.g. to see how close a decision that
+ * flips under ulp-level differences sits to its threshold. */
+static int trace_pixel(const Frag *F) {
+  static int tx = -2, ty = -2;
+  if (tx == -2) {
+    const char *e = getenv("RT0_ORACLE_TRACE");
+    tx = ty = -1;
+    if (e) sscanf(e, "%d,%d", &tx, &ty);
+  }
+  return tx >= 0 && F->fcx == (float)tx + 0.5f && F->fcy == (float)ty + 0.5f;
+}
+
 /* radiance(), raytracer.glsl:1986-2105 */
 static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
   const Oracle *o = F->o;
@@ -1279,6 +1292,9 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
     F->n_iter++;
     Hit hit;
     float t = intersection(F, ro, rd, &hit);
+    if (trace_pixel(F))
+      fprintf(stderr, "frame %d depth %d ro (%.9g %.9g %.9g) rd (%.9g %.9g %.9g) t %.9g index %d spec %d\n", F->frame,
+              depth, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, t, t == INF_T ? -1 : hit.index, spec);
     if (o->use_vol) {
       float sd = -logf(gmax(or_hash(seed + 4729.3f + (float)depth * 991.1f), 1e-6f)) / VOL_SIGMA_T;
       float tb = gmin(INF_T, t);

@@ -190,7 +190,7 @@ struct LaunchParams {
   // + threadIdx.x / 64 of the pass grid); results go to
   // nee_out[k * width * height + pix]; nee_partial[pix] = (the path's radiance
   // without them, hero wavelength), nee_n[pix] = its number of calls
-  int32_t defer, nee_cap;
+  int32_t defer, nee_cap, nee_regions;  // nee_regions = pass waves (entries of nee_count)
   NeeRec *nee_rec;
   uint32_t *nee_count;
   float4 *nee_out, *nee_partial;

@@ -34,6 +34,11 @@ extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_mo
 // shards, against 0.89 / 0.78 / 0.61 unchunked).
 static const long kTargetWaves = 16384;
 static const long kChunkWaves = 65536;
+// pass-wave record regions per light-sampling wave (JitKey::nee_regions); RT0_NEE_REGIONS overrides
+static long nee_regions_per_wave() {
+  static const long k = getenv("RT0_NEE_REGIONS") ? std::max(1L, atol(getenv("RT0_NEE_REGIONS"))) : 2L;
+  return k;
+}
 
 enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
 
@@ -677,6 +682,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       key.halo_check = c->n_shards > 1 ? 1 : 0;
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
       key.defer = defer ? 1 : 0;
+      key.nee_regions = (int)nee_regions_per_wave();
       int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
       c->jit_dirty = false;
@@ -706,6 +712,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     }
     p.defer = 1;
     p.nee_cap = 64 * p.max_bounces;
+    p.nee_regions = (int32_t)pass_waves;
     p.nee_rec = c->d_nee_rec;
     p.nee_count = c->d_nee_count;
     p.nee_out = c->d_nee_out;
@@ -735,8 +742,9 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
         // waves wholly outside the viewport write no count
         HIPCHK(c, hipMemsetAsync(c->d_nee_count, 0, pass_waves * sizeof(uint32_t), c->stream));
         HIPCHK(c, launch(p, 1, grid));
-        // one NEE wave per pass wave's region
-        HIPCHK(c, rt0h::jit_launch(c->jit.nee, &p, grid.x * grid.y, 1, 1, c->stream) == RT0_OK
+        // one light-sampling wave per RT0_NEE_REGIONS pass waves' regions
+        const unsigned nee_waves = (unsigned)((pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave());
+        HIPCHK(c, rt0h::jit_launch(c->jit.nee, &p, (nee_waves + 3) / 4, 1, 1, c->stream) == RT0_OK
                       ? hipSuccess
                       : hipErrorLaunchFailure);
         HIPCHK(c, rt0h::jit_launch(c->jit.resolve, &p, grid.x, grid.y, 1, c->stream) == RT0_OK

@@ -93,6 +93,9 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_DEFER_NEE
 #define RT0_DEFER_NEE 0
 #endif
+#ifndef RT0_NEE_REGIONS  // pass-wave record regions per light-sampling wave
+#define RT0_NEE_REGIONS 2
+#endif
 // ReSTIR reservoir taps fetched per batch (temporal levels together, spatial
 // taps RT0_TAP_BATCH at a time); 1 = one tap at a time.  The scene-specialised
 // kernels of ReSTIR scenes without models use 2 (rt0_jit.cpp)
@@ -2363,12 +2366,30 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 // raytracer.glsl:2171-2174).
 template <class Scene, class Cfg, bool VOL, bool SDF, bool SPECTRAL>
 DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
-  // one wave per region of the pass grid (host: gridDim.x = the pass grid's workgroups)
-  const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6);
-  const uint32_t n = min(P.nee_count[gw], (uint32_t)P.nee_cap);
-  const size_t plane = (size_t)P.width * P.height, base = (size_t)gw * (uint32_t)P.nee_cap;
-  for (uint32_t i = threadIdx.x & 63u; i < n; i += 64u) {
-    const NeeRec r = P.nee_rec[base + i];
+  // one wave per RT0_NEE_REGIONS consecutive regions: their records form one
+  // list, so a region's tail chunk does not idle most of a wave (C5 averages
+  // ~68 records per region: one region per wave ran a 64-record chunk and a
+  // 4-record chunk).  Measured 1 / 2 / 4 / 8 regions: C3 5326 / 5491 / 4627 /
+  // 3320, C5 1467 / 1558 / 1513 / 1403 Msamples/s (profiles/r03/defer/)
+  const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6))) *
+                      RT0_NEE_REGIONS;
+  if (r0 >= (uint32_t)P.nee_regions) return;
+  uint32_t cnt[RT0_NEE_REGIONS], total = 0;
+#pragma unroll
+  for (int q = 0; q < RT0_NEE_REGIONS; ++q) {
+    cnt[q] = r0 + q < (uint32_t)P.nee_regions ? min(P.nee_count[r0 + q], (uint32_t)P.nee_cap) : 0u;
+    total += cnt[q];
+  }
+  const size_t plane = (size_t)P.width * P.height;
+  for (uint32_t i = threadIdx.x & 63u; i < total; i += 64u) {
+    uint32_t q = 0, off = i;
+#pragma unroll
+    for (int k = 0; k < RT0_NEE_REGIONS - 1; ++k)
+      if (q == (uint32_t)k && off >= cnt[k]) {
+        off -= cnt[k];
+        q = k + 1;
+      }
+    const NeeRec r = P.nee_rec[(size_t)(r0 + q) * (uint32_t)P.nee_cap + off];
     Integrator<Scene, Cfg, true, VOL, SDF, SPECTRAL, false> it(P, sc, cfg);
     it.frame = P.frame0;
     const int py = r.pix / P.width, px = r.pix - py * P.width;

@@ -64,7 +64,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // per workgroup would cap a CU at three workgroups
   if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
   o << "#define RT0_HALO_CHECK " << k.halo_check << "\n";
-  if (k.defer) o << "#define RT0_DEFER_NEE 1\n";
+  if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
   // occupancy target below); with a BVH the extra registers cost more than

@@ -20,6 +20,7 @@ struct JitKey {
   int bvh_stack = 0;  // LDS traversal stack entries (push bound + 1) when the scene has models
   int halo_check = 1;  // RT0_HALO_CHECK: sharded launches count reservoir fetches outside the halo
   int defer = 0;       // RT0_DEFER_NEE: ReSTIR light sampling in its own kernel (rt0_jit_nee + rt0_jit_resolve)
+  int nee_regions = 2;  // RT0_NEE_REGIONS: pass-wave record regions per light-sampling wave
 };
 
 // The kernels of one compiled module: the pass kernel and, for a deferred

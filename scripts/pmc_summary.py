@@ -58,6 +58,7 @@ def main():
     kernels = []
     by_kernel = {}  # kernel -> {counter: mean per dispatch}
     for d in sys.argv[6:]:
+        in_dir = {}  # this pass directory's counters, the group's kernels summed
         for kernel in GROUP:
             vals, dur = dispatches(d, kernel)
             ids = sorted(vals)[skip:]
@@ -68,13 +69,14 @@ def main():
             names = set().union(*(vals[i].keys() for i in ids))
             for c in names:  # per pass: the group's kernels summed
                 m = sum(vals[i].get(c, 0.0) for i in ids) / len(ids)
-                per[c] = per.get(c, 0.0) + m
+                in_dir[c] = in_dir.get(c, 0.0) + m
                 by_kernel.setdefault(kernel, {})[c] = m
                 n_kept[c] = len(ids)
             if "GRBM_GUI_ACTIVE" in names and kernel == KERNEL:
                 for i in ids:
                     if dur.get(i):
                         clock.append(vals[i]["GRBM_GUI_ACTIVE"] / 8.0 / dur[i])  # cycles per ns = GHz
+        per.update(in_dir)  # a counter collected in two passes: the later pass's value
     res = {"kernel": "+".join(kernels) or KERNEL, "skipped_dispatches": skip, "dispatches_kept": n_kept, "counters": per,
            "algorithmic_bytes_per_launch": W * H * bpp}
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
