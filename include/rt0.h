@@ -320,7 +320,8 @@ int rt0_read_counters_n(rt0_ctx *ctx, uint64_t *out, int n);
 /* Wall time of the kernels of the last rt0_render (HIP events on the
  * context's stream), milliseconds, and the number of kernel launches (a
  * ReSTIR pass with deferred light sampling -- three dependent dispatches on the
- * stream: path, light sampling, resolve -- counts as one). */
+ * stream: path, light sampling, resolve -- counts as one, and so does a
+ * frame-chunked launch: the pass kernel and the frame-order sum after it). */
 int rt0_last_kernel_ms(const rt0_ctx *ctx, float *ms, int *launches);
 /* Bytes of device scratch the context holds for frame-chunked launches
  * (per-frame sample planes over the launch rectangle; grows on demand). */

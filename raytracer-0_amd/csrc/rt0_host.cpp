@@ -804,7 +804,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
         p.samples = c->d_samples;
         HIPCHK(c, launch(p, (unsigned)chunks, grid));
         HIPCHK(c, rt0_launch_sum(&p, grid, c->stream));
-        launches += 2;
+        launches++;  // pass + rt0_sum_kernel: one launch (rt0_last_kernel_ms)
       } else {
         p.frame_chunk = p.nframes;
         p.samples = nullptr;
