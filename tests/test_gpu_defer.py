@@ -1,0 +1,91 @@
+"""Deferred ReSTIR light sampling (rt0_integrator.h pool of NeeRec regions,
+rt0_jit_nee, rt0_jit_resolve) against the inline calls.
+
+Every sampleLightsReSTIR call runs with the same arguments and the same
+source in the deferred kernels as inline.  What can differ is FMA placement
+(the compiler contracts a product into an add only when the product has one
+use, which depends on the surrounding kernel) and the order of a sample's
+final additions (the path's own radiance first, then the light-sampling
+results in call order, instead of interleaved).  Measured on the GPU: 98.7-
+99.7% of samples bit-identical, the rest within 4.8e-7; reservoir MRTs
+(g_final_reservoir, raytracer.glsl:2171-2174) identical except 0-56 of 4096
+pixels per pass, by <= 1.5e-5 relative.  The test holds them to that: every
+reservoir within 1e-4 and every sample within 1e-5 relative (the parity
+tolerance is 1e-3), >= 98% of each bit-identical.
+RT0_DEFER_NEE is read when the context is created (rt0_create).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import rt0
+from test_gpu_parity import cfg_by_name, configure, have
+
+import oracle as O
+
+
+def chain(cfgs, name, defer, n=6, size=64, viewport=None):
+    old = os.environ.get("RT0_DEFER_NEE")
+    os.environ["RT0_DEFER_NEE"] = defer
+    try:
+        r = rt0.Renderer(size, size)
+    finally:
+        if old is None:
+            del os.environ["RT0_DEFER_NEE"]
+        else:
+            os.environ["RT0_DEFER_NEE"] = old
+    cfg = cfg_by_name(cfgs, name)
+    configure(r, cfg, cfgs)
+    r.set_temporal_frames(cfg.get("temporal_frames", 5))
+    if viewport:
+        r.set_viewport(*viewport)
+    S, M, A = [], [], []
+    for k in range(1, n + 1):
+        r.render(k, 1, O.pass_time(cfg, k) if cfg.get("time_ms") else 0.0)
+        S.append(r.read_accum())
+        m, a = r.read_restir(0)
+        M.append(m)
+        A.append(a)
+    return np.stack(S), np.stack(M), np.stack(A)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c3_outdoor_restir", "restir_mis_demo", "c5_spectral_sphere", "anim_restir_demo"])
+def test_deferred_matches_inline(name, cfgs, gpu_required):
+    if not have(name):
+        pytest.skip("fixture not generated")
+    s0, m0, a0 = chain(cfgs, name, "0")
+    s1, m1, a1 = chain(cfgs, name, "1")
+    if os.environ.get("RT0_TEST_DUMP"):
+        np.savez_compressed(os.path.join(os.environ["RT0_TEST_DUMP"], name + "_defer.npz"),
+                            s0=s0, m0=m0, a0=a0, s1=s1, m1=m1, a1=a1)
+    close_and_mostly_identical(m0, m1, "reservoir main")
+    close_and_mostly_identical(a0, a1, "reservoir aux")
+    assert np.isfinite(s1).all()
+    close_and_mostly_identical(s0[..., :3], s1[..., :3], "samples")
+    assert s1[..., :3].mean() > 0.0
+
+
+def close_and_mostly_identical(x, y, what, rel=None):
+    rel = rel or (1e-5 if what == "samples" else 1e-4)
+    d = np.abs(x - y)
+    assert (d <= rel * np.maximum(1.0, np.abs(x))).all(), (what, float(d.max()))
+    same = (x == y).all(-1).mean()
+    assert same >= 0.98, (what, same)
+
+
+@pytest.mark.gpu
+def test_deferred_viewport_matches_inline(cfgs, gpu_required):
+    """A tile (gl.viewport rectangle, index.js:761-792) with deferral: only
+    the rectangle's pixels get records, and they resolve like the inline
+    render of the same rectangle."""
+    vp = (8, 16, 40, 24)
+    s0, m0, a0 = chain(cfgs, "c3_outdoor_restir", "0", n=3, viewport=vp)
+    s1, m1, a1 = chain(cfgs, "c3_outdoor_restir", "1", n=3, viewport=vp)
+    close_and_mostly_identical(m0, m1, "reservoir main")
+    close_and_mostly_identical(a0, a1, "reservoir aux")
+    close_and_mostly_identical(s0[..., :3], s1[..., :3], "samples")
+    outside = np.ones(s1.shape[1:3], bool)
+    outside[vp[1]:vp[1] + vp[3], vp[0]:vp[0] + vp[2]] = False
+    assert not s1[:, outside, :3].any()
