@@ -342,6 +342,39 @@ def pmc_summary(config):
     return None, None
 
 
+def calibration():
+    """{kernel: true bytes / FETCH_SIZE bytes} of scripts/fetch_calib (16-B/lane
+    stream, 64-B gathers, bilinear 2x2 RGBA32F taps), committed under profiles/."""
+    for rd in PROFILE_ROUNDS:
+        path = os.path.join(HERE, "profiles", rd, "calib.json")
+        if os.path.exists(path):
+            c = json.load(open(path))
+            return {k: v["factor"][-1] for k, v in c.items() if v.get("factor")}, "profiles/%s/calib.json" % rd
+    return {}, None
+
+
+def hbm_traffic(pmc, config, pixels, calib):
+    """(estimate, low, high) HBM bytes per launch from the PMC counters.
+    FETCH_SIZE under-reports a 16-B/lane stream by 2x but reports a 64-B gather
+    at x0.99 and bilinear RGBA32F taps at x0.5 (calib), so the correction is by
+    access shape: the accumulator read (16 B/pixel, a stream) at x2; the rest at
+    x2 for the progressive workloads (streams only), at the bilinear factor for
+    C3 (reservoir taps dominate), at the gather factor for C5 (64-B node,
+    48-B triangle and record gathers beside the taps); low/high bound the mix
+    at x0.5 .. x2.  WRITE_SIZE is exact for 16-B/lane stores."""
+    c = pmc["counters"]
+    fetch, write = c["FETCH_SIZE"] * 1024.0, c["WRITE_SIZE"] * 1024.0
+    acc = 16.0 * pixels
+    rest = max(0.0, fetch - acc / 2.0)
+    if config in ("c1", "c2", "c2_refcaps", "c4"):
+        est = lo = hi = 2.0 * fetch + write
+    else:
+        f = calib.get("k_bilin", 0.5) if config == "c3" else calib.get("k_node64", 1.0)
+        est = acc + rest * f + write
+        lo, hi = acc + 0.5 * rest + write, acc + 2.0 * rest + write
+    return est, lo, hi
+
+
 def valu_rates():
     """(ns per non-transcendental, ns per transcendental) wave64 VALU
     instruction per SIMD, measured by scripts/valu_peak (16 independent chains
@@ -448,9 +481,13 @@ def main():
     # workload (FETCH_SIZE x2 gfx950 correction); counters cannot be read from
     # inside this process
     pmc_path, pmc = pmc_summary(args.config) if world == 1 else (None, None)
-    traffic = pmc["traffic_bytes_per_launch"] if pmc else None
+    calib, calib_src = calibration()
+    traffic = lo = hi = None
+    if pmc and "FETCH_SIZE" in pmc.get("counters", {}):
+        traffic, lo, hi = hbm_traffic(pmc, args.config, W * H, calib)
     roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+            "traffic_range": [lo, hi] if traffic else None, "traffic_calibration": calib_src,
             "traffic_unit": "bytes/launch", "traffic_source": pmc_path,
             "algorithmic_bytes": alg_bytes,
             "algorithmic_gbs": round(alg_bytes / kern_launch_s / 1e9, 1),
@@ -466,7 +503,8 @@ def main():
             "kernel_ms_per_launch": round(kern_launch_s * 1000.0, 3),
             "note": "FP32 vector kernel (no MFMA): peak = MI355X FP32 vector 157.3 TF; FLOP model SURVEY 8d x "
                     "counted events (counting instance, whole image); achieved over rank 0's kernel time (HIP "
-                    "events on librt0's stream); hbm_gbs = PMC traffic per launch over the same kernel time"}
+                    "events on librt0's stream); traffic = PMC FETCH_SIZE corrected per access shape (hbm_traffic) + "
+                    "WRITE_SIZE per launch; hbm_gbs = traffic over the same kernel time"}
     if pmc and "valu" in pmc:
         roof["valu_lane_utilisation"] = round(pmc.get("valu_lane_utilisation", 0.0), 4)
         rates = valu_rates()

@@ -19,16 +19,19 @@ For every workload:
     time of their class (scripts/valu_peak: non-transcendental = the mean of
     v_add/v_mul/v_fma rates, transcendental = v_exp_f32's), per SIMD, over the
     median kernel time -- the share of time the VALU pipe is occupied;
-  * HBM traffic: FETCH_SIZE x 1024 B x the calibrated factor of the access
-    shape (scripts/fetch_calib: 16-B/lane stream x2, 64-B gathers x1, bilinear
-    2x2 RGBA32F taps x0.5) + WRITE_SIZE.  A kernel that mixes shapes gets its
-    accumulator stream at x2 and the rest at the factor of its dominant shape
-    (ReSTIR taps x0.5 for C3; C5: reported as the range x0.5 .. x2), over the
-    median kernel time -> GB/s and the fraction of 8 TB/s.
+  * HBM traffic: bench.py's hbm_traffic -- FETCH_SIZE x 1024 B x the
+    calibrated factor of the access shape (scripts/fetch_calib: 16-B/lane
+    stream x2, 64-B gathers x1, bilinear 2x2 RGBA32F taps x0.5) + WRITE_SIZE;
+    a kernel that mixes shapes gets its accumulator stream at x2 and the rest
+    at the factor of its dominant shape, with the x0.5 .. x2 range beside it;
+    over the median kernel time -> GB/s and the fraction of 8 TB/s.
 """
 import json
 import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import hbm_traffic  # noqa: E402
 
 PEAK_SPEC = 157.3
 D = sys.argv[1]
@@ -82,18 +85,8 @@ for c in ("c1", "c2", "c3", "c4", "c5"):
         row["stall_share"] = pmc.get("stall_share")
         cnt = pmc.get("counters", {})
         if "FETCH_SIZE" in cnt and "WRITE_SIZE" in cnt:
-            fetch = cnt["FETCH_SIZE"] * 1024.0  # counter bytes as reported
-            write = cnt["WRITE_SIZE"] * 1024.0
-            acc = 16.0 * pixels  # the accumulator read: a 16-B/lane stream
-            rest = max(0.0, fetch - acc / 2.0)  # counter bytes of everything else
-            if c in ("c1", "c2", "c4"):
-                lo = hi = est = 2.0 * fetch + write
-            elif c == "c3":  # bilinear reservoir taps dominate the rest
-                est = acc + rest * (fac.get("k_bilin") or 0.5) + write
-                lo, hi = acc + 0.5 * rest + write, acc + 2.0 * rest + write
-            else:  # c5: taps, 64-B node / 48-B triangle gathers and spills mixed
-                lo, hi = acc + 0.5 * rest + write, acc + 2.0 * rest + write
-                est = acc + rest * (fac.get("k_node64") or 1.0) + write
+            fetch, write = cnt["FETCH_SIZE"] * 1024.0, cnt["WRITE_SIZE"] * 1024.0
+            est, lo, hi = hbm_traffic(pmc, c, pixels, fac)  # the bench line's own correction
             row.update(fetch_counter_bytes=fetch, write_bytes=write, traffic_est=est, traffic_lo=lo, traffic_hi=hi,
                        hbm_gbs=est / (med * 1e-3) / 1e9, hbm_frac=est / (med * 1e-3) / 8e12,
                        algorithmic_bytes=pmc.get("algorithmic_bytes_per_launch"))

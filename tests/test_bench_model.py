@@ -1,0 +1,58 @@
+"""bench.py's measurement model on CPU: the FLOP model's terms, the HBM
+traffic correction by access shape, the measured VALU rates and the committed
+profiles it reads."""
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+
+def test_isect_flop_cornell_is_survey_figure():
+    wl = json.load(open(os.path.join(REPO, "raytracer-0_amd", "rt0", "workloads.json")))["workloads"]["c2"]
+    assert bench.isect_flop(wl["scene_lines"]) == 151.0  # 150
+
+
+def test_hbm_traffic_by_access_shape():
+    pmc = {"counters": {"FETCH_SIZE": 1000.0, "WRITE_SIZE": 300.0}}  # KiB
+    fetch, write = 1000.0 * 1024, 300.0 * 1024
+    est, lo, hi = bench.hbm_traffic(pmc, "c2", 1000, {})
+    assert est == lo == hi == 2.0 * fetch + write  # streams only: FETCH_SIZE x2
+    calib = {"k_bilin": 0.5, "k_node64": 0.99}
+    acc = 16.0 * 1000
+    rest = fetch - acc / 2.0
+    est, lo, hi = bench.hbm_traffic(pmc, "c3", 1000, calib)
+    assert est == pytest.approx(acc + 0.5 * rest + write)
+    assert lo <= est <= hi and hi == pytest.approx(acc + 2.0 * rest + write)
+    est5, _, _ = bench.hbm_traffic(pmc, "c5", 1000, calib)
+    assert est5 == pytest.approx(acc + 0.99 * rest + write)
+
+
+def test_committed_profiles_feed_the_bench_line():
+    """The files the bench line cites exist and hold what it reads."""
+    rates = bench.valu_rates()
+    assert rates is not None, "profiles/<round>/valu_peak.json missing"
+    ns_valu, ns_trans, src = rates
+    assert 0.5 < ns_valu < 2.0 and ns_trans > 2.0 * ns_valu, (ns_valu, ns_trans)  # transcendentals are slow
+    calib, csrc = bench.calibration()
+    assert csrc and abs(calib["k_stream"] - 2.0) < 0.05
+    for c in ("c1", "c2", "c3", "c4", "c5"):
+        path, pmc = bench.pmc_summary(c)
+        assert pmc is not None, c
+        assert {"FETCH_SIZE", "WRITE_SIZE"} <= set(pmc["counters"]), c
+        assert pmc["valu"]["SQ_INSTS_VALU"] > pmc["valu"]["SQ_INSTS_VALU_TRANS_F32"] > 0, c
+
+
+def test_roofline_summary_reproduces_committed_table(tmp_path):
+    """profiles/r03/roofline.md is what scripts/roofline_summary.py computes
+    from the committed per-workload files (no hand edits)."""
+    import subprocess
+    d = os.path.join(REPO, "profiles", "r03")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "roofline_summary.py"), d],
+                         capture_output=True, text=True, check=True).stdout
+    assert out == open(os.path.join(d, "roofline.md")).read()
