@@ -12,7 +12,10 @@
 //                                 SIMD cycles per instruction at the clock
 //                                 the fma kernel implies (spec: 2 cycles)
 // plus pairs interleaved 1:1 (fma+add_u32, fma+exp, fma+cndmask) to see
-// whether two instruction classes share one issue port.
+// whether two instruction classes share one issue port.  Covers the classes
+// the integrator issues: FP32 add/mul/fma, moves, integer add/shift/multiply
+// (the RNG hash, raytracer.glsl:302-306), conversions, floor (hash2), the
+// transcendentals (exp, sqrt, rcp, sin), compares and selects.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -47,6 +50,13 @@
 #define B_MOV(k) asm volatile("v_mov_b32 %0, %0" : "+v"(x[k]));
 #define B_IADD(k) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[k]) : "v"(b));
 #define B_EXP(k) asm volatile("v_exp_f32 %0, %0" : "+v"(x[k]));
+#define B_IMUL(k) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[k]) : "v"(b));
+#define B_CVT(k) asm volatile("v_cvt_f32_i32 %0, %0" : "+v"(x[k]));
+#define B_FLOOR(k) asm volatile("v_floor_f32 %0, %0" : "+v"(x[k]));
+#define B_SQRT(k) asm volatile("v_sqrt_f32 %0, %0" : "+v"(x[k]));
+#define B_RCP(k) asm volatile("v_rcp_f32 %0, %0" : "+v"(x[k]));
+#define B_SIN(k) asm volatile("v_sin_f32 %0, %0" : "+v"(x[k]));
+#define B_LSHR(k) asm volatile("v_lshrrev_b32 %0, %1, %0" : "+v"(x[k]) : "v"(b));
 #define B_CND(k) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(x[k]) : "v"(b), "s"(m));
 #define B_CMP(k) asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(mk[k & 3]) : "v"(x[k]), "v"(a));
 #define B_FMA_IADD(k) \
@@ -65,6 +75,13 @@ VKERNEL(k_mul, DECL_F, INIT_F, B_MUL, FOLD_F)
 VKERNEL(k_mov, DECL_F, INIT_F, B_MOV, FOLD_F)
 VKERNEL(k_iadd, DECL_F, INIT_F, B_IADD, FOLD_F)
 VKERNEL(k_exp, DECL_F, INIT_F, B_EXP, FOLD_F)
+VKERNEL(k_imul, DECL_F, INIT_F, B_IMUL, FOLD_F)
+VKERNEL(k_cvt, DECL_F, INIT_F, B_CVT, FOLD_F)
+VKERNEL(k_floor, DECL_F, INIT_F, B_FLOOR, FOLD_F)
+VKERNEL(k_sqrt, DECL_F, INIT_F, B_SQRT, FOLD_F)
+VKERNEL(k_rcp, DECL_F, INIT_F, B_RCP, FOLD_F)
+VKERNEL(k_sin, DECL_F, INIT_F, B_SIN, FOLD_F)
+VKERNEL(k_lshr, DECL_F, INIT_F, B_LSHR, FOLD_F)
 VKERNEL(k_cnd, DECL_F; unsigned long long m = __ballot(threadIdx.x & 1), INIT_F, B_CND, FOLD_F)
 VKERNEL(k_cmp, DECL_F; unsigned long long mk[4]; mk[0] = mk[1] = mk[2] = mk[3] = 0, INIT_F, B_CMP,
         FOLD_F; s += (float)(mk[0] ^ mk[1] ^ mk[2] ^ mk[3]))
@@ -109,7 +126,11 @@ int main() {
                   {"v_add_f32", k_add, 1, 1.0},       {"v_mul_f32", k_mul, 1, 1.0},
                   {"v_mov_b32", k_mov, 1, 0.0},       {"v_add_u32", k_iadd, 1, 0.0},
                   {"v_exp_f32", k_exp, 1, 0.0},       {"v_cndmask_b32", k_cnd, 1, 0.0},
-                  {"v_cmp_gt_f32", k_cmp, 1, 0.0},    {"fma+add_u32", k_fma_iadd, 2, 1.0},
+                  {"v_cmp_gt_f32", k_cmp, 1, 0.0},    {"v_mul_lo_u32", k_imul, 1, 0.0},
+                  {"v_cvt_f32_i32", k_cvt, 1, 0.0},   {"v_floor_f32", k_floor, 1, 0.0},
+                  {"v_sqrt_f32", k_sqrt, 1, 0.0},     {"v_rcp_f32", k_rcp, 1, 0.0},
+                  {"v_sin_f32", k_sin, 1, 0.0},       {"v_lshrrev_b32", k_lshr, 1, 0.0},
+                  {"fma+add_u32", k_fma_iadd, 2, 1.0},
                   {"fma+exp", k_fma_exp, 2, 1.0},     {"fma+cndmask", k_fma_cnd, 2, 1.0}};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
