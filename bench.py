@@ -135,7 +135,8 @@ def cpu_baseline_js(wl, budget_s=10.0):
     fp32 restatement of the same integrator, parity-checked in
     tests/test_cpu_js.py) on node worker_threads, timed on a bounded sample of
     the same workload: a 64-row band through the image centre, successive
-    passes until the time budget."""
+    passes until the time budget (ReSTIR workloads: the band's passes run
+    the reservoir chain, the rest of the planes stays empty)."""
     import shutil
     node = shutil.which("node")
     if node is None:
@@ -145,7 +146,8 @@ def cpu_baseline_js(wl, budget_s=10.0):
     r0 = H // 2 - 32
     r = subprocess.run([node, os.path.join(HERE, "oracle", "js", "cpu_bench.js"),
                         os.path.join(HERE, "tests", "golden", "configs.json"), wl["fixture"], str(W), str(H),
-                        str(threads), "bench", str(r0), str(r0 + 64), str(budget_s)]
+                        str(threads), "restir-bench" if wl.get("defines", {}).get("USE_RESTIR") else "bench",
+                        str(r0), str(r0 + 64), str(budget_s)]
                        + (["--constants", json.dumps(wl["constants"])]),
                        capture_output=True, text=True, timeout=budget_s * 10 + 60)
     if r.returncode != 0:
@@ -558,9 +560,9 @@ def main():
         out["secondary_refcaps_Msamples_s"] = round(W * H * sec["spp"] * args.steps
                                                     / (time.perf_counter() - t1) / 1e6, 3)
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-        # the JS integrator covers quadrics, SDFs, media and MIS (SURVEY 8d's
-        # C1/C2/C4 feature sets), not ReSTIR or triangle models
-        js_gap = ("ReSTIR" if workloads.restir(wl) else None) or ("triangle models" if wl.get("models") else None)
+        # the JS integrator covers quadrics, SDFs, media, MIS and ReSTIR
+        # (SURVEY 8d's C1-C4 feature sets), not spectral rendering or triangle models
+        js_gap = "triangle models and spectral rendering" if wl.get("models") else None
         js = None if js_gap else cpu_baseline_js(wl)
         c_port = cpu_baseline_c(wl)
         out["cpu_baseline"] = js if js and "value" in js else c_port

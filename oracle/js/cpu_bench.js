@@ -9,6 +9,15 @@
 //                                          [--constants JSON] overrides constants,
 //                                          successive passes until the deadline;
 //                                          prints {"samples", "seconds", "msamples_s", ...}
+//   mode "restir-image" <n> <out>        : ReSTIR passes 1..n of the whole image with
+//                                          index.js's swap chain (795-820): per pass the
+//                                          sample and both reservoir MRTs -> <out> as
+//                                          [n][3][H][W][4] f32
+//   mode "restir-bench" <y0> <y1> <seconds>: ReSTIR passes on rows [y0,y1) (the rest of
+//                                          the reservoir planes stays empty), the swap
+//                                          chain after each, until the deadline
+// ReSTIR modes keep the eight reservoir planes in SharedArrayBuffers; the
+// threads render one pass's rows each and meet between passes.
 const os = require('os');
 const fs = require('fs');
 const path = require('path');
@@ -23,7 +32,24 @@ function makeRenderer(d) {
   return new CpuRenderer(cfg, cfgs.cornell_lines, cfgs.default_camera, d.W, d.H);
 }
 
-if (!isMainThread) {
+// plane roles of the swap chain: [out main, out aux, back, back aux, hist1, hist1 aux, hist2, hist2 aux]
+function nextRoles(k) {  // outputs become the newest (back), back -> hist1, hist1 -> hist2, hist2 recycled
+  return [k[6], k[7], k[0], k[1], k[2], k[3], k[4], k[5]];
+}
+
+if (!isMainThread && workerData.mode && workerData.mode.startsWith('restir')) {
+  const d = workerData;
+  const r = makeRenderer(d);
+  const planes = d.planes.map((b) => new Float32Array(b));
+  const sample = new Float32Array(d.sample);
+  parentPort.on('message', (msg) => {
+    if (msg.quit) { process.exit(0); }
+    const k = msg.roles;
+    r.tex = [planes[k[2]], planes[k[3]], planes[k[4]], planes[k[5]], planes[k[6]], planes[k[7]]];
+    r.renderPass(msg.frame, d.y0, d.y1, sample, planes[k[0]], planes[k[1]]);
+    parentPort.postMessage({ done: true, samples: (d.y1 - d.y0) * d.W });
+  });
+} else if (!isMainThread) {
   const d = workerData;
   const r = makeRenderer(d);
   if (d.mode === 'image') {
@@ -59,7 +85,56 @@ if (!isMainThread) {
     w.on('message', res);
     w.on('error', rej);
   })));
-  if (mode === 'image') {
+  // ReSTIR: persistent workers over shared planes, one pass at a time
+  const restir = (y0, y1, passes, deadline, onPass) => {
+    const n = base.W * base.H * 4;
+    const planes = Array.from({ length: 8 }, () => new SharedArrayBuffer(n * 4));
+    const sample = new SharedArrayBuffer(n * 4);
+    const ws = split(y0, y1).map(([lo, hi]) => new Worker(__filename, {
+      workerData: Object.assign({ mode, y0: lo, y1: hi, planes, sample }, base) }));
+    let roles = [0, 1, 2, 3, 4, 5, 6, 7], samples = 0;
+    const t0 = process.hrtime.bigint();
+    // one persistent handler per worker: the pending pass's resolve/reject
+    const pending = ws.map(() => null);
+    ws.forEach((w, i) => {
+      w.on('message', (m) => { samples += m.samples; const p = pending[i]; pending[i] = null; p.res(); });
+      w.on('error', (e) => { const p = pending[i]; if (p) p.rej(e); else { console.error(e); process.exit(1); } });
+    });
+    const passOnce = (frame) => Promise.all(ws.map((w, i) => new Promise((res, rej) => {
+      pending[i] = { res, rej };
+      w.postMessage({ frame, roles });
+    })));
+    const loop = async () => {
+      for (let frame = 1; frame <= passes; frame++) {
+        await passOnce(frame);
+        if (onPass) onPass(frame, new Float32Array(sample), new Float32Array(planes[roles[0]]), new Float32Array(planes[roles[1]]));
+        roles = nextRoles(roles);
+        if (deadline && Number(process.hrtime.bigint() - t0) / 1e9 > deadline) break;
+      }
+      ws.forEach((w) => w.postMessage({ quit: true }));
+      return { samples, seconds: Number(process.hrtime.bigint() - t0) / 1e9, threads: ws.length };
+    };
+    return loop();
+  };
+  if (mode === 'restir-image') {
+    const passes = +a[6], out = a[7];
+    const n = base.W * base.H * 4, img = new Float32Array(passes * 3 * n);
+    restir(0, base.H, passes, 0, (frame, s, m, x) => {
+      const o = (frame - 1) * 3 * n;
+      img.set(s, o); img.set(m, o + n); img.set(x, o + 2 * n);
+    }).then((res) => {
+      fs.writeFileSync(out, Buffer.from(img.buffer));
+      console.log(JSON.stringify({ ok: true, threads: res.threads }));
+    }).catch((e) => { console.error(e); process.exit(1); });
+  } else if (mode === 'restir-bench') {
+    const y0 = +a[6], y1 = +a[7], seconds = +a[8];
+    restir(y0, y1, 1 << 30, seconds, null).then((res) => {
+      console.log(JSON.stringify({
+        samples: res.samples, seconds: res.seconds, msamples_s: res.samples / res.seconds / 1e6, threads: res.threads,
+        passes: Math.round(res.samples / ((y1 - y0) * base.W)), cpu: os.cpus()[0].model, node: process.version,
+      }));
+    }).catch((e) => { console.error(e); process.exit(1); });
+  } else if (mode === 'image') {
     const frame0 = +a[6], n = +a[7], out = a[8];
     run(split(0, base.H).map(([y0, y1]) => Object.assign({ mode, frame0, n, y0, y1 }, base))).then((parts) => {
       const img = new Float32Array(base.W * base.H * 4);

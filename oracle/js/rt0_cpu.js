@@ -14,8 +14,12 @@
 // configs -- planes, spheres, boxes, SDFs (every #sdf_meshes kind, sphere-traced
 // with calcNormal), every untextured material, sky, plain NEE, MIS, SDF lights,
 // homogeneous volumetrics (free-flight sampling, in-scatter NEE, HG phase, fog
-// transmittance).  Spectral, ReSTIR, cubemap and texture configs are rejected
-// (the C oracle covers them).
+// transmittance), and ReSTIR in RENDER_MODE 0 (sampleLightsReSTIR with its
+// candidates, two-level temporal history, spatial taps, finalize, MRT packing:
+// renderPass() takes the six reservoir input planes and writes the two MRTs,
+// the caller runs index.js's swap chain), under GLSL semantics.  Spectral,
+// animated-mode, cubemap and texture configs are rejected (the C oracle covers
+// them).
 const f = Math.fround;
 
 // ------------------------------------------------------------------ RNG
@@ -212,18 +216,57 @@ function parseScene(lines) {
   return { meshes, lights, nMeshes };
 }
 
+// ------------------------------------------------- ReSTIR (1264-1801)
+function EMPTY_RES() { return { pos: V(0, 0, 0), col: V(0, 0, 0), ws: 0, M: 0, W: 0, age: 0, idx: -1 }; }
+const POISSON = [[-0.4706, 0.4706], [0.8090, 0.2628], [-0.2628, -0.8090], [0.6882, -0.5000],
+  [-0.9511, -0.1625], [0.1625, 0.9511], [0.5000, -0.6882], [-0.6882, 0.5000]].map((p) => [f(p[0]), f(p[1])]);
+const LUM = V(f(0.2126), f(0.7152), f(0.0722));
+const finite = (x) => Number.isFinite(x);
+// updateReservoir, 1305-1326
+function updateReservoir(r, pos, col, idx, weight, rnd) {
+  if (weight <= 0) return;
+  r.ws = f(r.ws + weight);
+  r.M = f(r.M + 1);
+  if (r.M > 60) { r.ws = f(r.ws * f(0.95)); r.M = f(r.M * f(0.95)); }
+  if (r.ws > 0) {
+    const p = f(weight / r.ws);
+    if (rnd < p) { r.pos = pos; r.col = col; r.idx = idx; }
+  }
+}
+// evaluateTargetFunction, 1361-1387
+function targetFn(lp, lc, hp, hn, m) {
+  const lv = sub(lp, hp), distSq = dot(lv, lv);
+  if (distSq < f(EPS * EPS)) return 0;
+  const ld = normalize(lv), ct = gmax(0, dot(hn, ld));
+  if (ct <= 0) return 0;
+  const llum = dot(lc, LUM);
+  if (llum <= 0) return 0;
+  const slum = dot(m.c, LUM);
+  const nnt = f(f(m.nt - 1) / f(m.nt + 1)), R0 = f(nnt * nnt);
+  const isRefr = (m.mt === M_REFR_FRESNEL || m.mt === M_REFR_SCHLICK) ? 1 : 0, isCoat = m.mt === M_COAT ? 1 : 0;
+  const base = mixf(slum, R0, isRefr);
+  const bw = f(mixf(base, f(f(1 - R0) * slum), isCoat) * ONE_OVER_PI);
+  return f(f(f(llum * bw) * ct) / gmax(distSq, f(1e-4)));
+}
+
 // ---------------------------------------------------------- renderer
 class CpuRenderer {
   // cfg: a tests/golden/configs.json entry; cornell: cfgs.cornell_lines; camera default
   constructor(cfg, cornellLines, defaultCamera, width, height) {
     const defs = Object.assign({ USE_PROCEDURAL_SKY: true, USE_BIASED_SAMPLING: true }, cfg.defines || {});
-    for (const k of ['USE_RESTIR', 'USE_SPECTRAL', 'USE_CUBEMAP'])
+    for (const k of ['USE_SPECTRAL', 'USE_CUBEMAP'])
       if (defs[k]) throw new Error(k + ' is outside the JS baseline');
     const c = Object.assign({
       MAX_BOUNCES: 12, MAX_DIFF_BOUNCES: 4, MAX_SPEC_BOUNCES: 4, MAX_TRANS_BOUNCES: 12, MAX_SCATTERING_EVENTS: 12,
       sample_lights: true, use_mis: false, use_restir: false, MARCHING_STEPS: 128, FUDGE_FACTOR: 0.9,
+      RESTIR_SAMPLES: 16, RENDER_MODE: 0,
     }, cfg.constants || {});
-    if (c.use_restir) throw new Error('use_restir is outside the JS baseline');
+    if (c.RENDER_MODE !== 0) throw new Error('RENDER_MODE 1 is outside the JS baseline');
+    this.restir = !!c.use_restir;
+    this.restirDef = !!defs.USE_RESTIR;
+    this.restirSamples = c.RESTIR_SAMPLES;
+    this.tex = [null, null, null, null, null, null];  // reservoir inputs: back, back aux, hist1, hist1 aux, hist2, hist2 aux
+    this.fr = EMPTY_RES();  // g_final_reservoir of the current fragment
     this.sky = !!defs.USE_PROCEDURAL_SKY;
     this.biased = !!defs.USE_BIASED_SAMPLING;
     this.maxB = c.MAX_BOUNCES; this.maxD = c.MAX_DIFF_BOUNCES; this.maxS = c.MAX_SPEC_BOUNCES;
@@ -419,6 +462,189 @@ class CpuRenderer {
     return f(1 / FOUR_PI);
   }
 
+  // isValidReservoir, 1389-1416
+  validRes(r) {
+    if (!finite(r.M) || !finite(r.ws) || !finite(r.W) || !finite(r.age)) return false;
+    if (r.M <= 0 || r.M > 200) return false;
+    if (r.ws <= 0 || r.ws > 1000) return false;
+    if (r.W < 0 || r.W > 20) return false;
+    if (r.age < 0 || r.age > 35) return false;
+    const lc = dot(r.col, r.col);
+    if (lc < f(0.000001) || lc > 10000) return false;
+    if (r.idx >= this.lights.length && r.idx !== -1) return false;
+    if (dot(r.pos, r.pos) < f(EPS * EPS) && r.idx >= 0) return false;
+    return true;
+  }
+  // isVisible, 1539-1557
+  visible(from, to) {
+    let sd = sub(to, from);
+    const dist = length(sd);
+    if (dist < f(EPS * 10)) return true;
+    sd = normalize(sd);
+    const h = this.intersect(add(from, muls(muls(sd, EPS), 2)), sd);
+    if (h.t < f(dist - f(EPS * 2))) {
+      if (h.index >= 0 && h.index < this.meshes.length) return this.meshes[h.index].mt === M_LIGHT;
+      return false;
+    }
+    return true;
+  }
+  // texture(sampler, uv) of an RGBA32F plane: GL LINEAR + CLAMP_TO_EDGE, level 0
+  bilinear(tex, u, v) {
+    if (!tex) return [0, 0, 0, 0];
+    const W = this.w, H = this.h;
+    const x = f(f(u * W) - 0.5), y = f(f(v * H) - 0.5);
+    const fx0 = Math.floor(x), fy0 = Math.floor(y), a = f(x - fx0), b = f(y - fy0);
+    const cl = (i, n) => (i < 0 ? 0 : (i > n - 1 ? n - 1 : i));
+    const x0 = cl(fx0, W), x1 = cl(fx0 + 1, W), y0 = cl(fy0, H), y1 = cl(fy0 + 1, H);
+    const out = [0, 0, 0, 0];
+    for (let c = 0; c < 4; c++) {
+      const t00 = tex[(y0 * W + x0) * 4 + c], t10 = tex[(y0 * W + x1) * 4 + c];
+      const t01 = tex[(y1 * W + x0) * 4 + c], t11 = tex[(y1 * W + x1) * 4 + c];
+      const top = f(t00 + f(a * f(t10 - t00))), bot = f(t01 + f(a * f(t11 - t01)));
+      out[c] = f(top + f(b * f(bot - top)));
+    }
+    return out;
+  }
+  // unpackReservoir, 1437-1468
+  unpack(m, a) {
+    const r = EMPTY_RES();
+    if (m[3] > 0) {
+      r.pos = V(m[0], m[1], m[2]);
+      r.W = m[3];
+      r.col = V(a[0], a[1], a[2]);
+      const pa = a[3];
+      const nli = fract(f(pa * f(2.94)));
+      const temp = f(pa - f(nli * f(0.34)));
+      const nM = fract(f(temp * f(3.03)));
+      const nage = f(f(temp - f(nM * f(0.33))) * f(3.03));
+      r.age = f(nage * 30);
+      r.M = f(nM * 100);
+      const len1 = this.lights.length > 1 ? this.lights.length : 1;
+      r.idx = Math.trunc(f(nli * len1)) - 1;
+      if (r.idx < -1) r.idx = -1;
+      if (r.idx > this.lights.length - 1) r.idx = this.lights.length - 1;
+      r.M = gmax(1, r.M);
+      r.ws = f(r.W * r.M);
+    }
+    return r;
+  }
+  // combineReservoirs, 1579-1611
+  combine(t, s, hp, hn, m, rnd) {
+    if (!this.validRes(s)) return;
+    const tw = targetFn(s.pos, s.col, hp, hn, m);
+    if (tw <= 0) return;
+    const sc = clamp(f(f(tw * gmax(s.W, 0)) * gmax(s.M, 1)), 0, 200);
+    t.ws = f(t.ws + sc);
+    t.M = f(t.M + s.M);
+    if (t.M > 40) {
+      const inv = f(40 / t.M);
+      t.ws = f(t.ws * inv);
+      t.M = 40;
+    }
+    if (t.ws > 0) {
+      const p = f(sc / t.ws);
+      if (rnd < p) { t.pos = s.pos; t.col = s.col; t.idx = s.idx; t.age = gmin(f(s.age + f(0.25)), 30); }
+    }
+  }
+  // sampleLightsReSTIR, 1619-1801 (RENDER_MODE 0); sets this.fr (g_final_reservoir)
+  restirLight(hp, hn, m, sx, sy, frame) {
+    if (!this.restir) return V(0, 0, 0);
+    const nl = this.lights.length;
+    if (nl === 0 || this.lights[0] < 0) return V(0, 0, 0);
+    const scx = f(this.fcx / this.w), scy = f(this.fcy / this.h);
+    const init = EMPTY_RES();
+    const eff = Math.min(this.restirSamples, Math.max(nl, 4));
+    for (let i = 0; i < eff; i++) {
+      const rv = hash2(f(sx + f(f(i) * f(0.1))), f(sy + f(f(i) * f(0.2))));
+      let ai = Math.trunc(f(rv[0] * nl));
+      ai = ai < 0 ? 0 : (ai > nl - 1 ? nl - 1 : ai);
+      const li = this.lights[ai];
+      if (li < 0 || li >= this.meshes.length) continue;
+      const L = this.meshes[li];
+      const tv = targetFn(L.pos, mul(L.c, L.e), hp, hn, m);
+      if (tv > 0) updateReservoir(init, L.pos, mul(L.c, L.e), li, tv, rv[1]);
+    }
+    const tr = Object.assign({}, init);
+    if (frame > 2) {
+      for (let lvl = 0; lvl < 2; lvl++) {  // sampleTemporalHistory, 1485-1523
+        let h = EMPTY_RES();
+        const m3 = sub(hp, this.camPos);
+        const ms = f(f(0.001) * (lvl + 1));
+        const mvx = f(m3.x * ms), mvy = f(m3.y * ms);
+        const js = f(f(lvl + frame) * f(0.1));
+        const hj = hash2(f(scx + js), f(scy + js));
+        const jx = f(f(hj[0] - 0.5) * f(0.002)), jy = f(f(hj[1] - 0.5) * f(0.002));
+        const px = f(f(scx + mvx) + jx), py = f(f(scy + mvy) + jy);
+        if (!(px < f(0.01) || px > f(0.99) || py < f(0.01) || py > f(0.99))) {
+          h = this.unpack(this.bilinear(this.tex[lvl === 0 ? 2 : 4], px, py),
+            this.bilinear(this.tex[lvl === 0 ? 3 : 5], px, py));
+          if (this.validRes(h)) h.age = f(h.age + (lvl + 1));
+        }
+        if (this.validRes(h) && h.M > 0 && h.age < 30) {
+          h.age = f(h.age + (lvl + 1));
+          let ta = f(0.95);
+          if (lvl === 1) ta = f(ta * f(0.80));
+          h.M = f(h.M * ta);
+          h.ws = f(h.ws * ta);
+          const trand = hash(f(f(sx + f(789.123)) + f(f(lvl) * f(456.789))));
+          this.combine(tr, h, hp, hn, m, trand);
+        }
+      }
+      if (tr.M > 100) { tr.M = gmin(tr.M, 80); tr.ws = f(tr.ws * f(0.9)); }
+    }
+    const fr = Object.assign({}, tr);
+    let ns = 8;
+    if (nl > 10) ns = 4;
+    if (frame < 10) ns = Math.max(Math.trunc(ns / 2), 2);
+    for (let i = 0; i < ns; i++) {
+      const sr = hash2(f(sx + f(f(i) * f(0.3))), f(sy + f(f(i) * f(0.4))));
+      const ox = f(f(POISSON[i][0] * 16) / this.w), oy = f(f(POISSON[i][1] * 16) / this.h);
+      const nx = f(scx + ox), ny = f(scy + oy);
+      let nb = EMPTY_RES();
+      if (!(nx < 0 || nx > 1 || ny < 0 || ny > 1)) nb = this.unpack(this.bilinear(this.tex[0], nx, ny), this.bilinear(this.tex[1], nx, ny));
+      if (nb.M > 0) {
+        if (nb.idx >= 0) {
+          const ldf = sub(nb.pos, hp);
+          if (dot(ldf, ldf) > 225) continue;
+        }
+        if (nb.age > 24 || sr[0] < f(0.03)) continue;
+        this.combine(fr, nb, hp, hn, m, sr[1]);
+      }
+    }
+    // finalizeReservoir, 1525-1576
+    if (fr.ws <= 0 || fr.M <= 0) fr.W = 0;
+    else {
+      const tp = targetFn(fr.pos, fr.col, hp, hn, m);
+      if (tp <= 0 || !this.visible(hp, fr.pos)) fr.W = 0;
+      else {
+        const cM = clamp(fr.M, 1, 40);
+        const raw = f(fr.ws / f(tp * cM));
+        let bc = 1;
+        if (fr.age > 0) {
+          const na = clamp(f(fr.age / 30), 0, 1);
+          bc = f(bc * mixf(f(0.85), 1, f(1 - f(na * f(0.3)))));
+        }
+        if (cM > 16) bc = f(bc * f(Math.sqrt(f(16 / cM))));
+        fr.W = clamp(f(bc * raw), 0, 12);
+        if (!finite(fr.W)) fr.W = 0;
+      }
+    }
+    fr.age = gmin(fr.age, 30);
+    this.fr = fr;
+    if (fr.W > 0 && fr.idx >= 0 && fr.idx < nl) {
+      const act = this.lights[fr.idx];
+      if (act >= 0 && act < this.meshes.length) {
+        const lc = this.directLight(act, hp, hn, f(sx + f(456.789)));
+        let ew = clamp(fr.W, 0, 8);
+        if (fr.M > 30) ew = f(ew * f(Math.sqrt(f(30 / fr.M))));
+        const fc = muls(lc, ew);
+        if (!finite(fc.x) || !finite(fc.y) || !finite(fc.z)) return V(0, 0, 0);
+        return fc;
+      }
+    }
+    return V(0, 0, 0);
+  }
+
   // radiance() + brdf(), 1986-2105 and 1804-1980
   radiance(ro, rd, seed, frame) {
     let acc = V(0, 0, 0), mask = V(1, 1, 1), spec = true, prevNl = V(0, 1, 0);
@@ -522,7 +748,32 @@ class CpuRenderer {
           rd = rdir; mask = mul(mask, c); diffB++; spec = false;
         }
       }
-      if (!spec && this.sampleLights) {  // 1899-1976
+      if (!spec && this.sampleLights && this.restir) {  // 1900-1946: ReSTIR routes
+        if (this.restirDef) {
+          const sx = f(f(seed + f(f(8652.1) * fr)) + f(bounce * f(7895.13)));
+          const sy = f(f(seed + f(f(1234.567) * fr)) + f(bounce * f(9876.54)));
+          let tot = V(0, 0, 0);
+          if (!this.mis || this.lights.length > 8) {
+            tot = this.restirLight(x, nl, m, sx, sy, frame);
+          } else {  // use_mis with <= 8 lights: importance-culled MIS over the lights
+            const base = f(f(f(seed + f(f(8652.1) * fr)) + f(5681.123)) + f(bounce * f(7895.13)));
+            for (let i = 0; i < this.lights.length; i++) {
+              const idx = this.lights[i];
+              if (idx < 0) continue;
+              const L = this.meshes[idx];
+              if (L.mt !== M_LIGHT) continue;
+              const lv = sub(L.pos, x), ld = normalize(lv), dsq = dot(lv, lv);
+              const ct = gmax(0, dot(nl, ld));
+              const imp = f(f(ct * dot(L.e, LUM)) * isqrt(f(dsq + 1)));
+              if (imp < f(0.001)) continue;
+              const ls = this.directLight(idx, x, nl, f(base + f(f(i) * f(123.456))));
+              if (dot(ls, ls) < f(f(0.001) * f(0.001))) continue;
+              tot = add(tot, muls(ls, CpuRenderer.power(CpuRenderer.lightPdf(L, x), CpuRenderer.cosPdf(ld, nl))));
+            }
+          }
+          acc = add(acc, mul(tot, mask));
+        }
+      } else if (!spec && this.sampleLights) {  // 1899-1976
         const base = f(f(f(seed + f(f(8652.1) * fr)) + f(5681.123)) + f(bounce * f(7895.13)));
         let lc = V(0, 0, 0);
         for (let i = 0; i < this.lights.length; i++) {
@@ -552,6 +803,9 @@ class CpuRenderer {
   sample(px, py, frame) {
     const rx = f(this.w), ry = f(this.h);
     const fcx = f(px + 0.5), fcy = f(py + 0.5);
+    this.fcx = fcx;
+    this.fcy = fcy;
+    this.fr = EMPTY_RES();
     const stx = f(f(f(2 * fcx) / rx) - 1), sty = f(f(f(2 * fcy) / ry) - 1);
     const seed = hash(f(f(f(fcx * f(12.9898)) + f(fcy * f(78.233))) + f(f(1113.1) * f(frame))));
     const uVLen = f(Math.tan(f(f(this.camParams.x * RAD) * 0.5)));
@@ -570,6 +824,25 @@ class CpuRenderer {
     const rad = f(hash(f(seed + f(249.1686))) * this.camParams.y);
     const ap = muls(add(muls(u, fcos(ang)), muls(v, fsin(ang))), rad);
     return this.radiance(add(this.camPos, ap), normalize(sub(fp, ap)), seed, frame);
+  }
+
+  // One ReSTIR pass over rows [y0, y1): sample[y][x] = that pass's sample
+  // (rgb, a = 0); main/aux = the packed g_final_reservoir MRTs (1418-1433,
+  // 2171-2179).  this.tex holds the six reservoir input planes (W*H RGBA
+  // Float32Arrays, rows bottom-up, or null for zeros).
+  renderPass(frame, y0, y1, sample, main, aux) {
+    const len1 = this.lights.length > 1 ? this.lights.length : 1;
+    for (let y = y0; y < y1; y++) {
+      for (let x = 0; x < this.w; x++) {
+        const s = this.sample(x, y, frame), p = (y * this.w + x) * 4, r = this.fr, have = this.restirDef;
+        sample[p] = s.x; sample[p + 1] = s.y; sample[p + 2] = s.z; sample[p + 3] = 0;
+        main[p] = have ? r.pos.x : 0; main[p + 1] = have ? r.pos.y : 0; main[p + 2] = have ? r.pos.z : 0;
+        main[p + 3] = have ? r.W : 0;
+        const na = clamp(f(r.age / 30), 0, 1), nM = clamp(f(r.M / 100), 0, 1), nli = f((r.idx + 1) / len1);
+        aux[p] = have ? r.col.x : 0; aux[p + 1] = have ? r.col.y : 0; aux[p + 2] = have ? r.col.z : 0;
+        aux[p + 3] = have ? f(f(f(na * f(0.33)) + f(nM * f(0.33))) + f(nli * f(0.34))) : 0;
+      }
+    }
   }
 
   // rows [y0, y1) of passes frame0..frame0+n-1 accumulated: Float32Array RGBA

@@ -1,7 +1,7 @@
 """The JS CPU integrator (oracle/js/rt0_cpu.js) -- the reported CPU baseline
 of bench.py, SURVEY 8d -- renders what the reference renders: checked against
 the golden fixtures (the reference shader under SwiftShader) and the C oracle
-on the configs it covers (quadrics, SDFs, volumetrics).  CPU only."""
+on the configs it covers (quadrics, SDFs, volumetrics, ReSTIR).  CPU only."""
 import json
 import os
 import shutil
@@ -72,6 +72,53 @@ def test_js_bench_mode_reports_throughput():
 
 
 def test_js_integrator_rejects_features_outside_its_scope(tmp_path):
-    r = subprocess.run([NODE, BENCH, CONFIGS, "c3_outdoor_restir", "16", "16", "1", "image", "1", "1",
-                        str(tmp_path / "x.f32")], capture_output=True, text=True, timeout=120)
-    assert r.returncode != 0 and "outside the JS baseline" in r.stderr
+    for name in ("spectral_cornell", "anim_restir_demo"):  # spectral; RENDER_MODE 1
+        r = subprocess.run([NODE, BENCH, CONFIGS, name, "16", "16", "1", "image", "1", "1",
+                            str(tmp_path / "x.f32")], capture_output=True, text=True, timeout=120)
+        assert r.returncode != 0 and "outside the JS baseline" in r.stderr, name
+
+
+def js_restir_chain(name, w, h, n, tmp_path, constants=None, threads=4):
+    out = tmp_path / ("%s_restir.f32" % name)
+    cmd = [NODE, BENCH, CONFIGS, name, str(w), str(h), str(threads), "restir-image", str(n), str(out)]
+    if constants:
+        cmd += ["--constants", json.dumps(constants)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return np.fromfile(str(out), np.float32).reshape(n, 3, h, w, 4)
+
+
+def res_match(a, b):
+    return ((np.abs(a - b) <= 1e-3 * np.maximum(1.0, np.abs(b))).all(-1)).mean()
+
+
+@pytest.mark.parametrize("name,constants", [("c3_outdoor_restir", None), ("restir_mis_demo", None),
+                                            ("c3_outdoor_restir", {"use_mis": True})])
+def test_js_restir_chain_matches_c_oracle(name, constants, cfgs, tmp_path):
+    """ReSTIR in the JS baseline (sampleLightsReSTIR, raytracer.glsl:1619-1801,
+    and index.js's swap chain, 795-820), GLSL semantics: six chained passes
+    against the C restatement's chain -- samples and both reservoir MRTs per
+    pass -- and pass 1 (no history yet) against the reference's own fixture.
+    With use_mis and <= 8 lights the call routes to the importance-culled MIS
+    loop instead (1900-1946): the third case."""
+    cfg = dict([c for c in cfgs["configs"] if c["name"] == name][0])
+    if constants:
+        cfg["constants"] = dict(cfg.get("constants", {}), **constants)
+    n = 6
+    J = js_restir_chain(name, 64, 64, n, tmp_path, constants)
+    S, M, A = O.Oracle(cfg, cfgs, width=64, height=64).frames_restir(n, cfg)
+    for k in range(n):
+        assert match(J[k, 0], S[k]) >= 0.995, (name, k + 1, "sample")
+        assert res_match(J[k, 1], M[k]) >= 0.995 and res_match(J[k, 2], A[k]) >= 0.995, (name, k + 1, "reservoirs")
+    assert abs(J[:, 0, ..., :3].mean() - S[..., :3].mean()) <= 1e-3 * S[..., :3].mean()
+    if not constants:
+        gold = np.load(os.path.join(REPO, "tests", "golden", name + ".npz"))["samples"]
+        assert match(J[0, 0], gold[0]) >= 0.99
+
+
+def test_js_restir_bench_mode_reports_throughput():
+    r = subprocess.run([NODE, BENCH, CONFIGS, "c3_outdoor_restir", "192", "108", "2", "restir-bench", "40", "48", "0.5"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["samples"] > 0 and d["msamples_s"] > 0 and d["threads"] == 2 and d["passes"] >= 1
