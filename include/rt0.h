@@ -296,6 +296,15 @@ int rt0_set_jit(rt0_ctx *ctx, int enable);
  * pass after pass); 0 (default) = GLSL semantics.  Radiance of a pass is the
  * same either way; only the reservoirs the next passes read differ. */
 int rt0_set_executor_compat(rt0_ctx *ctx, int enable);
+/* Deferred ReSTIR light sampling (scene-specialised kernels): a pass runs its
+ * paths with every sampleLightsReSTIR call (raytracer.glsl:1619-1801)
+ * appended to a per-wave list, evaluates the list in a second kernel with
+ * every lane busy, and completes the samples in a third.  Same arguments,
+ * same arithmetic as the inline calls (results equal up to FMA placement).
+ * 1 (default; RT0_DEFER_NEE=0 in the environment at rt0_create turns it
+ * off) or 0 = inline calls.  Executor compatibility always runs them inline.
+ * Replaces nothing in the reference: the GL pipeline has no such choice. */
+int rt0_set_defer_light_sampling(rt0_ctx *ctx, int enable);
 /* Compile the scene-specialised kernel for (scene, config) without a device
  * (hipRTC only): checks the generated code builds; *code_size receives the
  * code-object size.  err (may be NULL) receives the compiler log. */

@@ -15,6 +15,10 @@
 #include <string>
 #include <vector>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include "../../include/rt0.h"
 #include "rt0_device.h"
 #include "rt0_internal.h"
@@ -160,6 +164,37 @@ static int clear_buffers(rt0_ctx *c) {
   return RT0_OK;
 }
 
+// Diagnostics: RT0_SEGV_TRACE=1 prints the native stack of a segmentation
+// fault to stderr (then the previous handler -- e.g. Python's faulthandler --
+// runs).  Installed at the first rt0_create.
+static struct sigaction g_prev_segv;
+static void segv_trace(int sig, siginfo_t *si, void *) {
+  void *frames[64];
+  const int n = backtrace(frames, 64);
+  char msg[96];
+  const int len = snprintf(msg, sizeof msg, "rt0: signal %d at address %p; native stack:\n", sig, si ? si->si_addr : nullptr);
+  if (len > 0) (void)!write(2, msg, (size_t)len);
+  backtrace_symbols_fd(frames, n, 2);
+  sigaction(SIGSEGV, &g_prev_segv, nullptr);  // the fault repeats into the previous handler
+}
+static void install_segv_trace() {
+  static bool done = false;
+  if (done || !getenv("RT0_SEGV_TRACE")) return;
+  done = true;
+  // an alternate stack, so that a stack overflow can be reported too
+  static char altstack[1 << 16];
+  stack_t ss;
+  memset(&ss, 0, sizeof ss);
+  ss.ss_sp = altstack;
+  ss.ss_size = sizeof altstack;
+  sigaltstack(&ss, nullptr);
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
+}
+
 extern "C" {
 
 const char *rt0_version(void) { return "rt0-mi355x 0.1 (gfx950)"; }
@@ -170,6 +205,7 @@ int rt0_create(int width, int height, int device, rt0_ctx **out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT0_E_HIP;
   if (device < 0 || device >= ndev) return RT0_E_ARG;
+  install_segv_trace();
   rt0_ctx *c = new rt0_ctx();
   c->device = device;
   if (const char *e = getenv("RT0_JIT")) c->use_jit = atoi(e) != 0;
@@ -955,6 +991,12 @@ int rt0_device_accum(rt0_ctx *c, void **dptr, void **stream) {
 int rt0_set_jit(rt0_ctx *c, int enable) {
   if (!c) return RT0_E_ARG;
   c->use_jit = enable != 0;
+  return RT0_OK;
+}
+
+int rt0_set_defer_light_sampling(rt0_ctx *c, int enable) {
+  if (!c) return RT0_E_ARG;
+  c->defer_nee = enable != 0;  // the next render picks the matching JIT module
   return RT0_OK;
 }
 

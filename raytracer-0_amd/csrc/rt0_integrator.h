@@ -1155,7 +1155,18 @@ struct Integrator {
   // calcDirectLighting, raytracer.glsl:1174-1230
   // ms/susp: resumable shadow-ray march (SUSP kernels); *susp = true when it
   // was suspended (the call is repeated with the same arguments later)
-  DEV v3 direct_light(int li, v3 x, v3 nl, float seed, March *ms = nullptr, bool *susp = nullptr) {
+  // What the MIS weight of a sphere light's sample reuses from the sampling
+  // (brdf(), 1956-1962): lightSamplingPdf's d², r² and cos θmax are the
+  // same expressions as calcDirectLighting's (1185-1187) when the light does
+  // not move (RENDER_MODE 0): max(0, 1 - r²/d²) and 1 - clamp(r²/d², 0, 1)
+  // agree wherever lightSamplingPdf reaches its sqrt (d² > r²)
+  struct LightGeo {
+    bool sphere;
+    float d2, r2, cam;
+    v3 ld;  // normalize(light - x)
+  };
+  DEV v3 direct_light(int li, v3 x, v3 nl, float seed, March *ms = nullptr, bool *susp = nullptr,
+                      LightGeo *geo = nullptr) {
     if (COUNT) ++n_nee;
     const GeomRec g = sc.geom(li);
     const MatRec lm = sc.mat(li);
@@ -1166,7 +1177,9 @@ struct Integrator {
         v3 sw = lpos(li, g) - x;  // 1185
         float d2 = dot(sw, sw);
         float cos_a_max = fsqrt(1.0f - fminf(fmaxf(fdiv(g.d0, d2), 0.0f), 1.0f));
-        v3 sr = sample_cone(normalize(sw), 1.0f - cos_a_max, seed + 23.1656f);
+        const v3 lw = normalize(sw);
+        if (geo) *geo = LightGeo{true, d2, g.d0, cos_a_max, lw};
+        v3 sr = sample_cone(lw, 1.0f - cos_a_max, seed + 23.1656f);
         if (fast_shadow()) {
           float t;
           if (COUNT) ++n_isect;
@@ -1702,10 +1715,20 @@ struct Integrator {
         const GeomRec lg = sc.geom(idx);
         const MatRec lmt = sc.mat(idx);
         if (lmt.type != M_LIGHT) return;
-        v3 ls = direct_light(idx, x, nl, nc_addmul(base, (float)i, 123.456f));
+        LightGeo geo{false, 0.f, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
+        v3 ls = direct_light(idx, x, nl, nc_addmul(base, (float)i, 123.456f), nullptr, nullptr, &geo);
         if (dot(ls, ls) > 0.000001f) {
-          v3 ld = normalize(lpos(idx, lg) - x);  // 1959 (lightSamplingPdf keeps light.pos)
-          acc = acc + ls * power_heuristic(light_pdf(lg, lmt, x), cos_pdf(ld, nl));
+#ifdef RT0_NO_MIS_REUSE  // A/B only: recompute lightSamplingPdf's geometry
+          geo.sphere = false;
+#endif
+          if (geo.sphere && !flag(F_ANIM)) {  // the sampling's own d², cos θmax and direction
+            float lp = 0.0f;
+            if (geo.d2 > geo.r2 && 1.0f - geo.cam >= 1e-6f) lp = frcp(TWO_PI * (1.0f - geo.cam));
+            acc = acc + ls * power_heuristic(lp, cos_pdf(geo.ld, nl));
+          } else {
+            v3 ld = normalize(lpos(idx, lg) - x);  // 1959 (lightSamplingPdf keeps light.pos)
+            acc = acc + ls * power_heuristic(light_pdf(lg, lmt, x), cos_pdf(ld, nl));
+          }
         }
       });
     } else {

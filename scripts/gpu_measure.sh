@@ -23,6 +23,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${OUT:-measure}
 mkdir -p "$O"
 export TMPDIR=/tmp
+export RT0_SEGV_TRACE=1  # librt0 prints the native stack of a segmentation fault (rt0_host.cpp)
 STEPS=${STEPS:-5}
 WARMUP=${WARMUP:-2}
 

@@ -49,7 +49,7 @@ if os.path.exists(os.path.join(D, "valu_peak.json")):
     for line in open(os.path.join(D, "valu_peak.json")):
         if line.startswith("{"):
             d = json.loads(line)
-            vp[d["kernel"]] = d["tflops"]
+            vp[d["kernel"]] = d.get("tflops")
             rate[d["kernel"]] = d.get("wave_instr_per_simd_per_ns")
 PEAK_SCALAR = vp.get("v_fma_f32", 78.6)
 NS_NORM = 3.0 / (rate["v_add_f32"] + rate["v_mul_f32"] + rate["v_fma_f32"]) if rate.get("v_add_f32") else None

@@ -111,6 +111,13 @@ VKERNEL(k_fma_cnd, DECL_F; float y[16]; unsigned long long m = __ballot(threadId
         INIT_F; _Pragma("unroll") for (int k = 0; k < 16; k++) y[k] = x[k], B_FMA_CND,
         FOLD_F; _Pragma("unroll") for (int k = 0; k < 16; k++) s += y[k])
 
+// exactness of the hardware reciprocal square root at powers of four (the
+// integrator normalises unit axis vectors: is v_rsq_f32(1) exactly 1?)
+__global__ void k_rsq_exact(const float *in, float *out) {
+  const int i = threadIdx.x;
+  out[i] = __builtin_amdgcn_rsqf(in[i]);
+}
+
 struct K {
   const char *name;
   void (*fn)(float *, float, float);
@@ -155,6 +162,19 @@ int main() {
     printf("{\"kernel\": \"%s\", \"tflops\": %.2f, \"wave_instr_per_simd_per_ns\": %.4f, "
            "\"relative_to_fma\": %.3f, \"ms_per_launch\": %.4f}\n",
            k.name, tflops, per_simd_per_ns, per_simd_per_ns * fma_ns_per_instr, ms);
+  }
+  {
+    const float h_in[4] = {1.0f, 4.0f, 0.25f, 16.0f};
+    float *d_in, *d_out, h_out[4];
+    (void)hipMalloc(&d_in, sizeof h_in);
+    (void)hipMalloc(&d_out, sizeof h_out);
+    (void)hipMemcpy(d_in, h_in, sizeof h_in, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_rsq_exact, dim3(1), dim3(4), 0, 0, d_in, d_out);
+    (void)hipMemcpy(h_out, d_out, sizeof h_out, hipMemcpyDeviceToHost);
+    printf("{\"kernel\": \"v_rsq_f32 exactness\", \"in\": [1, 4, 0.25, 16], \"out\": [%.9g, %.9g, %.9g, %.9g], "
+           "\"exact\": %s}\n",
+           h_out[0], h_out[1], h_out[2], h_out[3],
+           (h_out[0] == 1.0f && h_out[1] == 0.5f && h_out[2] == 2.0f && h_out[3] == 0.25f) ? "true" : "false");
   }
   if (hipGetLastError() != hipSuccess) return 1;
   return 0;

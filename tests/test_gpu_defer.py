@@ -12,7 +12,7 @@ results in call order, instead of interleaved).  Measured on the GPU: 98.7-
 pixels per pass, by <= 1.5e-5 relative.  The test holds them to that: every
 reservoir within 1e-4 and every sample within 1e-5 relative (the parity
 tolerance is 1e-3), >= 98% of each bit-identical.
-RT0_DEFER_NEE is read when the context is created (rt0_create).
+rt0_set_defer_light_sampling switches between the two per context.
 """
 import os
 
@@ -26,15 +26,8 @@ import oracle as O
 
 
 def chain(cfgs, name, defer, n=6, size=64, viewport=None):
-    old = os.environ.get("RT0_DEFER_NEE")
-    os.environ["RT0_DEFER_NEE"] = defer
-    try:
-        r = rt0.Renderer(size, size)
-    finally:
-        if old is None:
-            del os.environ["RT0_DEFER_NEE"]
-        else:
-            os.environ["RT0_DEFER_NEE"] = old
+    r = rt0.Renderer(size, size)
+    r.set_defer_light_sampling(defer == "1")
     cfg = cfg_by_name(cfgs, name)
     configure(r, cfg, cfgs)
     r.set_temporal_frames(cfg.get("temporal_frames", 5))
