@@ -117,7 +117,9 @@ def test_chunked_viewport_scratch_is_tile_sized(cfgs, gpu_required):
     r.set_viewport(96, 64, 32, 32)
     r.render(1, 8)
     _, launches = r.last_kernel_ms()
-    assert launches == 2  # chunked pass + ordered sum
+    # the chunked pass and its ordered sum count as one launch of the pass
+    # (rt0_host.cpp render_impl); the scratch shows that the pass was chunked
+    assert launches == 1
     assert r.samples_bytes() == 8 * 32 * 32 * 16
     got = r.read_accum()
     assert np.array_equal(got[64:96, 96:128], ref[64:96, 96:128])
