@@ -24,8 +24,10 @@ runs under it; WORLD_SIZE must equal --gpus.  One process per GPU:
     at every band boundary after every pass (RCCL point-to-point,
     rt0/shard.py: RestirShard), the band gather at the end of the step.
 librt0 launches on its own stream; it is ordered against torch's stream (the
-accumulator zeroing, the exchanges, the gather) with events, so a step makes
-one host synchronisation, at its end.  Both gathers are inside the timed
+accumulator zeroing, the exchanges, the gather) with events, so steps run back
+to back with no host synchronisation between them (one device-wide
+synchronize ends the timed region; the last step's kernel time is read
+after it).  Both gathers are inside the timed
 region ("strong" scaling: total work fixed); rank 0's gather time is reported
 separately.  `--dist-backend gloo` stages every transfer through host memory:
 the one-GPU rehearsal of the N>1 path (all ranks on one device with
@@ -234,7 +236,13 @@ class Progressive:
             ev = self.order.begin_timing()
             self.image = self.gather.gather()  # RCCL gather of the HDR bands + one reorder on rank 0
             self.order.end_timing(ev)
-        self.r.sync()  # the step's one host synchronisation (kernel time of this render call)
+        # no host synchronisation: the next step's zero_() and render are
+        # stream-ordered after this one, so steps run back to back
+
+    def collect(self):
+        """After a device-wide synchronize: the last step's kernel time (librt0's
+        timing events of its render call) and gather time."""
+        self.r.sync()
         ms, n = self.r.last_kernel_ms()
         self.kernel_ms.append(ms)
         self.launches = n
@@ -290,15 +298,21 @@ class Restir:
     def step(self, i):
         first = 1 + i * self.spp
         if self.sh is None:
-            self.r.render(first, self.spp)  # one call, spp launches, synchronous
-            ms, n = self.r.last_kernel_ms()
+            self.r.render_async(first, self.spp)  # one call, spp launches on librt0's stream
         else:
             self.sh.render(first, self.spp)  # async passes, halo exchanges event-ordered
             ev = self.order.begin_timing()
             self.torch.index_select(self.acc, 0, self.rows, out=self.send)
             self.image = self.gather.gather(self.send_buf)
             self.order.end_timing(ev)
-            self.r.sync()
+        # no host synchronisation: the next step's passes follow on the same stream
+
+    def collect(self):
+        """After a device-wide synchronize: the last step's kernel time."""
+        self.r.sync()
+        if self.sh is None:
+            ms, n = self.r.last_kernel_ms()  # the render call's spp launches
+        else:
             # the last pass's kernel time (the timing events of earlier async
             # passes are overwritten): ReSTIR pass times are flat over frames
             m, _ = self.r.last_kernel_ms()
@@ -447,10 +461,11 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         job.step(args.warmup + i)
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # device-wide: librt0's stream included
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    job.collect()  # the last timed step's kernel time, read outside the timed region
     if dist:
         t = torch.tensor([dt], device="cuda:%d" % local) if not staged else torch.tensor([dt])
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
