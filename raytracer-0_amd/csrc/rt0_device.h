@@ -98,6 +98,21 @@ struct NeeRec {
   int32_t pad;
 };
 
+// RT0_NEE_WALK (scenes with triangle models): a light-sampling call's
+// triangle occlusion queries go to rt0_jit_walk as WalkJobs, 32 B: the ray
+// and its bound, and `slot2` = 2 * the call's record slot + which ray (0 =
+// visibility, 1 = shadow ray); the answer (1 = occluded) goes to
+// walk_res[slot2].  The call's result plane entry then holds its result as it
+// is if both rays pass, and w = a tag ((slot + 1) << 2 | 1 if the visibility
+// ray was walked | 2 if the shadow ray was) as int bits, which
+// rt0_jit_resolve reads (a finished call's w is 0.0f).
+struct WalkJob {
+  float ox, oy, oz, tmax;
+  float dx, dy, dz;
+  uint32_t slot2;
+};
+static_assert(sizeof(WalkJob) == 32, "WalkJob is 32 B");
+
 struct SceneDev {
   int32_t n_meshes, n_sdfs, n_lights, n_total;
   int32_t n_models;  // TRIANGLE entries: geom/mat[n_meshes + n_sdfs + k]
@@ -195,5 +210,11 @@ struct LaunchParams {
   uint32_t *nee_count;
   float4 *nee_out, *nee_partial;
   int32_t *nee_n;
+  // RT0_NEE_WALK: walk_jobs[w * walk_cap ...] = light-sampling wave w's
+  // jobs (walk_count[w] of them, walk_cap = 2 * RT0_NEE_REGIONS * nee_cap),
+  // walk_res[2 * record slot + ray]; walk_waves = light-sampling waves
+  WalkJob *walk_jobs;
+  uint32_t *walk_count, *walk_res;
+  int32_t walk_waves;
   float4 apos[RT0_MAX_MESH];
 };

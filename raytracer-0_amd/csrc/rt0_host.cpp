@@ -43,6 +43,11 @@ static long nee_regions_per_wave() {
   static const long k = getenv("RT0_NEE_REGIONS") ? std::max(1L, atol(getenv("RT0_NEE_REGIONS"))) : 2L;
   return k;
 }
+// light-sampling calls' triangle occlusion queries in rt0_jit_walk (JitKey::walk); RT0_NEE_WALK=0 keeps them inline
+static bool nee_walk_enabled() {
+  static const bool k = !(getenv("RT0_NEE_WALK") && atoi(getenv("RT0_NEE_WALK")) == 0);
+  return k;
+}
 
 enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
 
@@ -115,6 +120,9 @@ struct rt0_ctx {
   NeeRec *d_nee_rec = nullptr;
   uint32_t *d_nee_count = nullptr;  // records per pass wave
   float4 *d_nee_out = nullptr, *d_nee_partial = nullptr;
+  WalkJob *d_walk_jobs = nullptr;  // RT0_NEE_WALK buffers (LaunchParams::walk_*)
+  uint32_t *d_walk_count = nullptr, *d_walk_res = nullptr;
+  size_t walk_jobs_n = 0, walk_res_n = 0, walk_waves_n = 0;
   int32_t *d_nee_n = nullptr;
   size_t nee_slots = 0;  // records d_nee_rec holds (pass waves x 64 x calls per lane)
   size_t nee_waves = 0;  // entries of d_nee_count
@@ -238,6 +246,8 @@ void rt0_destroy(rt0_ctx *c) {
   if (c->d_counters) (void)hipFree(c->d_counters);
   if (c->d_halo_miss) (void)hipFree(c->d_halo_miss);
   if (c->d_samples) (void)hipFree(c->d_samples);
+  for (void *q : {(void *)c->d_walk_jobs, (void *)c->d_walk_count, (void *)c->d_walk_res})
+    if (q) (void)hipFree(q);
   for (void *q : {(void *)c->d_nee_rec, (void *)c->d_nee_count, (void *)c->d_nee_out, (void *)c->d_nee_partial,
                   (void *)c->d_nee_n})
     if (q) (void)hipFree(q);
@@ -719,6 +729,14 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
       key.defer = defer ? 1 : 0;
       key.nee_regions = (int)nee_regions_per_wave();
+      // (Integrator::restir_split: quadric-only shadow rays -- no SDFs, no
+      // textured lights -- and RENDER_MODE 0)
+      // (the result tag holds record slot + 1 in 29 bits)
+      key.walk = defer && nee_walk_enabled() && c->host_scene.n_models > 0 && c->n_tris > 0 &&
+                         c->host_scene.n_sdfs == 0 && !c->host_scene.any_tex && !(key.flags & F_ANIM) &&
+                         (size_t)grid.x * grid.y * 4 * 64 * (size_t)p.max_bounces < (1u << 29) - 1u
+                     ? 1
+                     : 0;
       int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
       c->jit_dirty = false;
@@ -754,6 +772,30 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     p.nee_out = c->d_nee_out;
     p.nee_partial = c->d_nee_partial;
     p.nee_n = c->d_nee_n;
+    if (c->jit.walk) {
+      if (slots >= (1u << 29) - 1u)  // the module was compiled for a smaller grid (the tag's slot field)
+        return fail(c, RT0_E_UNSUPPORTED, "too many light-sampling records for the walk tags");
+      // per light-sampling wave: up to two rays per record of its regions
+      const size_t waves = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave();
+      const size_t jobs = waves * 2 * (size_t)nee_regions_per_wave() * (size_t)p.nee_cap;
+      if (jobs > c->walk_jobs_n || 2 * slots > c->walk_res_n || waves > c->walk_waves_n) {
+        for (void **q : {(void **)&c->d_walk_jobs, (void **)&c->d_walk_count, (void **)&c->d_walk_res}) {
+          if (*q) HIPCHK(c, hipFree(*q));
+          *q = nullptr;
+        }
+        c->walk_jobs_n = c->walk_res_n = c->walk_waves_n = 0;
+        HIPCHK(c, hipMalloc(&c->d_walk_jobs, jobs * sizeof(WalkJob)));
+        HIPCHK(c, hipMalloc(&c->d_walk_count, waves * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&c->d_walk_res, 2 * slots * sizeof(uint32_t)));
+        c->walk_jobs_n = jobs;
+        c->walk_res_n = 2 * slots;
+        c->walk_waves_n = waves;
+      }
+      p.walk_jobs = c->d_walk_jobs;
+      p.walk_count = c->d_walk_count;
+      p.walk_res = c->d_walk_res;
+      p.walk_waves = (int32_t)waves;
+    }
   }
   auto launch = [&](const LaunchParams &lp, unsigned gz, dim3 g) -> hipError_t {
     if (jit_fn) return rt0h::jit_launch(jit_fn, &lp, g.x, g.y, gz, c->stream) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
@@ -783,6 +825,10 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
         HIPCHK(c, rt0h::jit_launch(c->jit.nee, &p, (nee_waves + 3) / 4, 1, 1, c->stream) == RT0_OK
                       ? hipSuccess
                       : hipErrorLaunchFailure);
+        if (c->jit.walk)  // the calls' triangle occlusion queries (resolve completes the calls)
+          HIPCHK(c, rt0h::jit_launch(c->jit.walk, &p, (nee_waves + 3) / 4, 1, 1, c->stream) == RT0_OK
+                        ? hipSuccess
+                        : hipErrorLaunchFailure);
         HIPCHK(c, rt0h::jit_launch(c->jit.resolve, &p, grid.x, grid.y, 1, c->stream) == RT0_OK
                       ? hipSuccess
                       : hipErrorLaunchFailure);

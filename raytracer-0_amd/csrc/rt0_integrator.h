@@ -102,6 +102,9 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_TAP_BATCH
 #define RT0_TAP_BATCH 1
 #endif
+#ifndef RT0_NEE_WALK  // light-sampling calls' triangle occlusion queries in rt0_jit_walk (models scenes)
+#define RT0_NEE_WALK 0
+#endif
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
   return x - floorf(x);
@@ -549,6 +552,23 @@ struct Geometry {
   static DEV int shadow_light(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, float &tl,
                               unsigned long long *nbvh = nullptr) {
     const v3 m = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+    int il = shadow_light_q<Cfg>(P, sc, C, o, d, m, tl);
+    if constexpr (Scene::kMayHaveModels) {
+      // triangles come after the quadrics (strict <): one before tL is the
+      // closest hit, and no model is a light -- an occlusion query suffices
+#ifndef RT0_EXP_NO_BVH_OCC  // profiling experiment only (breaks parity): no triangle occlusion queries
+      if (il >= 0 && sc.n_models() > 0 && P.n_tris > 0) {
+        float tt = tl;
+        if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) il = -1;
+      }
+#endif
+    }
+    return il;
+  }
+  // shadow_light's quadric part (m = 1/d): the light mesh the ray reaches
+  // through the quadrics, or -1; tl = its t
+  template <class Cfg>
+  static DEV int shadow_light_q(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, v3 m, float &tl) {
     const v3 mo = m * o;
     float tL = INF_T;
     int iL = -1;
@@ -568,16 +588,7 @@ struct Geometry {
       occ |= prim<Cfg>(P, sc, C, i, o, d, m, mo, i < iL ? tL_up : tL, t) >= 0;
     });
     tl = tL;
-    int il = occ ? -1 : (iL >= 0 ? iL : (sc.mat(0).type == M_LIGHT ? 0 : -1));
-    if constexpr (Scene::kMayHaveModels) {
-      // triangles come after the quadrics (strict <): one before tL is the
-      // closest hit, and no model is a light -- an occlusion query suffices
-      if (il >= 0 && sc.n_models() > 0 && P.n_tris > 0) {
-        float tt = tL;
-        if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) il = -1;
-      }
-    }
-    return il;
+    return occ ? -1 : (iL >= 0 ? iL : (sc.mat(0).type == M_LIGHT ? 0 : -1));
   }
   // isVisible() (raytracer.glsl:1539-1557) in the same spirit: the closest
   // quadric (t_q, i_q), then one occlusion query of the triangles up to
@@ -587,6 +598,22 @@ struct Geometry {
   static DEV bool visible_fast(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, float lim,
                                unsigned long long *nbvh = nullptr) {
     const v3 m = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+    float tt;
+    const bool vq = visible_q<Cfg>(P, sc, C, o, d, m, lim, tt);
+    if constexpr (Scene::kMayHaveModels) {
+#ifndef RT0_EXP_NO_BVH_OCC
+      if (sc.n_models() > 0 && P.n_tris > 0) {
+        if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) return false;
+      }
+#endif
+    }
+    return vq;
+  }
+  // visible_fast's quadric part: what the quadrics decide, and tt = the
+  // bound of the triangle occlusion query, min(t_q, lim)
+  template <class Cfg>
+  static DEV bool visible_q(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, v3 m, float lim,
+                            float &tt) {
     const v3 mo = m * o;
     float tq = INF_T;
     int iq = 0;
@@ -596,12 +623,7 @@ struct Geometry {
       tq = ok ? t : tq;
       iq = ok ? i : iq;
     });
-    if constexpr (Scene::kMayHaveModels) {
-      if (sc.n_models() > 0 && P.n_tris > 0) {
-        float tt = fminf(tq, lim);
-        if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) return false;
-      }
-    }
+    tt = fminf(tq, lim);
     if (tq < lim) return sc.mat(iq).type == M_LIGHT;
     return true;
   }
@@ -1165,6 +1187,17 @@ struct Integrator {
     float d2, r2, cam;
     v3 ld;  // normalize(light - x)
   };
+  // calcDirectLighting's contribution of a sphere light's sample whose shadow
+  // ray reached light mesh il at t (1198-1205; il < 0: blocked)
+  DEV v3 sphere_light_lit(int il, float t, float cos_a_max, v3 sr, v3 nl) {
+    if (il < 0) return mk(0.f, 0.f, 0.f);
+    const MatRec mh = light_mat(il);
+    float weight = 2.0f * (1.0f - cos_a_max);
+    float T_fog = 1.0f;
+    if (VOL && flag(F_VOL)) T_fog = fexp(-VOL_SIGMA_T * t);
+    v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
+    return (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
+  }
   DEV v3 direct_light(int li, v3 x, v3 nl, float seed, March *ms = nullptr, bool *susp = nullptr,
                       LightGeo *geo = nullptr) {
     if (COUNT) ++n_nee;
@@ -1184,15 +1217,7 @@ struct Integrator {
           float t;
           if (COUNT) ++n_isect;
           const int il = G::template shadow_light<Cfg>(P, sc, C, x + nl * EPSILON, sr, t, COUNT ? n_bvh : nullptr);
-          if (il >= 0) {
-            const MatRec mh = light_mat(il);
-            float weight = 2.0f * (1.0f - cos_a_max);
-            float T_fog = 1.0f;
-            if (VOL && flag(F_VOL)) T_fog = fexp(-VOL_SIGMA_T * t);
-            v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
-            dl = (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
-          }
-          return dl;
+          return sphere_light_lit(il, t, cos_a_max, sr, nl);
         }
 #ifdef RT0_EXP_NO_SHADOW  // profiling experiment only (breaks parity): shadow ray skipped
         float t = 1.0f;
@@ -1412,6 +1437,13 @@ struct Integrator {
     const int nl = sc.n_lights();
     if (nl == 0 || sc.light(0) < 0) return mk(0.f, 0.f, 0.f);
     if (COUNT && !GHOST) ++n_restir;
+    return restir_finalize<GHOST>(restir_reservoir<GHOST>(hp, hn, mat, sx, sy), hp, hn, mat, sx);
+  }
+  // sampleLightsReSTIR up to finalizeReservoir (1625-1760): the initial RIS
+  // reservoir, the two temporal levels and the spatial taps combined
+  template <bool GHOST = false>
+  DEV Res restir_reservoir(v3 hp, v3 hn, const MatRec &mat, float sx, float sy) {
+    const int nl = sc.n_lights();
     const float scx = fcx / P.res_x, scy = fcy / P.res_y;
     Res init = empty_res();
     int eff = GHOST ? 0 : min(C.restir_samples(), max(4, nl));
@@ -1585,7 +1617,136 @@ struct Integrator {
       }
     }
 #endif
-    // finalizeReservoir, 1525-1576
+    return fr;
+  }
+  // finalizeReservoir's W of a visible reservoir with target tp > 0 (1541-1568)
+  DEV float restir_weight(const Res &fr, float tp) {
+    float cM = fminf(fmaxf(fr.M, 1.0f), 40.0f);
+    float raw = fr.ws / (tp * cM);
+    float bc = 1.0f;
+    if (fr.age > 0.0f) {
+      float na = fminf(fmaxf(fr.age / 30.0f, 0.0f), 1.0f);
+      bc *= mixf(0.85f, 1.0f, 1.0f - na * 0.3f);
+    }
+    if (cM > 16.0f) bc *= fsqrt(16.0f / cM);
+    float W = fminf(fmaxf(bc * raw, 0.0f), 12.0f);
+    return finite_(W) ? W : 0.0f;
+  }
+  // the light's shading weight of a reservoir (1778-1780)
+  DEV static float restir_ew(const Res &fr) {
+    float ew = fminf(fmaxf(fr.W, 0.0f), 8.0f);
+    if (fr.M > 30.0f) ew *= fsqrt(30.0f / fr.M);
+    return ew;
+  }
+
+  // RT0_NEE_WALK (light-sampling kernels of scenes with triangle models):
+  // sampleLightsReSTIR with its two triangle occlusion queries -- the
+  // visibility ray of finalizeReservoir (isVisible, 1539-1557) and the shadow
+  // ray of the picked light (calcDirectLighting, 1185-1205) -- handed to
+  // rt0_jit_walk, which walks them on dense lanes; rt0_jit_resolve completes the
+  // call from their answers.  Everything else runs here, as in restir(): the
+  // reservoir, the quadric part of both rays (a quadric that decides alone
+  // leaves no walk), W, and the light's contribution as it is if the shadow
+  // ray passes.  The shadow ray is cast before visibility is known (it is a
+  // function of the hit point, the light and the seed only); its answer is
+  // used only where restir() would cast it (visible, W > 0).
+  struct Split {
+    bool done;     // finished here: c and fin are final
+    v3 c;          // done: the call's result
+    WalkJob j[2];  // [0] visibility, [1] shadow ray
+    bool has[2];
+    float W;  // W if visible
+    v3 f;     // the result if visible and the shadow ray passes
+  };
+  DEV Split restir_split(v3 hp, v3 hn, const MatRec &mat, float sx, float sy) {
+    Split o;
+    o.done = true;
+    o.c = mk(0.f, 0.f, 0.f);
+    o.has[0] = o.has[1] = false;
+    if (!flag(F_RESTIR)) return o;
+    const int nl = sc.n_lights();
+    if (nl == 0 || sc.light(0) < 0) return o;
+    Res fr = restir_reservoir<false>(hp, hn, mat, sx, sy);
+    // the host selects RT0_NEE_WALK only for such scenes (and a BVH with
+    // triangles), so in a walk module this folds away
+    if (!fast_shadow() || flag(F_ANIM) || sc.n_models() <= 0) {
+      o.c = restir_finalize<false>(fr, hp, hn, mat, sx);
+      return o;
+    }
+    const float tp = (fr.ws > 0.0f && fr.M > 0.0f) ? target_fn(fr.pos, fr.col, hp, hn, mat) : 0.0f;
+    if (!(tp > 0.0f)) {  // W = 0 without a ray
+      fr.W = 0.0f;
+      fr.age = fminf(fr.age, 30.0f);
+      fin = fr;
+      return o;
+    }
+    // visible(hp, fr.pos)
+    v3 sd = fr.pos - hp;
+    const float dist = length(sd);
+    if (!(dist < EPSILON * 10.0f)) {
+      sd = normalize(sd);
+      const v3 o1 = hp + (sd * EPSILON) * 2.0f;
+      const v3 m1 = mk(frcp(sd.x), frcp(sd.y), frcp(sd.z));
+      float t1;
+      if (!G::template visible_q<Cfg>(P, sc, C, o1, sd, m1, dist - EPSILON * 2.0f, t1)) {
+        fr.W = 0.0f;  // a quadric hides the light
+        fr.age = fminf(fr.age, 30.0f);
+        fin = fr;
+        return o;
+      }
+      o.has[0] = true;
+      o.j[0] = WalkJob{o1.x, o1.y, o1.z, t1, sd.x, sd.y, sd.z, 0u};
+    }
+    fr.W = restir_weight(fr, tp);
+    v3 f = mk(0.f, 0.f, 0.f);
+    if (fr.W > 0.0f && fr.idx >= 0 && fr.idx < nl) {
+      const int act = sc.light(fr.idx);
+      if (act >= 0 && act < sc.n_meshes() + sc.n_sdfs()) {
+        // direct_light(act, hp, hn, sx + 456.789f), 1174-1230, up to its triangle query
+        const GeomRec g = sc.geom(act);
+        const MatRec lm = sc.mat(act);
+        const float ew = restir_ew(fr);
+        const v3 o2 = hp + hn * EPSILON;
+        if (lm.type == M_LIGHT && g.type == T_SPHERE) {  // 1185-1205
+          const v3 sw = mk(g.px, g.py, g.pz) - hp;
+          const float d2 = dot(sw, sw);
+          const float cos_a_max = fsqrt(1.0f - fminf(fmaxf(fdiv(g.d0, d2), 0.0f), 1.0f));
+          const v3 sr = sample_cone(normalize(sw), 1.0f - cos_a_max, (sx + 456.789f) + 23.1656f);
+          float t2;
+          const int il = G::template shadow_light_q<Cfg>(P, sc, C, o2, sr, mk(frcp(sr.x), frcp(sr.y), frcp(sr.z)), t2);
+          f = sphere_light_lit(il, t2, cos_a_max, sr, hn) * ew;
+          if (il >= 0) o.j[1] = WalkJob{o2.x, o2.y, o2.z, t2, sr.x, sr.y, sr.z, 1u};
+        } else if (lm.type == M_DIR_LIGHT) {  // 1224-1229: lit iff intersection() misses everything
+          const v3 ld = mk(g.px, g.py, g.pz);
+          float tq;
+          (void)G::template visible_q<Cfg>(P, sc, C, o2, ld, mk(frcp(ld.x), frcp(ld.y), frcp(ld.z)), INF_T, tq);
+          if (tq == INF_T) {
+            f = ((mk(lm.cr, lm.cg, lm.cb) * mk(lm.er, lm.eg, lm.eb)) * fmaxf(0.001f, dot(ld, hn))) * ew;
+            o.j[1] = WalkJob{o2.x, o2.y, o2.z, INF_T, ld.x, ld.y, ld.z, 1u};
+          }
+        }  // other light meshes contribute nothing (direct_light's own cases)
+        if (!finite_(f.x) || !finite_(f.y) || !finite_(f.z)) f = mk(0.f, 0.f, 0.f);
+        // a shadow ray matters only for a non-zero contribution
+        o.has[1] = f.x != 0.0f || f.y != 0.0f || f.z != 0.0f;
+        if (!o.has[1]) f = mk(0.f, 0.f, 0.f);
+      }
+    }
+    fr.age = fminf(fr.age, 30.0f);
+    fin = fr;  // W as if visible; rt0_jit_resolve zeroes it when the visibility ray is blocked
+    if (!o.has[0] && !o.has[1]) {  // nothing left to walk
+      o.c = f;
+      return o;
+    }
+    o.done = false;
+    o.W = fr.W;
+    o.f = f;
+    return o;
+  }
+
+  // finalizeReservoir (1525-1576) and the light's shading (1762-1800)
+  template <bool GHOST = false>
+  DEV v3 restir_finalize(Res fr, v3 hp, v3 hn, const MatRec &mat, float sx) {
+    const int nl = sc.n_lights();
     if (fr.ws <= 0.0f || fr.M <= 0.0f) {
       fr.W = 0.0f;
     } else {
@@ -1593,16 +1754,7 @@ struct Integrator {
       if (tp <= 0.0f || !(GHOST ? ghost_visible(hp, fr.pos) : visible(hp, fr.pos))) {
         fr.W = 0.0f;
       } else {
-        float cM = fminf(fmaxf(fr.M, 1.0f), 40.0f);
-        float raw = fr.ws / (tp * cM);
-        float bc = 1.0f;
-        if (fr.age > 0.0f) {
-          float na = fminf(fmaxf(fr.age / 30.0f, 0.0f), 1.0f);
-          bc *= mixf(0.85f, 1.0f, 1.0f - na * 0.3f);
-        }
-        if (cM > 16.0f) bc *= fsqrt(16.0f / cM);
-        fr.W = fminf(fmaxf(bc * raw, 0.0f), 12.0f);
-        if (!finite_(fr.W)) fr.W = 0.0f;
+        fr.W = restir_weight(fr, tp);
       }
     }
     fr.age = fminf(fr.age, 30.0f);
@@ -1615,9 +1767,7 @@ struct Integrator {
         // (1767-1776); g_final_reservoir was stored before that update
         if (flag(F_ANIM) && !visible(hp, lpos(act, sc.geom(act)))) return mk(0.f, 0.f, 0.f);
         v3 lc = direct_light(act, hp, hn, sx + 456.789f);
-        float ew = fminf(fmaxf(fr.W, 0.0f), 8.0f);
-        if (fr.M > 30.0f) ew *= fsqrt(30.0f / fr.M);
-        v3 fc = lc * ew;
+        v3 fc = lc * restir_ew(fr);
         if (!finite_(fc.x) || !finite_(fc.y) || !finite_(fc.z)) return mk(0.f, 0.f, 0.f);
         return fc;
       }
@@ -2404,7 +2554,9 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     total += cnt[q];
   }
   const size_t plane = (size_t)P.width * P.height;
-  for (uint32_t i = threadIdx.x & 63u; i < total; i += 64u) {
+  using It = Integrator<Scene, Cfg, true, VOL, SDF, SPECTRAL, false>;
+  // list position i -> the record's slot in its pass wave's region
+  auto slot_of = [&](uint32_t i) -> size_t {
     uint32_t q = 0, off = i;
 #pragma unroll
     for (int k = 0; k < RT0_NEE_REGIONS - 1; ++k)
@@ -2412,23 +2564,173 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
         off -= cnt[k];
         q = k + 1;
       }
-    const NeeRec r = P.nee_rec[(size_t)(r0 + q) * (uint32_t)P.nee_cap + off];
-    Integrator<Scene, Cfg, true, VOL, SDF, SPECTRAL, false> it(P, sc, cfg);
+    return (size_t)(r0 + q) * (uint32_t)P.nee_cap + off;
+  };
+  auto setup = [&](It &it, const NeeRec &r) {
     it.frame = P.frame0;
     const int py = r.pix / P.width, px = r.pix - py * P.width;
     it.fcx = (float)px + 0.5f;
     it.fcy = (float)py + 0.5f;
     it.fin = empty_res();
     it.gr_have = false;
-    const v3 c = it.restir(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), sc.mat(r.mat), r.sx, r.sy);
+  };
+  // the call's result x mask; the pixel's last call writes g_final_reservoir
+  auto store = [&](const NeeRec &r, v3 c, const Res &q) {
     P.nee_out[(size_t)r.k * plane + r.pix] = make_float4(c.x * r.mr, c.y * r.mg, c.z * r.mb, 0.f);
     if (r.k == P.nee_n[r.pix] - 1 && P.rout_main != nullptr && P.rout_aux != nullptr) {
-      const Res &q = it.fin;
       P.rout_main[r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
       P.rout_aux[r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
     }
+  };
+#if RT0_NEE_WALK
+  // the calls' triangle occlusion queries become this wave's walk jobs,
+  // appended densely in record order (wave-wide ballots, no atomics)
+  WalkJob *wj = P.walk_jobs + (size_t)(r0 / RT0_NEE_REGIONS) * (2u * RT0_NEE_REGIONS * (uint32_t)P.nee_cap);
+  uint32_t njob = 0;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint32_t base = 0; base < total; base += 64u) {  // wave-uniform trip count
+    const uint32_t i = base + lane;
+    bool has0 = false, has1 = false;
+    WalkJob j0, j1;
+    if (i < total) {
+      const size_t slot = slot_of(i);
+      const NeeRec r = P.nee_rec[slot];
+      It it(P, sc, cfg);
+      setup(it, r);
+      const auto sp = it.restir_split(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), sc.mat(r.mat), r.sx, r.sy);
+      if (sp.done) {
+        store(r, sp.c, it.fin);
+      } else {
+        // the result as it is if both rays pass, tagged for rt0_jit_resolve; the
+        // pixel's last call writes the reservoir MRTs with W as if visible
+        // (resolve zeroes W when the visibility ray is blocked)
+        const int tag = (int)(((uint32_t)slot + 1u) << 2) | (sp.has[0] ? 1 : 0) | (sp.has[1] ? 2 : 0);
+        P.nee_out[(size_t)r.k * plane + r.pix] =
+            make_float4(sp.f.x * r.mr, sp.f.y * r.mg, sp.f.z * r.mb, __int_as_float(tag));
+        if (r.k == P.nee_n[r.pix] - 1 && P.rout_main != nullptr && P.rout_aux != nullptr) {
+          const Res &q = it.fin;
+          P.rout_main[r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, sp.W);
+          P.rout_aux[r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+        }
+        has0 = sp.has[0];
+        has1 = sp.has[1];
+        j0 = sp.j[0];
+        j1 = sp.j[1];
+        j0.slot2 = 2u * (uint32_t)slot;
+        j1.slot2 = 2u * (uint32_t)slot + 1u;
+      }
+    }
+    const uint64_t b0 = __ballot(has0), b1 = __ballot(has1);
+    const uint32_t n0 = (uint32_t)__popcll(b0);
+    if (has0) wj[njob + (uint32_t)__popcll(b0 & lt)] = j0;
+    if (has1) wj[njob + n0 + (uint32_t)__popcll(b1 & lt)] = j1;
+    njob += n0 + (uint32_t)__popcll(b1);
+  }
+  if (lane == 0) P.walk_count[r0 / RT0_NEE_REGIONS] = njob;
+#else
+  for (uint32_t i = threadIdx.x & 63u; i < total; i += 64u) {
+    const NeeRec r = P.nee_rec[slot_of(i)];
+    It it(P, sc, cfg);
+    setup(it, r);
+    const v3 c = it.restir(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), sc.mat(r.mat), r.sx, r.sy);
+    store(r, c, it.fin);
+  }
+#endif
+}
+
+#if RT0_NEE_WALK
+// rt0_jit_walk: the triangle occlusion queries of one light-sampling wave's
+// calls (WalkJobs, bvh_closest<true>'s walk), with lanes that stay busy: a
+// lane whose ray is answered takes the wave's next job (an LDS counter), so
+// the wave walks on full lanes until its list runs dry instead of waiting for
+// its longest ray every 64 jobs.  One node (two child boxes) per iteration.
+DEV void walk_body(const LaunchParams &P) {
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
+  if (w >= (uint32_t)P.walk_waves) return;
+  const uint32_t n = P.walk_count[w];
+  const WalkJob *__restrict__ jobs = P.walk_jobs + (size_t)w * (2u * RT0_NEE_REGIONS * (uint32_t)P.nee_cap);
+  uint32_t *ctr = nee_wave_counter();
+  *(volatile uint32_t *)ctr = 64u;  // every lane stores the same value: jobs 0..63 go by lane index
+  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
+  const TriDev *__restrict__ tris = P.tris;
+  int32_t *stk = bvh_stack_lds();
+  uint32_t j = threadIdx.x & 63u;
+  bool have = j < n;
+  v3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
+  float tmax = 0.f;
+  uint32_t slot2 = 0;
+  int node = 0, sp = 0, guard = 0;
+  if (have) {
+    const WalkJob jb = jobs[j];
+    o = mk(jb.ox, jb.oy, jb.oz);
+    d = mk(jb.dx, jb.dy, jb.dz);
+    inv = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+    tmax = jb.tmax;
+    slot2 = jb.slot2;
+  }
+  while (__ballot(have) != 0ull) {
+    if (have) {
+      bool done = false, occ = false;
+      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
+      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+      float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmax);
+      float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmax);
+      const int cl = lk.x, cr = lk.y;
+      int l0 = -1, l1 = -1;
+      if (tl != F_INF && cl < 0) {
+        l0 = ~cl;
+        tl = F_INF;
+      }
+      if (tr != F_INF && cr < 0) {
+        if (l0 < 0) l0 = ~cr;
+        else l1 = ~cr;
+        tr = F_INF;
+      }
+      if (l0 >= 0) {
+        float t;
+        occ = tri_test(tris[l0], o, d, tmax, t) || (l1 >= 0 && tri_test(tris[l1], o, d, tmax, t));
+      }
+      if (occ) {
+        done = true;
+      } else if (tl != F_INF && tr != F_INF) {
+        const bool lfirst = tl <= tr;
+        stk[256 * sp] = lfirst ? cr : cl;
+        sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
+        node = lfirst ? cl : cr;
+      } else if (tl != F_INF) {
+        node = cl;
+      } else if (tr != F_INF) {
+        node = cr;
+      } else if (sp == 0) {
+        done = true;
+      } else {
+        node = stk[256 * --sp];
+      }
+      // a ray visits each node at most once: the cap only guarantees that
+      // every wave drains even on a corrupt tree
+      if (++guard > 2 * P.n_tris + 8) done = true;
+      if (done) {
+        P.walk_res[slot2] = occ ? 1u : 0u;
+        j = atomicAdd(ctr, 1u);
+        have = j < n;
+        if (have) {
+          const WalkJob jb = jobs[j];
+          o = mk(jb.ox, jb.oy, jb.oz);
+          d = mk(jb.dx, jb.dy, jb.dz);
+          inv = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+          tmax = jb.tmax;
+          slot2 = jb.slot2;
+          node = 0;
+          sp = 0;
+          guard = 0;
+        }
+      }
+    }
   }
 }
+
+#endif
 
 // Completes the samples of a deferred pass (rt0_jit_resolve): the path's own
 // radiance plus its light-sampling results in call order, main()'s spectral
@@ -2449,7 +2751,18 @@ DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
   const int n = P.nee_n[pix];
   v3 col = mk(part.x, part.y, part.z);
   for (int k = 0; k < n; ++k) {
-    const float4 o = P.nee_out[(size_t)k * plane + pix];
+    float4 o = P.nee_out[(size_t)k * plane + pix];
+#if RT0_NEE_WALK
+    if (const uint32_t tag = (uint32_t)__float_as_int(o.w)) {
+      // a call rt0_jit_nee left to the walks: its result counts if both rays
+      // passed; a blocked visibility ray makes the last call's W 0
+      // (finalizeReservoir, 1541-1545)
+      const size_t slot2 = 2u * (size_t)((tag >> 2) - 1u);
+      const bool vis = !(tag & 1u) || P.walk_res[slot2] == 0u;
+      if (!(vis && (!(tag & 2u) || P.walk_res[slot2 + 1] == 0u))) o = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!vis && k == n - 1 && P.rout_main != nullptr) P.rout_main[pix].w = 0.0f;
+    }
+#endif
     col = col + mk(o.x, o.y, o.z);
   }
   if constexpr (SPECTRAL) {

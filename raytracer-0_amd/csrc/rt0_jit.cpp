@@ -65,6 +65,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
   o << "#define RT0_HALO_CHECK " << k.halo_check << "\n";
   if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
+  if (k.defer && k.walk) o << "#define RT0_NEE_WALK 1\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
   // occupancy target below); with a BVH the extra registers cost more than
@@ -157,7 +158,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
     if (wn_env)
       o << "__attribute__((amdgpu_waves_per_eu(" << atoi(wn_env) << "))) ";
-    else if (s.n_models > 0)
+    else if (s.n_models > 0 && !k.walk)  // it walks the BVH itself
       o << "__attribute__((amdgpu_waves_per_eu(6))) ";
     else
       o << "__attribute__((amdgpu_waves_per_eu(4))) ";
@@ -167,6 +168,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_resolve(const LaunchParams P) {\n"
          "  rt0::resolve_body<rt0::JitScene, rt0::JitCfg, "
       << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    if (k.walk)
+      o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_walk(const LaunchParams P) { rt0::walk_body(P); }\n";
   }
   return o.str();
 }
@@ -297,12 +300,14 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
   int rc = jit_compile(src, code, err);
   if (rc != RT0_OK) return rc;
   CacheEntry e;
-  hipFunction_t f[3] = {};
+  hipFunction_t f[4] = {};
   bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess &&
             hipModuleGetFunction(&f[0], e.mod, "rt0_jit_pass") == hipSuccess;
   if (ok && k.defer)
     ok = hipModuleGetFunction(&f[1], e.mod, "rt0_jit_nee") == hipSuccess &&
          hipModuleGetFunction(&f[2], e.mod, "rt0_jit_resolve") == hipSuccess;
+  if (ok && k.defer && k.walk)
+    ok = hipModuleGetFunction(&f[3], e.mod, "rt0_jit_walk") == hipSuccess;
   if (!ok) {
     err = "hipModuleLoadData/GetFunction failed for the JIT module";
     return RT0_E_HIP;
@@ -310,6 +315,7 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
   e.fns.pass = (void *)f[0];
   e.fns.nee = (void *)f[1];
   e.fns.resolve = (void *)f[2];
+  e.fns.walk = (void *)f[3];
   g_cache[{h, device}] = e;
   *fns = e.fns;
   return RT0_OK;
@@ -432,6 +438,9 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     // the kernels rt0_render launches: deferred light sampling for ReSTIR (rt0_host.cpp)
     const char *d = getenv("RT0_DEFER_NEE");
     key.defer = key.restir && key.max_bounces > 0 && (!d || atoi(d) != 0);
+    // (the host also needs a built BVH; here the scene's TRIANGLE entries decide)
+    const char *wk = getenv("RT0_NEE_WALK");
+    key.walk = key.defer && nm > 0 && ns == 0 && !s.any_tex && !(key.flags & F_ANIM) && (!wk || atoi(wk) != 0) ? 1 : 0;
     rc = rt0h::jit_compile(rt0h::jit_source(s, key), code, e);
   }
   if (code_size) *code_size = code.size();

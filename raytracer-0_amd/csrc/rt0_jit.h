@@ -21,12 +21,14 @@ struct JitKey {
   int halo_check = 1;  // RT0_HALO_CHECK: sharded launches count reservoir fetches outside the halo
   int defer = 0;       // RT0_DEFER_NEE: ReSTIR light sampling in its own kernel (rt0_jit_nee + rt0_jit_resolve)
   int nee_regions = 2;  // RT0_NEE_REGIONS: pass-wave record regions per light-sampling wave
+  int walk = 0;         // RT0_NEE_WALK: the light-sampling calls' triangle occlusion queries in rt0_jit_walk
 };
 
 // The kernels of one compiled module: the pass kernel and, for a deferred
 // ReSTIR key, the light-sampling and resolve kernels (hipFunction_t each).
 struct JitFns {
   void *pass = nullptr, *nee = nullptr, *resolve = nullptr;
+  void *walk = nullptr;  // RT0_NEE_WALK keys
 };
 
 std::string jit_source(const SceneDev &s, const JitKey &k);
