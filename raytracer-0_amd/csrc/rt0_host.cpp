@@ -728,6 +728,14 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       key.halo_check = c->n_shards > 1 ? 1 : 0;
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
       key.defer = defer ? 1 : 0;
+      {  // 16-bit traversal stack entries + high bits in a 64-bit register (rt0_integrator.h BvhStack)
+        const int entries = key.bvh_stack > 0 ? rt0h::jit_stack_entries(key) : 0;
+        const char *e16 = getenv("RT0_BVH_STACK16");
+        key.stack16 = entries > 0 && entries <= 32 && (!e16 || atoi(e16) != 0) &&
+                             (long long)c->n_tris - 1 < (1ll << (16 + 64 / entries))
+                         ? 1
+                         : 0;
+      }
       key.nee_regions = (int)nee_regions_per_wave();
       // (Integrator::restir_split: quadric-only shadow rays -- no SDFs, no
       // textured lights -- and RENDER_MODE 0)

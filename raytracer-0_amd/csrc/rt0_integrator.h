@@ -105,6 +105,9 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_NEE_WALK  // light-sampling calls' triangle occlusion queries in rt0_jit_walk (models scenes)
 #define RT0_NEE_WALK 0
 #endif
+#ifndef RT0_BVH_STACK16  // BVH traversal stacks as 16-bit LDS entries + high bits in a register
+#define RT0_BVH_STACK16 0
+#endif
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
   return x - floorf(x);
@@ -355,10 +358,36 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
 // kernel (closest-hit and occlusion instances alike -- a __shared__ array
 // declared inside the template would be one array per instance); stride =
 // block size, so the 64 lanes of a wave hit 64 different banks.
-DEV int32_t *bvh_stack_lds() {
-  __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
-  return stk_base + threadIdx.x;
-}
+// RT0_BVH_STACK16 (scene-specialised kernels whose every node index fits
+// 16 + 64 / RT0_BVH_STACK bits, selected by the host): 16-bit LDS entries
+// (the index's low half) and the high bits of every entry in one 64-bit
+// register -- 2 B of LDS per entry instead of 4, so the stack no longer caps
+// the waves per CU.  Pushed entries are inner nodes (>= 0).
+struct BvhStack {
+#if RT0_BVH_STACK16
+  static constexpr int HB = 64 / RT0_BVH_STACK;
+  static constexpr uint64_t HM = (1ull << HB) - 1ull;
+  uint16_t *s;
+  uint64_t hb = 0;
+  DEV BvhStack() {
+    __shared__ uint16_t stk_base[RT0_BVH_STACK * 256];
+    s = stk_base + threadIdx.x;
+  }
+  DEV void put(int sp, int v) {
+    s[256 * sp] = (uint16_t)v;
+    hb = (hb & ~(HM << (HB * sp))) | ((uint64_t)((uint32_t)v >> 16) << (HB * sp));
+  }
+  DEV int get(int sp) const { return (int)((uint32_t)s[256 * sp] | ((uint32_t)((hb >> (HB * sp)) & HM) << 16)); }
+#else
+  int32_t *s;
+  DEV BvhStack() {
+    __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
+    s = stk_base + threadIdx.x;
+  }
+  DEV void put(int sp, int v) { s[256 * sp] = v; }
+  DEV int get(int sp) const { return s[256 * sp]; }
+#endif
+};
 // the record counter of this wave's deferred light-sampling region
 DEV uint32_t *nee_wave_counter() {
   __shared__ uint32_t cnt[4];
@@ -373,7 +402,7 @@ DEV uint32_t *nee_wave_counter() {
 // (8.36-8.39 vs 8.57-8.59 ms at 1024^2).
 template <bool ANY = false>
 DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
-  int32_t *stk = bvh_stack_lds();
+  BvhStack stk;
   int sp = 0, node = 0, best = -1;
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
   const TriDev *__restrict__ tris = P.tris;
@@ -411,7 +440,7 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
     }
     if (tl != F_INF && tr != F_INF) {
       const bool lfirst = tl <= tr;
-      stk[256 * sp] = lfirst ? cr : cl;
+      stk.put(sp, lfirst ? cr : cl);
       sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
       node = lfirst ? cl : cr;
     } else if (tl != F_INF) {
@@ -420,7 +449,7 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
       node = cr;
     } else {
       if (sp == 0) break;
-      node = stk[256 * --sp];
+      node = stk.get(--sp);
     }
   }
   return best;
@@ -2654,7 +2683,7 @@ DEV void walk_body(const LaunchParams &P) {
   *(volatile uint32_t *)ctr = 64u;  // every lane stores the same value: jobs 0..63 go by lane index
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
   const TriDev *__restrict__ tris = P.tris;
-  int32_t *stk = bvh_stack_lds();
+  BvhStack stk;
   uint32_t j = threadIdx.x & 63u;
   bool have = j < n;
   v3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
@@ -2695,7 +2724,7 @@ DEV void walk_body(const LaunchParams &P) {
         done = true;
       } else if (tl != F_INF && tr != F_INF) {
         const bool lfirst = tl <= tr;
-        stk[256 * sp] = lfirst ? cr : cl;
+        stk.put(sp, lfirst ? cr : cl);
         sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
         node = lfirst ? cl : cr;
       } else if (tl != F_INF) {
@@ -2705,7 +2734,7 @@ DEV void walk_body(const LaunchParams &P) {
       } else if (sp == 0) {
         done = true;
       } else {
-        node = stk[256 * --sp];
+        node = stk.get(--sp);
       }
       // a ray visits each node at most once: the cap only guarantees that
       // every wave drains even on a corrupt tree
@@ -2723,7 +2752,7 @@ DEV void walk_body(const LaunchParams &P) {
           slot2 = jb.slot2;
           node = 0;
           sp = 0;
-          guard = 0;
+          guard = 0;  // (stale stack entries are never read: sp restarts at 0)
         }
       }
     }

@@ -55,6 +55,8 @@ static std::string strip_includes(const char *src) {
   return out;
 }
 
+int jit_stack_entries(const JitKey &k) { return ((k.bvh_stack + 7) / 8) * 8; }
+
 std::string jit_source(const SceneDev &s, const JitKey &k) {
   std::ostringstream o;
   if (const char *x = getenv("RT0_JIT_EXTRA")) o << "// options: " << x << "\n";  // part of the cache key
@@ -62,16 +64,17 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // the LDS traversal stack sized to this tree (depth + 1 entries, rounded up to
   // 8) instead of the ahead-of-time kernels' 48: 48 x 256 lanes x 4 B = 48 KiB
   // per workgroup would cap a CU at three workgroups
-  if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << ((k.bvh_stack + 7) / 8) * 8 << "\n";
+  if (k.bvh_stack > 0) o << "#define RT0_BVH_STACK " << jit_stack_entries(k) << "\n";
   o << "#define RT0_HALO_CHECK " << k.halo_check << "\n";
   if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
   if (k.defer && k.walk) o << "#define RT0_NEE_WALK 1\n";
+  if (k.bvh_stack > 0 && k.stack16) o << "#define RT0_BVH_STACK16 1\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
   // occupancy target below); with a BVH the extra registers cost more than
   // the halved round trips save (C5 22.95 vs 18.39 ms), so 1 there
   if (k.restir && s.n_models == 0) o << "#ifndef RT0_TAP_BATCH\n#define RT0_TAP_BATCH 2\n#endif\n";
-  o << "using __hip_internal::int32_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
+  o << "using __hip_internal::int32_t; using __hip_internal::uint16_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
   o << strip_includes(rt0_jit_source_text);
   const int nt = s.n_total;
   o << "namespace rt0 {\n";
@@ -147,8 +150,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   const char *wn_env = getenv("RT0_JIT_NEE_WAVES_PER_EU");
   if (w_env)
     o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w_env) << "))) ";
-  else if (s.n_models > 0)
-    o << "__attribute__((amdgpu_waves_per_eu(6))) ";
+  else if (s.n_models > 0)  // with 16-bit stack entries the LDS allows 8: C5 9.14 vs 9.38 ms per pass at 6
+    o << "__attribute__((amdgpu_waves_per_eu(" << (k.stack16 && k.bvh_stack > 0 ? 8 : 6) << "))) ";
   else if (k.restir && !k.defer)
     o << "__attribute__((amdgpu_waves_per_eu(4))) ";
   o << "void rt0_jit_pass(const LaunchParams P) {\n"
@@ -441,6 +444,11 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     // (the host also needs a built BVH; here the scene's TRIANGLE entries decide)
     const char *wk = getenv("RT0_NEE_WALK");
     key.walk = key.defer && nm > 0 && ns == 0 && !s.any_tex && !(key.flags & F_ANIM) && (!wk || atoi(wk) != 0) ? 1 : 0;
+    // (the tree's depth and size are unknown here: RT0_BVH_STACK16=1 and
+    // RT0_JIT_STACK=<entries> select what rt0_render would for such a tree)
+    const char *w16 = getenv("RT0_BVH_STACK16"), *st = getenv("RT0_JIT_STACK");
+    key.stack16 = w16 && atoi(w16) != 0 ? 1 : 0;
+    if (st && nm > 0) key.bvh_stack = atoi(st);
     rc = rt0h::jit_compile(rt0h::jit_source(s, key), code, e);
   }
   if (code_size) *code_size = code.size();

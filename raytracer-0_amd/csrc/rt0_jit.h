@@ -22,6 +22,7 @@ struct JitKey {
   int defer = 0;       // RT0_DEFER_NEE: ReSTIR light sampling in its own kernel (rt0_jit_nee + rt0_jit_resolve)
   int nee_regions = 2;  // RT0_NEE_REGIONS: pass-wave record regions per light-sampling wave
   int walk = 0;         // RT0_NEE_WALK: the light-sampling calls' triangle occlusion queries in rt0_jit_walk
+  int stack16 = 0;      // RT0_BVH_STACK16: every BVH node index fits 16 + 64 / RT0_BVH_STACK bits
 };
 
 // The kernels of one compiled module: the pass kernel and, for a deferred
@@ -32,6 +33,7 @@ struct JitFns {
 };
 
 std::string jit_source(const SceneDev &s, const JitKey &k);
+int jit_stack_entries(const JitKey &k);  // RT0_BVH_STACK of the module (bvh_stack rounded up to 8)
 int jit_compile(const std::string &src, std::vector<char> &code, std::string &err);
 // runtime feature flags (F_*) of a config, and the JIT key of (config, scene)
 uint32_t flags_from_config(const rt0_config &c);
