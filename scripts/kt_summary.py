@@ -8,9 +8,9 @@ Keeps the rt0_jit_pass dispatches after the first SKIP (the warm-up step's
 launches) and reports their median / mean / min / max duration, plus the other
 kernels' totals (rocprofv3's own --stats table averages every dispatch,
 warm-up included).  A deferred ReSTIR pass is three dispatches (rt0_jit_pass,
-rt0_jit_nee, rt0_jit_resolve; rt0_integrator.h): their kept medians are
-reported per kernel and "median_ms" .. "max_ms" are then per pass, the three
-kernels' durations summed pass by pass.
+rt0_jit_nee, rt0_jit_resolve; rt0_integrator.h), four in scenes with models
+(+ rt0_jit_walk): their kept medians are reported per kernel and "median_ms"
+.. "max_ms" are then per pass, the kernels' durations summed pass by pass.
 """
 import csv
 import glob
@@ -20,7 +20,7 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
-GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_resolve")
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve")
 
 
 def main():
@@ -33,9 +33,10 @@ def main():
            for k in GROUP}
     pas = dur[KERNEL]
     per_kernel = {}
-    if dur["rt0_jit_nee"]:  # deferred passes: pass + nee + resolve, one of each per pass
-        n = min(len(v) for v in dur.values())
-        pas = [sum(dur[k][i] for k in GROUP) for i in range(n)]
+    if dur["rt0_jit_nee"]:  # deferred passes: pass + nee (+ walk) + resolve, one of each per pass
+        ks = [k for k in GROUP if dur[k]]
+        n = min(len(dur[k]) for k in ks)
+        pas = [sum(dur[k][i] for k in ks) for i in range(n)]
         per_kernel = {k: statistics.median(v[skip:]) / 1e6 for k, v in dur.items() if v[skip:]}
     kept = pas[skip:]
     other = defaultdict(list)

@@ -7,8 +7,8 @@ into per-launch figures of the scene-specialised pass kernel (rt0_jit_pass).
 Per dispatch of rt0_jit_pass (the counting instance bench.py launches
 afterwards is a different kernel and is excluded), dropping the first SKIP
 dispatches (the warm-up step), averaged over the rest -- for a deferred ReSTIR
-pass (rt0_jit_pass + rt0_jit_nee + rt0_jit_resolve) the three kernels' means
-summed, i.e. per pass:
+pass (rt0_jit_pass + rt0_jit_nee [+ rt0_jit_walk] + rt0_jit_resolve) the
+kernels' means summed, i.e. per pass:
   * HBM traffic: FETCH_SIZE x 2 (MI355X_MICROARCH.md: gfx950 reports half the
     bytes of a 16-B/lane streaming read; scripts/fetch_calib.hip measures the
     factor for the 64-B gathers and bilinear taps of the ReSTIR/BVH kernels)
@@ -31,7 +31,7 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
-GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_resolve")
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve")
 
 
 def dispatches(d, kernel):
