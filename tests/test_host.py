@@ -165,3 +165,29 @@ def test_bench_flop_model_matches_survey():
     assert bench.isect_flop(wl["scene_lines"]) == 151.0
     fps = bench.flop_per_sample({"samples": 100, "isect": 1464, "iter": 736, "nee": 728, "map": 0}, wl)
     assert 4650 < fps < 4760
+
+
+def test_jit_walk_module_for_model_scenes(cfgs, tmp_path, monkeypatch):
+    """A ReSTIR scene with triangle models gets the occlusion-walk kernel
+    (rt0_jit_walk) in its module, and with 16-bit stack entries
+    (RT0_BVH_STACK16, the C5 tree's 24-entry stack) the traversal stacks take
+    2 B of LDS per entry: 256 x 24 x 2 B per workgroup.  Built with hipRTC,
+    no device; rt0_render selects the same key from the built tree."""
+    import glob
+    import re
+    import subprocess
+    cfg = next(c for c in cfgs["configs"] if c["name"] == "c5_spectral_models")
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    monkeypatch.setenv("RT0_JIT_DUMP", str(tmp_path / "k"))
+    monkeypatch.setenv("RT0_BVH_STACK16", "1")
+    monkeypatch.setenv("RT0_JIT_STACK", "24")
+    rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))
+    co = sorted(glob.glob(str(tmp_path / "k_*.co")))[-1]
+    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True,
+                           text=True).stdout
+    lds = {m.group(2): int(m.group(1)) for m in
+           re.finditer(r"\.group_segment_fixed_size:\s+(\d+)(?:.|\n)*?\.name:\s+(\S+)", notes)}
+    assert {"rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve"} <= set(lds), lds
+    assert lds["rt0_jit_walk"] == 256 * 24 * 2 + 16  # the stack + the wave counters
+    assert lds["rt0_jit_pass"] <= 256 * 24 * 2 + 16
+    assert lds["rt0_jit_nee"] == 0  # no BVH walk left in the light-sampling kernel
