@@ -228,6 +228,13 @@ class Progressive:
         self.image = None
 
     def step(self, i):
+        if self.gather is None:
+            # one rank: the zeroing goes straight onto librt0's stream (no
+            # cross-stream events: C1's 0.045-ms launches are host-bound)
+            with self.torch.cuda.stream(self.order.ext):
+                self.acc.zero_()
+            self.r.render_async(1, self.spp)
+            return
         self.acc.zero_()  # torch's stream
         self.order.rt0_after_torch()
         self.r.render_async(1, self.spp)  # librt0's stream
