@@ -8,7 +8,9 @@ accumulators, round-robin ReSTIR bands, the event ordering between librt0's
 stream and torch's, the gather's reorder -- is the code the 8-GPU RCCL run
 executes.  Rank 0's gathered image must equal the N=1 image bit for bit
 (pixels are independent in progressive mode; sharded ReSTIR reads only the
-exchanged halo rows, which hold the same values as the whole image's).
+exchanged halo rows, which hold the same values as the whole image's).  C5
+adds the triangle model: each rank's light-sampling kernel queues its own
+occlusion walks.
 """
 import json
 import os
@@ -36,7 +38,7 @@ def run_bench(tmp_path, config, gpus, extra=()):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("config", ["c2", "c3"])
+@pytest.mark.parametrize("config", ["c2", "c3", "c5"])
 def test_bench_two_ranks_match_one(tmp_path, gpu_required, config):
     one, a = run_bench(tmp_path, config, 1)
     two, b = run_bench(tmp_path, config, 2, ["--dist-backend", "gloo"])
