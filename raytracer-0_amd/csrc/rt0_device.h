@@ -82,7 +82,7 @@ struct BvhNode {
 // running it (its result only adds to the path's radiance; the path's next
 // direction does not depend on it), rt0_jit_nee evaluates the records densely
 // -- every lane has one -- and rt0_jit_resolve adds them to the pixel's
-// sample in bounce order.  64 B.  Each wave of the pass kernel owns a region
+// sample in bounce order.  60 B.  Each wave of the pass kernel owns a region
 // of nee_cap records (64 lanes x max_bounces calls) that it fills in call
 // order through an LDS counter -- no device-wide atomic, whose single address
 // serialises every wave of the chip -- and the NEE kernel gives each region to
@@ -97,6 +97,7 @@ struct NeeRec {
   int32_t k;         // the call's index along the path (0-based)
   int32_t pad;
 };
+static_assert(sizeof(NeeRec) == 60, "NeeRec is 15 words");
 
 // RT0_NEE_WALK (scenes with triangle models): a light-sampling call's
 // triangle occlusion queries go to rt0_jit_walk as WalkJobs, 32 B: the ray
