@@ -115,3 +115,30 @@ def test_deferred_walks_match_inline_models(cfgs, gpu_required):
     close_and_mostly_identical(s0[..., :3], s1[..., :3], "samples")
     # some calls were answered by the walks: the model occludes lights
     assert (m1[..., 3] == 0).any() and (m1[..., 3] > 0).any()
+
+
+@pytest.mark.gpu
+def test_deferred_walks_viewport_models(cfgs, gpu_required):
+    """The walk path on a tile (gl.viewport rectangle) of the model scene:
+    only the rectangle's calls queue walks, and they resolve like the inline
+    render of the same rectangle."""
+    import test_models as T
+    cfg = T.cfg_by_name(cfgs, "c5_spectral_models")
+    vp = (8, 16, 40, 24)
+    out = []
+    for defer in (False, True):
+        r = T.make(cfg, cfgs, 64, 64)
+        r.set_defer_light_sampling(defer)
+        r.set_viewport(*vp)
+        S, M = [], []
+        for k in range(1, 4):
+            r.render(k, 1)
+            S.append(r.read_accum())
+            M.append(r.read_restir(0)[0])
+        out.append((np.stack(S), np.stack(M)))
+    (s0, m0), (s1, m1) = out
+    close_and_mostly_identical(m0, m1, "reservoir main")
+    close_and_mostly_identical(s0[..., :3], s1[..., :3], "samples")
+    outside = np.ones(s1.shape[1:3], bool)
+    outside[vp[1]:vp[1] + vp[3], vp[0]:vp[0] + vp[2]] = False
+    assert not s1[:, outside, :3].any()
