@@ -199,6 +199,70 @@ def cpu_baseline_c(wl, budget_s=8.0):
                       "(%d samples, %.1f s)%s" % (threads, r0, r0 + rows - 1, W, H, n, samples, dt, what)}
 
 
+# ------------------------------------------------------------- GPU clock
+class ClockSampler:
+    """Samples the GPU's current shader clock during the timed region (the C2
+    kernel moves 5.26-5.45 ms with the box's clock, DESIGN 5.00, as much as most
+    A/B deltas): the starred level of the amdgpu driver's pp_dpm_sclk for the
+    device's PCI address, read every 10 ms by a host thread (no GPU call).
+    Reports the median and range, or why it could not (the file missing or
+    unreadable for this user)."""
+
+    def __init__(self, torch, local):
+        import glob
+        self.path, self.err, self.mhz = None, None, []
+        try:
+            bus = torch.cuda.get_device_properties(local).pci_bus_id
+        except Exception as e:  # noqa: BLE001 -- reported, not fatal
+            bus, self.err = None, "no pci_bus_id: %s" % e
+        if bus is not None:
+            for cand in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
+                dev = os.path.basename(os.path.realpath(os.path.dirname(cand))).lower()
+                if dev.endswith(str(bus).lower()[-7:]) or dev == str(bus).lower():
+                    self.path = cand
+                    break
+            if self.path is None:
+                self.err = "no pp_dpm_sclk for PCI %s" % bus
+        self._stop = None
+        self._th = None
+
+    def _read(self):
+        try:
+            for line in open(self.path):
+                if line.rstrip().endswith("*"):
+                    return float(line.split(":")[1].strip().lower().replace("mhz", "").replace("*", "").strip())
+        except (OSError, ValueError, IndexError) as e:
+            self.err = "%s: %s" % (self.path, e)
+        return None
+
+    def start(self):
+        import threading
+        if self.path is None:
+            return
+        self._stop = threading.Event()
+
+        def run():
+            while not self._stop.is_set():
+                v = self._read()
+                if v is not None:
+                    self.mhz.append(v)
+                self._stop.wait(0.01)
+        self._th = threading.Thread(target=run, daemon=True)
+        self._th.start()
+
+    def stop(self):
+        if self._th is not None:
+            self._stop.set()
+            self._th.join()
+
+    def report(self):
+        if not self.mhz:
+            return {"median_mhz": None, "source": self.path, "error": self.err or "no samples"}
+        m = sorted(self.mhz)
+        return {"median_mhz": m[len(m) // 2], "min_mhz": m[0], "max_mhz": m[-1], "samples": len(m),
+                "source": self.path + " (current level, sampled every 10 ms over the timed region)"}
+
+
 # ---------------------------------------------------------------- workloads
 class Progressive:
     """C1/C2/C4: 16-row bands round-robin, band-packed accumulators, one gather."""
@@ -225,6 +289,7 @@ class Progressive:
             self.samples_per_step = W * H * self.spp
         self.order = shard.StreamOrder(self.r, "cuda:%d" % local)
         self.kernel_ms, self.gather_ms, self.launches = [], [], 0
+        self.kernel_estimate = False
         self.image = None
 
     def step(self, i):
@@ -300,6 +365,7 @@ class Restir:
             self.r.set_accum_buffer(self.acc.data_ptr())
             self.samples_per_step = W * H * self.spp
         self.kernel_ms, self.gather_ms, self.launches = [], [], 0
+        self.kernel_estimate = False
         self.image = None
 
     def step(self, i):
@@ -320,10 +386,13 @@ class Restir:
         if self.sh is None:
             ms, n = self.r.last_kernel_ms()  # the render call's spp launches
         else:
-            # the last pass's kernel time (the timing events of earlier async
-            # passes are overwritten): ReSTIR pass times are flat over frames
+            # an ESTIMATE: the last pass's kernel time x spp (the timing events
+            # of earlier async passes are overwritten; pass times vary in early
+            # frames -- temporal taps from frame 3, halved spatial taps below
+            # frame 10 -- so the line labels it, kernel_time_source)
             m, _ = self.r.last_kernel_ms()
             ms, n = m * self.spp, self.spp
+            self.kernel_estimate = True
             self.gather_ms.append(self.order.elapsed_ms())
         self.kernel_ms.append(ms)
         self.launches = n
@@ -423,7 +492,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", help="workload of rt0/workloads.json: c1 c2 c2_refcaps c3 c4 c5")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--secondary", action="store_true", help="also time the MAX_DIFF_BOUNCES=4 variant of c2")
+    ap.add_argument("--secondary", action="store_true", help="(default now; kept for old command lines)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary line: c2 at MAX_DIFF_BOUNCES=4, c4 at MAX_DIFF_BOUNCES=12")
     ap.add_argument("--jit", type=int, default=1, help="1: scene-specialised kernels (default), 0: ahead-of-time")
     ap.add_argument("--executor-compat", action="store_true",
                     help="rt0_set_executor_compat(1): the reference executor's reservoir stores (ReSTIR workloads)")
@@ -462,9 +533,11 @@ def main():
         job.step(i)
     job.kernel_ms.clear()
     job.gather_ms.clear()
+    clock = ClockSampler(torch, local)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    clock.start()
     t0 = time.perf_counter()
     for i in range(args.steps):
         job.step(args.warmup + i)
@@ -472,6 +545,7 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    clock.stop()
     job.collect()  # the last timed step's kernel time, read outside the timed region
     if dist:
         t = torch.tensor([dt], device="cuda:%d" % local) if not staged else torch.tensor([dt])
@@ -525,6 +599,11 @@ def main():
             "kernel_ms_per_step": round(kern_s * 1000.0, 3),
             "launches_per_step": job.launches,
             "kernel_ms_per_launch": round(kern_launch_s * 1000.0, 3),
+            "kernel_time_source": "ESTIMATE: rank 0's last pass (HIP events) x passes per step"
+            if job.kernel_estimate else "HIP events on librt0's stream around the last timed step's launches",
+            # counters cannot be read from inside this process: traffic comes
+            # from the committed rocprofv3 --pmc passes of the same workload
+            "traffic_measured_in_this_run": False,
             "note": "FP32 vector kernel (no MFMA): peak = MI355X FP32 vector 157.3 TF; FLOP model SURVEY 8d x "
                     "counted events (counting instance, whole image); achieved over rank 0's kernel time (HIP "
                     "events on librt0's stream); traffic = PMC FETCH_SIZE corrected per access shape (hbm_traffic) + "
@@ -569,18 +648,26 @@ def main():
     if wl.get("baseline_spp") and wl["baseline_spp"] != wl["spp"]:
         out["config"]["spp_note"] = ("BASELINE.md quotes this config at %d spp; one bench step renders %d passes "
                                      "(Msamples/s is per sample either way)" % (wl["baseline_spp"], wl["spp"]))
+    out["gpu_clock"] = clock.report()
     if job.gather_ms:
         out["gather_ms_per_step"] = round(float(np.mean(job.gather_ms)), 3)
-    if args.secondary and args.config == "c2":
-        sec = workloads.get("c2_refcaps")
-        workloads.configure(job.r, sec)
+    if not args.no_secondary and world == 1 and args.config in ("c2", "c4"):
+        # after the timed region, same renderer: C2 at the reference's caps
+        # (MAX_DIFF_BOUNCES = 4, SURVEY 8d "report both"); C4 at its true depth
+        # (MAX_DIFF_BOUNCES = 12: the timed line keeps the reference's 4, a cap
+        # the 12-bounce loop reaches first)
+        if args.config == "c2":
+            sec, over, key = workloads.get("c2_refcaps"), None, "secondary_refcaps_Msamples_s"
+        else:
+            sec, over, key = wl, {"MAX_DIFF_BOUNCES": 12}, "secondary_truedepth_Msamples_s"
+        workloads.configure(job.r, sec, over)
         job.step(0)
+        torch.cuda.synchronize()
         t1 = time.perf_counter()
         for i in range(args.steps):
             job.step(i)
         torch.cuda.synchronize()
-        out["secondary_refcaps_Msamples_s"] = round(W * H * sec["spp"] * args.steps
-                                                    / (time.perf_counter() - t1) / 1e6, 3)
+        out[key] = round(W * H * sec["spp"] * args.steps / (time.perf_counter() - t1) / 1e6, 3)
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
         # the JS integrator covers quadrics, SDFs, media, MIS and ReSTIR
         # (SURVEY 8d's C1-C4 feature sets), not spectral rendering or triangle models

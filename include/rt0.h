@@ -125,10 +125,11 @@ int rt0_get_scene(const rt0_ctx *ctx, rt0_mesh *meshes, int max_meshes, int *n_m
  * reference's unshipped mesh.js/bvh.js path; its iTriangle is the commented
  * Moller-Trumbore of raytracer.glsl:864-892): positions = n_vertices x 3
  * floats (object space), indices = n_triangles x 3 vertex indices.  Copied.
- * The next render builds one LBVH over all instances in world space on the
- * device (Morton codes + radix sort + Karras hierarchy + refit, rt0_bvh.hip);
- * traversal is part of intersection() (after the quadrics, before the SDF
- * march).  rt0_model_info builds now if needed and reports the triangle count
+ * The next render builds one BVH over all instances in world space: a
+ * binned-SAH tree on the host (rt0_bvh_sah.cpp, the default), or with
+ * RT0_BVH_BUILD=lbvh in the environment the device LBVH of rt0_bvh.hip
+ * (Morton codes + radix sort + Karras hierarchy + refit).  Traversal is part
+ * of intersection() (after the quadrics, before the SDF march).  rt0_model_info builds now if needed and reports the triangle count
  * and tree depth (RT0_E_UNSUPPORTED if deeper than the traversal stack). */
 int rt0_set_model(rt0_ctx *ctx, int model, const float *positions, int n_vertices, const int32_t *indices,
                   int n_triangles);
@@ -261,10 +262,12 @@ int rt0_set_accum_buffer_compact(rt0_ctx *ctx, void *dptr, int *rows);
 
 /* Sharded ReSTIR: the reservoir textures of index.js:149-163
  * (units 7-12) and their swap chain (swapReSTIRBuffers, index.js:795-820).
- * A shard renders one contiguous row block (rt0_set_shard with
- * band_rows * n_shards >= height), one pass per rt0_render call; between
- * passes the caller copies `rows` halo rows of the newest reservoir planes
- * from the neighbouring shards (rt0/shard.py does it over RCCL).
+ * A shard renders its row bands of rt0_set_shard -- one contiguous row block
+ * when band_rows * n_shards >= height, or several bands dealt round-robin
+ * (what bench.py runs: rt0/shard.py interleaved_band), then halo <= band_rows
+ * -- one pass per rt0_render call; between passes the caller copies `rows`
+ * halo rows of the newest reservoir planes across every band boundary between
+ * two shards (rt0/shard.py RestirShard does it over RCCL).
  *   rt0_set_restir_buffers: 8 caller-owned W*H*4 f32 device planes (e.g.
  *     torch tensors the collective reads/writes); NULL returns to
  *     context-owned planes.  All planes are cleared.
@@ -299,8 +302,16 @@ int rt0_set_executor_compat(rt0_ctx *ctx, int enable);
 /* Deferred ReSTIR light sampling (scene-specialised kernels): a pass runs its
  * paths with every sampleLightsReSTIR call (raytracer.glsl:1619-1801)
  * appended to a per-wave list, evaluates the list in a second kernel with
- * every lane busy, and completes the samples in a third.  Same arguments,
- * same arithmetic as the inline calls (results equal up to FMA placement).
+ * every lane busy, and completes the samples in a last one (resolve).  In
+ * scenes with triangle models (RENDER_MODE 0, no SDFs, no textured lights)
+ * a third kernel between them answers the calls' triangle occlusion queries
+ * (the visibility and shadow rays) on dense lanes: four dispatches per pass.
+ * Same arguments and arithmetic as the inline calls, but NOT bitwise equal:
+ * FMA placement can differ, and a sample's fp32 additions run in another
+ * order (the path's own radiance first, then the light-sampling results in
+ * call order, instead of interleaved per bounce).  tests/test_gpu_defer.py
+ * holds samples within 1e-5 and reservoirs within 1e-4 relative of the
+ * inline calls, >= 98% of each bit-identical.
  * 1 (default; RT0_DEFER_NEE=0 in the environment at rt0_create turns it
  * off) or 0 = inline calls.  Executor compatibility always runs them inline.
  * Replaces nothing in the reference: the GL pipeline has no such choice. */

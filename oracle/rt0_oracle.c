@@ -185,6 +185,8 @@ typedef struct {
   /* 1 = model SwiftShader 4.1's masked-execution quirk (see radiance()) */
   int ghost;
   int scatter0_exit; /* SWIFTSHADER_SCATTER0_EXIT: the executor's first-iteration `continue` (see radiance) */
+  int scatter_exit;  /* SWIFTSHADER_SCATTER_EXIT: the executor retires the lane at every scatter `continue` */
+  int dbg_paths;     /* RT0_DEBUG_PATHS: non-ReSTIR reservoir outputs carry per-sample path statistics */
   /* camera uniforms (index.js:421-423) */
   v3 cam_pos, cam_look, cam_params;
   /* asset textures (index.js:256-296): 0..3 u_tex0..3, 4 u_rnd_tex; RGBA8 */
@@ -208,6 +210,8 @@ typedef struct {
   unsigned frame;
   float fcx, fcy; /* gl_FragCoord.xy */
   int diff_b, spec_b, trans_b, scat_ev;
+  int last_depth, first_scat; /* RT0_DEBUG_PATHS */
+  float dbg_hist, dbg_ev;      /* RT0_DEBUG_PATHS: depth history (base 16), loop-exit events (base 8) */
   float hero;
   /* ReSTIR */
   const float *tex[6]; /* restir_buffer, restir_aux, h1, h1a, h2, h2a */
@@ -1290,6 +1294,8 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
   regs.have = 0;
   for (int depth = 0; depth < o->max_bounces; ++depth) {
     F->n_iter++;
+    F->last_depth = depth;
+    F->dbg_hist = F->dbg_hist * 16.0f + (float)depth;
     Hit hit;
     float t = intersection(F, ro, rd, &hit);
     if (trace_pixel(F))
@@ -1329,9 +1335,10 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         ro = sp;
         spec = 0;
         ++F->scat_ev;
+        if (F->first_scat < 0) F->first_scat = depth;
         int stop = (F->scat_ev >= o->max_scatter || vmaxc(mask) < 0.01f);
         if (o->ghost) ghost_brdf(F, &regs, seed);
-        if (stop) break;
+        if (stop) { F->dbg_ev = F->dbg_ev * 8.0f + 6.0f; break; }
         /* SWIFTSHADER_SCATTER0_EXIT: the reference executor (SwiftShader 4.1)
          * leaves the bounce loop at this `continue` (raytracer.glsl:2050) when
          * it is executed in the loop's first iteration: the loop body has
@@ -1341,12 +1348,15 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
          * continues at iteration 0 ends with one iteration's contribution;
          * at later iterations the same continue is honoured). */
         if (o->scatter0_exit && depth == 0) break;
+        if (o->scatter_exit) break;
+        F->dbg_ev = F->dbg_ev * 8.0f + 1.0f;
         continue;
       }
     }
     if (t == INF_T) {
       if (!spec && o->sample_lights) {
         if (o->ghost) ghost_brdf(F, &regs, seed);
+        F->dbg_ev = F->dbg_ev * 8.0f + 2.0f;
         break;
       }
       if (o->use_cubemap) {
@@ -1358,6 +1368,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         acc = add(acc, mul(mask, sky));
       }
       if (o->ghost) ghost_brdf(F, &regs, seed);
+      F->dbg_ev = F->dbg_ev * 8.0f + 2.0f;
       break;
     }
     const Mesh *mesh = &o->meshes[hit.index];
@@ -1376,6 +1387,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
       }
       acc = add(acc, muls(mul(mask, e), w));
       if (o->ghost) ghost_brdf(F, &regs, seed);
+      F->dbg_ev = F->dbg_ev * 8.0f + 3.0f;
       break;
     }
     prev_nl = muls(hit.n, inside);
@@ -1384,10 +1396,16 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
       regs.have = 1; regs.hit = hit; regs.e = e; regs.inside = inside; regs.bounce = (float)depth;
       regs.rd = rd; regs.spec = spec;
     }
-    if (vmaxc(mask) < 0.01f) break;
-    if (F->diff_b >= o->max_diff || F->spec_b >= o->max_spec || F->trans_b >= o->max_trans ||
-        F->scat_ev >= o->max_scatter)
+    if (vmaxc(mask) < 0.01f) {
+      F->dbg_ev = F->dbg_ev * 8.0f + 4.0f;
       break;
+    }
+    if (F->diff_b >= o->max_diff || F->spec_b >= o->max_spec || F->trans_b >= o->max_trans ||
+        F->scat_ev >= o->max_scatter) {
+      F->dbg_ev = F->dbg_ev * 8.0f + 5.0f;
+      break;
+    }
+    F->dbg_ev = F->dbg_ev * 8.0f + 7.0f;
   }
   return acc;
 }
@@ -1424,6 +1442,10 @@ static v3 shade_pixel(Frag *F, int px, int py) {
   F->fcx = fcx;
   F->fcy = fcy;
   F->diff_b = F->spec_b = F->trans_b = F->scat_ev = 0;
+  F->last_depth = -1;
+  F->first_scat = -1;
+  F->dbg_hist = 0.0f;
+  F->dbg_ev = 0.0f;
   F->hero = 550.0f;
   float stx = 2.0f * fcx / rx - 1.0f, sty = 2.0f * fcy / ry - 1.0f;
   float aspect = rx / ry;
@@ -1628,6 +1650,8 @@ int or_set_constant(void *h, const char *name, double v) {
   else if (!strcmp(name, "LIGHT_PATH_LENGTH")) { /* unused by the shader */ }
   else if (!strcmp(name, "SWIFTSHADER_GHOST")) o->ghost = iv;
   else if (!strcmp(name, "SWIFTSHADER_SCATTER0_EXIT")) o->scatter0_exit = iv;
+  else if (!strcmp(name, "SWIFTSHADER_SCATTER_EXIT")) o->scatter_exit = iv;
+  else if (!strcmp(name, "RT0_DEBUG_PATHS")) o->dbg_paths = iv;
   else if (!strcmp(name, "RENDER_MODE")) {
     o->render_mode = iv;
     if (iv != 0 && iv != 1) { snprintf(o->err, sizeof o->err, "RENDER_MODE must be 0 or 1"); return -1; }
@@ -1699,9 +1723,17 @@ int or_render_frame(void *h, unsigned frame, float *out, const float *const *res
       F.fr_W = 0; F.fr_M = 0; F.fr_ws = 0; F.fr_age = 0; F.fr_idx = -1;
       memset(F.fr_pos, 0, sizeof F.fr_pos);
       memset(F.fr_col, 0, sizeof F.fr_col);
+      const uint64_t it0 = F.n_iter;
       v3 col = shade_pixel(&F, x, y);
       size_t p = ((size_t)y * o->w + x) * 4;
       out[p] = col.x; out[p + 1] = col.y; out[p + 2] = col.z; out[p + 3] = 0.0f;
+      if (o->dbg_paths && !o->use_restir_def && restir_main && restir_aux) {
+        restir_main[p] = (float)(F.n_iter - it0); restir_main[p + 1] = F.dbg_hist;
+        restir_main[p + 2] = (float)F.scat_ev; restir_main[p + 3] = (float)F.diff_b;
+        restir_aux[p] = F.dbg_ev; restir_aux[p + 1] = (float)F.trans_b;
+        restir_aux[p + 2] = (float)F.first_scat; restir_aux[p + 3] = (float)F.spec_b;
+        continue;
+      }
       if (restir_main) {
         int have = o->use_restir_def;
         restir_main[p] = have ? F.fr_pos[0] : 0; restir_main[p + 1] = have ? F.fr_pos[1] : 0;

@@ -127,6 +127,7 @@ struct rt0_ctx {
   size_t nee_slots = 0;  // records d_nee_rec holds (pass waves x 64 x calls per lane)
   size_t nee_waves = 0;  // entries of d_nee_count
   size_t nee_pixels = 0;
+  size_t nee_planes = 0;  // float4 planes of the image d_nee_out holds (one per call index)
   std::string jit_err;
   std::string err;
 };
@@ -176,20 +177,48 @@ static int clear_buffers(rt0_ctx *c) {
 // fault to stderr (then the previous handler -- e.g. Python's faulthandler --
 // runs).  Installed at the first rt0_create.
 static struct sigaction g_prev_segv;
+static void put_hex(char *buf, int *len, uintptr_t v) {  // async-signal-safe formatting
+  char t[2 + 2 * sizeof v];
+  int n = 0;
+  do {
+    t[n++] = "0123456789abcdef"[v & 15];
+    v >>= 4;
+  } while (v);
+  buf[(*len)++] = '0';
+  buf[(*len)++] = 'x';
+  while (n) buf[(*len)++] = t[--n];
+}
 static void segv_trace(int sig, siginfo_t *si, void *) {
-  void *frames[64];
-  const int n = backtrace(frames, 64);
   char msg[96];
-  const int len = snprintf(msg, sizeof msg, "rt0: signal %d at address %p; native stack:\n", sig, si ? si->si_addr : nullptr);
-  if (len > 0) (void)!write(2, msg, (size_t)len);
+  int len = 0;
+  static const char head[] = "rt0: SIGSEGV at address ";
+  memcpy(msg, head, sizeof head - 1);
+  len = sizeof head - 1;
+  put_hex(msg, &len, (uintptr_t)(si ? si->si_addr : nullptr));
+  static const char tail[] = "; native stack:\n";
+  memcpy(msg + len, tail, sizeof tail - 1);
+  len += sizeof tail - 1;
+  (void)!write(2, msg, (size_t)len);
+  void *frames[64];
+  const int n = backtrace(frames, 64);  // libgcc preloaded at install: no allocation here
   backtrace_symbols_fd(frames, n, 2);
-  sigaction(SIGSEGV, &g_prev_segv, nullptr);  // the fault repeats into the previous handler
+  // the fault repeats into the previous handler; an ignored or default
+  // disposition would re-execute the faulting instruction forever or be lost
+  if (!(g_prev_segv.sa_flags & SA_SIGINFO) &&
+      (g_prev_segv.sa_handler == SIG_IGN || g_prev_segv.sa_handler == SIG_DFL)) {
+    signal(sig, SIG_DFL);
+    raise(sig);
+    return;
+  }
+  sigaction(SIGSEGV, &g_prev_segv, nullptr);
 }
 static void install_segv_trace() {
   static bool done = false;
   if (done || !getenv("RT0_SEGV_TRACE")) return;
   done = true;
-  // an alternate stack, so that a stack overflow can be reported too
+  void *warm[2];
+  (void)backtrace(warm, 2);  // loads libgcc's unwinder now, not inside the handler
+  // an alternate stack (this thread's), so that a stack overflow can be reported too
   static char altstack[1 << 16];
   stack_t ss;
   memset(&ss, 0, sizeof ss);
@@ -721,8 +750,17 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   // (rt0_integrator.h nee_body): scene-specialised kernels only; the executor
   // ghost (F_EXEC_GHOST) keeps the inline calls
   const bool defer = restir && c->use_jit && !c->counting && !c->exec_compat && c->defer_nee && p.max_bounces > 0;
+  // the occlusion-walk kernel (rt0_integrator.h walk_body) for scenes with
+  // triangle models: quadric-only shadow geometry (no SDFs, no textured
+  // lights) and RENDER_MODE 0 (Integrator::restir_split), and a grid whose
+  // records fit the result tag's 29-bit slot field.  Re-evaluated every render:
+  // a viewport or image size change alone can flip it.
+  const bool want_walk = defer && nee_walk_enabled() && c->host_scene.n_models > 0 && c->n_tris > 0 &&
+                         c->host_scene.n_sdfs == 0 && !c->host_scene.any_tex && c->cfg.render_mode == 0 &&
+                         (size_t)grid.x * grid.y * 4 * 64 * (size_t)p.max_bounces < (1u << 29) - 1u;
   if (c->use_jit && !c->counting) {
-    if (c->jit_dirty || !c->jit.pass || (defer != (c->jit.nee != nullptr))) {
+    if (c->jit_dirty || !c->jit.pass || (defer != (c->jit.nee != nullptr)) ||
+        (defer && want_walk != (c->jit.walk != nullptr))) {
       rt0h::JitKey key = rt0h::make_jit_key(c->cfg, c->n_sdfs);
       if (c->exec_compat) key.flags |= F_EXEC_GHOST;
       key.halo_check = c->n_shards > 1 ? 1 : 0;
@@ -737,14 +775,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
                          : 0;
       }
       key.nee_regions = (int)nee_regions_per_wave();
-      // (Integrator::restir_split: quadric-only shadow rays -- no SDFs, no
-      // textured lights -- and RENDER_MODE 0)
-      // (the result tag holds record slot + 1 in 29 bits)
-      key.walk = defer && nee_walk_enabled() && c->host_scene.n_models > 0 && c->n_tris > 0 &&
-                         c->host_scene.n_sdfs == 0 && !c->host_scene.any_tex && !(key.flags & F_ANIM) &&
-                         (size_t)grid.x * grid.y * 4 * 64 * (size_t)p.max_bounces < (1u << 29) - 1u
-                     ? 1
-                     : 0;
+      key.walk = want_walk ? 1 : 0;
       int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
       c->jit_dirty = false;
@@ -755,14 +786,18 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   if (defer) {
     // a region of 64 lanes x max_bounces records per pass wave: a path makes
     // at most one light-sampling call per bounce (rt0_integrator.h step)
+    // (nee_out holds max_bounces planes of the whole image: a config with more
+    // bounces needs more planes even when a smaller viewport or shard needs
+    // fewer record slots)
     const size_t pixels = (size_t)c->W * c->H, slots = pass_waves * 64 * (size_t)p.max_bounces;
-    if (slots > c->nee_slots || pass_waves > c->nee_waves || pixels != c->nee_pixels) {
+    if (slots > c->nee_slots || pass_waves > c->nee_waves || pixels != c->nee_pixels ||
+        (size_t)p.max_bounces > c->nee_planes) {
       for (void **q : {(void **)&c->d_nee_rec, (void **)&c->d_nee_count, (void **)&c->d_nee_out,
                        (void **)&c->d_nee_partial, (void **)&c->d_nee_n}) {
         if (*q) HIPCHK(c, hipFree(*q));
         *q = nullptr;
       }
-      c->nee_slots = c->nee_waves = c->nee_pixels = 0;
+      c->nee_slots = c->nee_waves = c->nee_pixels = c->nee_planes = 0;
       HIPCHK(c, hipMalloc(&c->d_nee_rec, slots * sizeof(NeeRec)));
       HIPCHK(c, hipMalloc(&c->d_nee_count, pass_waves * sizeof(uint32_t)));
       HIPCHK(c, hipMalloc(&c->d_nee_out, pixels * (size_t)p.max_bounces * sizeof(float4)));
@@ -771,6 +806,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       c->nee_slots = slots;
       c->nee_waves = pass_waves;
       c->nee_pixels = pixels;
+      c->nee_planes = (size_t)p.max_bounces;
     }
     p.defer = 1;
     p.nee_cap = 64 * p.max_bounces;
@@ -781,8 +817,6 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     p.nee_partial = c->d_nee_partial;
     p.nee_n = c->d_nee_n;
     if (c->jit.walk) {
-      if (slots >= (1u << 29) - 1u)  // the module was compiled for a smaller grid (the tag's slot field)
-        return fail(c, RT0_E_UNSUPPORTED, "too many light-sampling records for the walk tags");
       // per light-sampling wave: up to two rays per record of its regions
       const size_t waves = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave();
       const size_t jobs = waves * 2 * (size_t)nee_regions_per_wave() * (size_t)p.nee_cap;

@@ -244,9 +244,6 @@ struct Hit {
 #ifndef RT0_MARCH_BUDGET
 #define RT0_MARCH_BUDGET 8
 #endif
-#ifndef RT0_FAST_SHADOW  // A/B knob: shadow rays through Geometry::shadow_light
-#define RT0_FAST_SHADOW 1
-#endif
 
 struct March {
   v3 o, d;
@@ -585,12 +582,10 @@ struct Geometry {
     if constexpr (Scene::kMayHaveModels) {
       // triangles come after the quadrics (strict <): one before tL is the
       // closest hit, and no model is a light -- an occlusion query suffices
-#ifndef RT0_EXP_NO_BVH_OCC  // profiling experiment only (breaks parity): no triangle occlusion queries
       if (il >= 0 && sc.n_models() > 0 && P.n_tris > 0) {
         float tt = tl;
         if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) il = -1;
       }
-#endif
     }
     return il;
   }
@@ -630,11 +625,9 @@ struct Geometry {
     float tt;
     const bool vq = visible_q<Cfg>(P, sc, C, o, d, m, lim, tt);
     if constexpr (Scene::kMayHaveModels) {
-#ifndef RT0_EXP_NO_BVH_OCC
       if (sc.n_models() > 0 && P.n_tris > 0) {
         if (bvh_closest<true>(P, o, d, m, tt, nbvh) >= 0) return false;
       }
-#endif
     }
     return vq;
   }
@@ -1162,10 +1155,10 @@ struct Integrator {
   DEV bool flag(uint32_t f) const { return (C.flags() & f) != 0; }
   // Shadow rays of sphere lights through G::shadow_light: scene-specialised
   // scenes of quadrics only (no SDF march, no triangle models, no textured
-  // light colour to evaluate at the hit).  RT0_FAST_SHADOW 0 = intersect().
+  // light colour to evaluate at the hit).
   DEV bool fast_shadow() const {
-    if constexpr (Scene::kStatic) return RT0_FAST_SHADOW && Scene::kSdfs == 0 && !Scene::any_tex();
-    else return RT0_FAST_SHADOW && sc.n_sdfs() == 0 && !sc.any_tex();
+    if constexpr (Scene::kStatic) return Scene::kSdfs == 0 && !Scene::any_tex();
+    else return sc.n_sdfs() == 0 && !sc.any_tex();
   }
   // material of a shadow ray's light: folds to the one light mesh of a
   // single-light scene, a per-lane record otherwise
@@ -1248,16 +1241,11 @@ struct Integrator {
           const int il = G::template shadow_light<Cfg>(P, sc, C, x + nl * EPSILON, sr, t, COUNT ? n_bvh : nullptr);
           return sphere_light_lit(il, t, cos_a_max, sr, nl);
         }
-#ifdef RT0_EXP_NO_SHADOW  // profiling experiment only (breaks parity): shadow ray skipped
-        float t = 1.0f;
-        hit.index = li;
-#else
         float t = isect(x + nl * EPSILON, sr, hit, ms);
         if (ms && t < 0.0f) {
           *susp = true;
           return dl;
         }
-#endif
         const MatRec mh = sc.mat(hit.index);
         if (mh.type == M_LIGHT) {
           float weight = 2.0f * (1.0f - cos_a_max);
@@ -1630,11 +1618,7 @@ struct Integrator {
       Res nb = empty_res();
       if (!(nx < 0.0f || nx > 1.0f || ny < 0.0f || ny > 1.0f)) {
         if (COUNT) ++n_stap;
-#ifdef RT0_EXP_SPATIAL_SELF  // profiling experiment only (breaks parity): every tap reads the pixel's own texels
-        nb = unpack(tex2d(P.rin[0], scx, scy), tex2d(P.rin[1], scx, scy));
-#else
         nb = unpack(tex2d(P.rin[0], nx, ny), tex2d(P.rin[1], nx, ny));
-#endif
       }
       if (nb.M > 0.0f) {
         if (nb.idx >= 0) {
@@ -1853,9 +1837,6 @@ struct Integrator {
   DEV v3 sample_lights(v3 x, v3 nl, const MatRec &mat, float seed, float bounce) {
     const float fr = (float)frame;
     v3 acc = mk(0.f, 0.f, 0.f);
-#ifdef RT0_EXP_NO_NEE  // profiling experiment only (breaks parity): no light sampling
-    return acc;
-#endif
     const int nlights = sc.n_lights();
     if (flag(F_RESTIR) && flag(F_MIS)) {
       if (RESTIR && flag(F_RESTIR_DEF)) {
@@ -1897,9 +1878,6 @@ struct Integrator {
         LightGeo geo{false, 0.f, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
         v3 ls = direct_light(idx, x, nl, nc_addmul(base, (float)i, 123.456f), nullptr, nullptr, &geo);
         if (dot(ls, ls) > 0.000001f) {
-#ifdef RT0_NO_MIS_REUSE  // A/B only: recompute lightSamplingPdf's geometry
-          geo.sphere = false;
-#endif
           if (geo.sphere && !flag(F_ANIM)) {  // the sampling's own d², cos θmax and direction
             float lp = 0.0f;
             if (geo.d2 > geo.r2 && 1.0f - geo.cam >= 1e-6f) lp = frcp(TWO_PI * (1.0f - geo.cam));
@@ -2033,7 +2011,6 @@ struct Integrator {
     March *mq = march_slot(ps);
     bool susp = false;
     if (VOL && nc.vol) {
-#ifndef RT0_EXP_NO_VOL_NEE  // profiling experiment only (breaks parity): no in-scatter NEE
       const v3 sp = nc.x, rd = nc.n;
       const float seed = ps.seed;
       const int depth = ps.depth;
@@ -2067,7 +2044,6 @@ struct Integrator {
         ps.acc = ps.acc + ((((ps.mask * mk(lmt.cr, lmt.cg, lmt.cb)) * mk(lmt.er, lmt.eg, lmt.eb)) * phase) * Tf) *
                               (PI_F * omega);
       });
-#endif
       return !susp;
     }
     // sample_lights() without ReSTIR: use_restir routes nothing here
@@ -2148,7 +2124,6 @@ struct Integrator {
             }
             return stop ? false : ++ps.depth < C.max_bounces();
           }
-#ifndef RT0_EXP_NO_VOL_NEE  // profiling experiment only (breaks parity): no in-scatter NEE
           if (flag(F_SAMPLE_LIGHTS)) {
             for_lights(sc, [&](int li) {
               int lidx = sc.light(li);
@@ -2176,7 +2151,6 @@ struct Integrator {
                               (PI_F * omega);
             });
           }
-#endif
           rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
           ro = sp;
           spec = false;

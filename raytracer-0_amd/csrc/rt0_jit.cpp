@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -27,6 +28,8 @@
 #include <dlfcn.h>
 #include <link.h>
 #include <unistd.h>
+
+extern char **environ;
 
 #include "../../include/rt0.h"
 #include "rt0_device.h"
@@ -75,7 +78,17 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // the halved round trips save (C5 22.95 vs 18.39 ms), so 1 there
   if (k.restir && s.n_models == 0) o << "#ifndef RT0_TAP_BATCH\n#define RT0_TAP_BATCH 2\n#endif\n";
   o << "using __hip_internal::int32_t; using __hip_internal::uint16_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
-  o << strip_includes(rt0_jit_source_text);
+  // RT0_JIT_SOURCE=<file>: the device source to compile instead of the
+  // embedded one (rt0_device.h + rt0_integrator.h concatenated) -- profiling
+  // probes only (scripts/probes.sh); part of the cache key like everything here
+  if (const char *f = getenv("RT0_JIT_SOURCE")) {
+    std::ifstream in(f);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    o << strip_includes(ss.str().c_str());
+  } else {
+    o << strip_includes(rt0_jit_source_text);
+  }
   const int nt = s.n_total;
   o << "namespace rt0 {\n";
   o << "__constant__ const GeomRec kJitGeom[" << (nt > 0 ? nt : 1) << "] = {";
@@ -218,6 +231,13 @@ struct Rtc {
   decltype(&hiprtcGetCodeSize) code_size = nullptr;
   decltype(&hiprtcGetCode) get_code = nullptr;
   decltype(&hiprtcDestroyProgram) destroy = nullptr;
+  // `environ` of the private namespace's own libc copy: it was set from the
+  // process environment when the namespace was created, and a later
+  // setenv()/putenv() in the process (Python's os.environ, node's
+  // process.env) may free that array -- hipRTC's getenv() calls then read
+  // freed memory (the crash of the round-3 test run, in hiprtcCreateProgram).
+  // jit_compile points it at the process's current environment first.
+  char ***ns_environ = nullptr;
   std::string path, error;
 };
 
@@ -240,6 +260,7 @@ static const Rtc &rtc() {
     r.code_size = (decltype(r.code_size))dlsym(h, "hiprtcGetCodeSize");
     r.get_code = (decltype(r.get_code))dlsym(h, "hiprtcGetCode");
     r.destroy = (decltype(r.destroy))dlsym(h, "hiprtcDestroyProgram");
+    r.ns_environ = (char ***)dlsym(h, "environ");  // found in the namespace's libc (a dependency of hipRTC)
     if (!r.create || !r.compile || !r.log_size || !r.log || !r.code_size || !r.get_code || !r.destroy)
       r.error = "hipRTC at " + r.path + " lacks an entry point";
   });
@@ -253,6 +274,7 @@ int jit_compile(const std::string &src, std::vector<char> &code, std::string &er
     return RT0_E_HIP;
   }
   dump_artifact(src, ".hip", src.data(), src.size());
+  if (R.ns_environ && *R.ns_environ != environ) *R.ns_environ = environ;  // (Rtc::ns_environ)
   hiprtcProgram prog;
   if (R.create(&prog, src.c_str(), "rt0_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
     err = "hiprtcCreateProgram failed";

@@ -1,6 +1,7 @@
 """A/B timing of the C4 workload's kernel under profiling-only macros
 (RT0_JIT_EXTRA) and constant overrides, to see where its time goes.
-usage: python scripts/exp_c4.py [size] [spp] [causes]"""
+usage: python scripts/exp_c4.py [size] [spp] [causes]
+(the "causes" probes need the probe source: scripts/probes.sh python scripts/exp_c4.py 1024 8 causes)"""
 import os
 import sys
 

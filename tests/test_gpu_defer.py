@@ -90,8 +90,9 @@ def test_deferred_walks_match_inline_models(cfgs, gpu_required):
     lights, the 81,920-triangle model): deferred light sampling hands each
     call's two triangle occlusion queries (the visibility ray and the picked
     light's shadow ray) to rt0_jit_walk, whose lanes take the next query as
-    soon as theirs is answered, and rt0_jit_fin completes the calls
-    (rt0_integrator.h restir_split, walk_body, fin_body).  Against the
+    soon as theirs is answered, and rt0_jit_resolve completes the calls
+    through the tagged result entries (rt0_integrator.h restir_split,
+    walk_body, resolve_body).  Against the
     inline calls of the same 6-pass chain: same answers, so the same
     tolerance as above."""
     import test_models as T
@@ -142,3 +143,41 @@ def test_deferred_walks_viewport_models(cfgs, gpu_required):
     outside = np.ones(s1.shape[1:3], bool)
     outside[vp[1]:vp[1] + vp[3], vp[0]:vp[0] + vp[2]] = False
     assert not s1[:, outside, :3].any()
+
+
+@pytest.mark.gpu
+def test_deferred_buffers_follow_bounce_count(cfgs, gpu_required):
+    """One context renders the whole image at the fixture's MAX_BOUNCES, then
+    a 16x16 tile at MAX_BOUNCES 12: fewer record slots but more result planes
+    (one per call index, nee_out).  The tile must equal a fresh context's
+    render of it -- the buffers are re-sized for the plane count, not only for
+    the slot count (an out-of-bounds write before)."""
+    import ctypes
+    cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
+    vp = (24, 24, 16, 16)
+
+    def deep(r):
+        c = r.get_config()
+        assert c.max_bounces < 12
+        c.max_bounces = 12
+        r.set_config(c)
+
+    r = rt0.Renderer(64, 64)
+    configure(r, cfg, cfgs)
+    r.render(1, 1)
+    deep(r)
+    r.set_viewport(*vp)
+    r.clear()
+    for k in (1, 2):
+        r.render(k, 1)
+    got = r.read_accum()
+    f = rt0.Renderer(64, 64)
+    configure(f, cfg, cfgs)
+    deep(f)
+    f.set_viewport(*vp)
+    for k in (1, 2):
+        f.render(k, 1)
+    want = f.read_accum()
+    assert np.isfinite(got).all()
+    assert np.array_equal(got, want)
+    assert got[vp[1]:vp[1] + 16, vp[0]:vp[0] + 16, :3].any()

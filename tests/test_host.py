@@ -167,32 +167,28 @@ def test_bench_flop_model_matches_survey():
     assert 4650 < fps < 4760
 
 
-def test_jit_walk_module_for_model_scenes(cfgs, tmp_path):
+def test_jit_walk_module_for_model_scenes(cfgs, tmp_path, monkeypatch):
     """A ReSTIR scene with triangle models gets the occlusion-walk kernel
     (rt0_jit_walk) in its module, and with 16-bit stack entries
     (RT0_BVH_STACK16, the C5 tree's 24-entry stack) the traversal stacks take
     2 B of LDS per entry: 256 x 24 x 2 B per workgroup.  Built with hipRTC,
-    no device; rt0_render selects the same key from the built tree.  The
-    compile runs in a fresh process: in this container hipRTC has been seen
-    to crash on a second in-process compile whose source sets RT0_BVH_STACK
-    (a model scene after another scene; the GPU boxes compile such sequences
-    in the GPU suite without trouble)."""
+    no device; rt0_render selects the same key from the built tree.  Runs in
+    this process after other compiles, with the environment changed in
+    between: hipRTC's private link namespace has its own libc, whose
+    `environ` rt0_jit.cpp re-points at every compile (it used to crash here,
+    reading the array os.environ had freed)."""
     import glob
     import re
     import subprocess
-    import sys
-    child = (
-        "import sys, os; sys.path[:0] = sys.argv[1:3]\n"
-        "import oracle as O, rt0\n"
-        "cfgs = O.load_configs()\n"
-        "cfg = next(c for c in cfgs['configs'] if c['name'] == 'c5_spectral_models')\n"
-        "scene, sdf = rt0.scene_strings(cfg, cfgs)\n"
-        "rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))\n")
-    env = dict(os.environ, RT0_JIT_DUMP=str(tmp_path / "k"), RT0_BVH_STACK16="1", RT0_JIT_STACK="24")
-    here = os.path.dirname(os.path.abspath(__file__))
-    paths = [os.path.join(here, "..", "raytracer-0_amd"), os.path.join(here, "..", "oracle")]
-    r = subprocess.run([sys.executable, "-c", child] + paths, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
+    cfg = next(c for c in cfgs["configs"] if c["name"] == "c5_spectral_models")
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))  # a first compile, default key
+    monkeypatch.setenv("RT0_JIT_DUMP", str(tmp_path / "k"))
+    monkeypatch.setenv("RT0_BVH_STACK16", "1")
+    monkeypatch.setenv("RT0_JIT_STACK", "24")
+    for i in range(64):  # grow the environment so its array is reallocated
+        monkeypatch.setenv("RT0_TEST_PAD_%d" % i, "x" * 64)
+    rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))
     co = sorted(glob.glob(str(tmp_path / "k_*.co")))[-1]
     notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True,
                            text=True).stdout
