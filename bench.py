@@ -138,27 +138,50 @@ def cpu_baseline_js(wl, budget_s=10.0):
     tests/test_cpu_js.py) on node worker_threads, timed on a bounded sample of
     the same workload: a 64-row band through the image centre, successive
     passes until the time budget (ReSTIR workloads: the band's passes run
-    the reservoir chain, the rest of the planes stays empty)."""
+    the reservoir chain, the rest of the planes stays empty).  Workloads with
+    triangle models: the JS integrator tests every triangle per ray (like the
+    C restatement; the reference has no triangle path), so the sample is a
+    16-row x 64-column patch at the image centre."""
     import shutil
+    import tempfile
     node = shutil.which("node")
     if node is None:
         return None
     threads = host_threads()
     W, H = wl["width"], wl["height"]
-    r0 = H // 2 - 32
-    r = subprocess.run([node, os.path.join(HERE, "oracle", "js", "cpu_bench.js"),
-                        os.path.join(HERE, "tests", "golden", "configs.json"), wl["fixture"], str(W), str(H),
-                        str(threads), "restir-bench" if wl.get("defines", {}).get("USE_RESTIR") else "bench",
-                        str(r0), str(r0 + 64), str(budget_s)]
-                       + (["--constants", json.dumps(wl["constants"])]),
-                       capture_output=True, text=True, timeout=budget_s * 10 + 60)
+    r0, rows, extra, what = H // 2 - 32, 64, [], ""
+    tmp = None
+    if wl.get("models"):
+        import numpy as np
+        sys.path.insert(0, os.path.join(HERE, "oracle"))
+        import oracle as O
+        from rt0 import meshes, workloads
+        inst = workloads.model_instances(wl)
+        soup = [meshes.world_triangles(v, t, pos, scale) for v, t, pos, scale, _ in inst]
+        owners = np.concatenate([np.full(len(x), i[4], np.int32) for x, i in zip(soup, inst)])
+        tmp = tempfile.mkdtemp(prefix="rt0_js_")
+        O.write_tris(os.path.join(tmp, "tris.bin"), np.concatenate(soup), owners)
+        r0, rows = H // 2 - 8, 16
+        x0 = W // 2 - 32
+        extra = ["--tris", os.path.join(tmp, "tris.bin"), "--xspan", str(x0), str(x0 + 64)]
+        what = ", columns %d..%d, brute force over all %d triangles per ray" % (x0, x0 + 63, len(owners))
+    try:
+        r = subprocess.run([node, os.path.join(HERE, "oracle", "js", "cpu_bench.js"),
+                            os.path.join(HERE, "tests", "golden", "configs.json"), wl["fixture"], str(W), str(H),
+                            str(threads), "restir-bench" if wl.get("defines", {}).get("USE_RESTIR") else "bench",
+                            str(r0), str(r0 + rows), str(budget_s)]
+                           + (["--constants", json.dumps(wl["constants"])]) + extra,
+                           capture_output=True, text=True, timeout=budget_s * 10 + 60)
+    finally:
+        if tmp:
+            shutil.rmtree(tmp, ignore_errors=True)
     if r.returncode != 0:
         return {"error": r.stderr[-300:]}
     d = json.loads(r.stdout)
     return {"value": d["msamples_s"], "unit": "Msamples/s", "cores": d["threads"], "kind": "port",
             "sample": "oracle/js/rt0_cpu.js (JS CPU integrator, node %s worker_threads x%d, %s): rows %d..%d of "
-                      "the %dx%d bench image, successive passes, %d samples in %.1f s"
-                      % (d["node"], d["threads"], d["cpu"], r0, r0 + 63, W, H, d["samples"], d["seconds"])}
+                      "the %dx%d bench image%s, successive passes, %d samples in %.1f s"
+                      % (d["node"], d["threads"], d["cpu"], r0, r0 + rows - 1, W, H, what, d["samples"], d["seconds"])}
 
 
 def cpu_baseline_c(wl, budget_s=8.0):
@@ -212,17 +235,23 @@ class ClockSampler:
         import glob
         self.path, self.err, self.mhz = None, None, []
         try:
-            bus = torch.cuda.get_device_properties(local).pci_bus_id
+            props = torch.cuda.get_device_properties(local)
+            bus, dom = int(props.pci_bus_id), int(getattr(props, "pci_domain_id", 0))
         except Exception as e:  # noqa: BLE001 -- reported, not fatal
-            bus, self.err = None, "no pci_bus_id: %s" % e
+            bus, dom, self.err = None, None, "no pci_bus_id: %s" % e
         if bus is not None:
+            # the device directory is named by its PCI address, DDDD:BB:DD.F (hex)
             for cand in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
-                dev = os.path.basename(os.path.realpath(os.path.dirname(cand))).lower()
-                if dev.endswith(str(bus).lower()[-7:]) or dev == str(bus).lower():
-                    self.path = cand
-                    break
+                addr = os.path.basename(os.path.realpath(os.path.dirname(cand)))
+                parts = addr.replace(".", ":").split(":")
+                try:
+                    if len(parts) == 4 and int(parts[1], 16) == bus and int(parts[0], 16) == dom:
+                        self.path = cand
+                        break
+                except ValueError:
+                    continue
             if self.path is None:
-                self.err = "no pp_dpm_sclk for PCI %s" % bus
+                self.err = "no pp_dpm_sclk for PCI %04x:%02x" % (dom, bus)
         self._stop = None
         self._th = None
 
@@ -669,16 +698,13 @@ def main():
         torch.cuda.synchronize()
         out[key] = round(W * H * sec["spp"] * args.steps / (time.perf_counter() - t1) / 1e6, 3)
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-        # the JS integrator covers quadrics, SDFs, media, MIS and ReSTIR
-        # (SURVEY 8d's C1-C4 feature sets), not spectral rendering or triangle models
-        js_gap = "triangle models and spectral rendering" if wl.get("models") else None
-        js = None if js_gap else cpu_baseline_js(wl)
+        # the JS integrator covers every BASELINE workload's features
+        # (quadrics, SDFs, media, MIS, ReSTIR, spectral, triangle models)
+        js = cpu_baseline_js(wl)
         c_port = cpu_baseline_c(wl)
         out["cpu_baseline"] = js if js and "value" in js else c_port
-        out["cpu_baseline_c"] = c_port  # the C oracle on the same sample (OpenMP)
-        if js_gap:
-            out["cpu_baseline_js_skipped"] = "the JS CPU integrator has no %s: the C restatement is the baseline" % js_gap
-        elif js and "error" in js:
+        out["cpu_baseline_c"] = c_port  # the C oracle on the same workload (OpenMP)
+        if js and "error" in js:
             out["cpu_baseline_js_error"] = js["error"][-160:]
     print(json.dumps(out), flush=True)
     if dist:

@@ -146,6 +146,67 @@ def swiftshader_dir(threads):
     return d
 
 
+# ---- executor path records (tiled configs with "paths": true) ----
+# Textual instrumentation of the expanded reference shader: globals written in
+# radiance()'s bounce loop body (raytracer.glsl:1994-2102) record, per lane,
+# the iterations the loop body ran, the depth at each (base 16), the way each
+# iteration ended (base 8: 1 scatter `continue`, 2 miss `break`, 3 light hit,
+# 4 mask cut-off, 5 bounce caps, 6 scatter cap, 7 end of body) and
+# SCATTERING_EVENTS; main() writes them to the reservoir MRTs, which a
+# non-ReSTIR shader leaves at zero (2220-2223).  Writes in the loop body are
+# masked like the body itself (mask_kat.py rule 1), so they show what the
+# executor ran.  FragColor is untouched; run_tiled keeps a pixel only if the
+# instrumented image equals the plain one bit for bit.
+PATH_EV = {1: "S", 2: "m", 3: "L", 4: "k", 5: "T", 6: "X", 7: "."}
+
+
+def instrument_paths(src):
+    def sub(old, new):
+        nonlocal src
+        assert src.count(old) == 1, old
+        src = src.replace(old, new)
+    sub("vec3 radiance(Ray r, float seed){", "float g_pit = 0.0; float g_ph = 0.0; float g_pev = 0.0;\n"
+        "vec3 radiance(Ray r, float seed){")
+    sub("  for (int depth = 0; depth < MAX_BOUNCES; ++depth){\n",
+        "  for (int depth = 0; depth < MAX_BOUNCES; ++depth){\n    g_pit += 1.0; g_ph = g_ph * 16.0 + float(depth);\n")
+    sub("max(mask.r, max(mask.g, mask.b)) < 0.01) break;\n            continue;",
+        "max(mask.r, max(mask.g, mask.b)) < 0.01) { g_pev = g_pev * 8.0 + 6.0; break; }\n"
+        "            g_pev = g_pev * 8.0 + 1.0;\n            continue;")
+    sub("      if(!bounceIsSpecular && sample_lights) break;",
+        "      if(!bounceIsSpecular && sample_lights) { g_pev = g_pev * 8.0 + 2.0; break; }")
+    sub("#endif\n\n      break;\n    }", "#endif\n      g_pev = g_pev * 8.0 + 2.0;\n      break;\n    }")
+    sub("      acc += mask * e * misWeight;\n      break;",
+        "      acc += mask * e * misWeight;\n      g_pev = g_pev * 8.0 + 3.0;\n      break;")
+    sub("    if(max(mask.x, max(mask.y, mask.z)) < 0.01) break;",
+        "    if(max(mask.x, max(mask.y, mask.z)) < 0.01) { g_pev = g_pev * 8.0 + 4.0; break; }")
+    sub("SCATTERING_EVENTS >= MAX_SCATTERING_EVENTS ) break;\n  }",
+        "SCATTERING_EVENTS >= MAX_SCATTERING_EVENTS ) { g_pev = g_pev * 8.0 + 5.0; break; }\n"
+        "    g_pev = g_pev * 8.0 + 7.0;\n  }")
+    sub("    ReSTIRData = vec4(0.0);\n    ReSTIRAux = vec4(0.0);",
+        "    ReSTIRData = vec4(g_pit, g_ph, float(SCATTERING_EVENTS), float(DIFF_BOUNCES));\n"
+        "    ReSTIRAux = vec4(g_pev, float(TRANS_BOUNCES), 0.0, float(SPEC_BOUNCES));")
+    return src
+
+
+def path_conformance(cfg, cfgs, exec_paths, exec_aux):
+    """GLSL-semantics path records of the restatement (oracle/rt0_oracle.c
+    RT0_DEBUG_PATHS: the same fields, the same encodings) and the lanes whose
+    executor record equals them: iterations, depth history, exit events and
+    scattering events all the same."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import oracle as O
+    F, Hh, Ww = exec_paths.shape[:3]
+    o = O.Oracle(cfg, cfgs, width=Ww, height=Hh, overrides={"SWIFTSHADER_GHOST": 1, "RT0_DEBUG_PATHS": 1})
+    ref_p, ref_a = [], []
+    for k in range(1, F + 1):
+        _, m, a = o.frame(k)
+        ref_p.append(m)
+        ref_a.append(a)
+    ref_p, ref_a = np.stack(ref_p), np.stack(ref_a)
+    return ((exec_paths[..., 0] == ref_p[..., 0]) & (exec_paths[..., 1] == ref_p[..., 1]) &
+            (exec_paths[..., 2] == ref_p[..., 2]) & (exec_aux[..., 0] == ref_a[..., 0]))
+
+
 def run_tiled(cfg, cmd, prefix, W, H, restir, defs, consts):
     """Tiled mode (deep volumetric configs): every (u_frame, tile) is its own
     glrun call with glScissor on the tile and a time limit, run once per
@@ -161,16 +222,31 @@ def run_tiled(cfg, cmd, prefix, W, H, restir, defs, consts):
     tcs = cfg.get("thread_counts", [1, 3])
     dirs = {t: swiftshader_dir(t) for t in tcs}
     jobs = [(k, x, y) for k in range(1, frames + 1) for y in range(0, H, th) for x in range(0, W, tw)]
+    paths = bool(cfg.get("paths")) and not restir
+    # with path records, the FIRST thread count runs the instrumented shader
+    # (its image must equal the plain runs' bit for bit to be kept)
+    pcmd = list(cmd)
+    if paths:
+        fi = cmd.index("--frag") + 1
+        ifrag = cmd[fi][:-len(".frag")] + "_paths.frag"
+        with open(ifrag, "w") as f:
+            f.write(instrument_paths(open(cmd[fi]).read()))
+        pcmd[fi] = ifrag
+        pcmd.append("--restir-out")
 
     def run(k, x, y, t):
         out = "%s_k%d_x%d_y%d_t%d" % (prefix, k, x, y, t)
+        instr = paths and t == tcs[0]
         try:
-            subprocess.run(cmd + ["--frames", "1", "--frame0", str(k), "--scissor", str(x), str(y), str(tw), str(th),
-                                  "--out", out], check=True, capture_output=True, cwd=dirs[t],
-                           timeout=float(cfg["tile_timeout"]))
+            subprocess.run((pcmd if instr else cmd) + ["--frames", "1", "--frame0", str(k), "--scissor", str(x), str(y),
+                                                      str(tw), str(th), "--out", out], check=True,
+                           capture_output=True, cwd=dirs[t], timeout=float(cfg["tile_timeout"]))
         except subprocess.TimeoutExpired:
             return None
         img = {"c": np.fromfile("%s_f%d_c.bin" % (out, k), dtype=np.float32).reshape(H, W, 4)}
+        if instr:
+            for tag in "ra":
+                img["p" + tag] = np.fromfile("%s_f%d_%s.bin" % (out, k, tag), dtype=np.float32).reshape(H, W, 4)
         if restir:
             for tag in "ra":
                 img[tag] = np.fromfile("%s_f%d_%s.bin" % (out, k, tag), dtype=np.float32).reshape(H, W, 4)
@@ -196,6 +272,8 @@ def run_tiled(cfg, cmd, prefix, W, H, restir, defs, consts):
     samples = np.zeros((frames, H, W, 4), np.float32)
     valid = np.zeros((frames, H, W), bool)
     aux = {tag: np.zeros((frames, H, W, 4), np.float32) for tag in ("ra" if restir else "")}
+    if paths:
+        aux.update({tag: np.zeros((frames, H, W, 4), np.float32) for tag in ("pr", "pa")})
     timed_out = 0
     for (k, x, y), imgs in results:
         sl = (k - 1, slice(y, y + th), slice(x, x + tw))
@@ -215,9 +293,17 @@ def run_tiled(cfg, cmd, prefix, W, H, restir, defs, consts):
     if restir:
         out["restir_main"], out["restir_aux"] = aux["r"], aux["a"]
     name = cfg["name"]
+    extra = {}
+    if paths:
+        # exec_paths: iterations, depth history, SCATTERING_EVENTS, DIFF_BOUNCES;
+        # exec_exits: exit events, TRANS_BOUNCES, 0, SPEC_BOUNCES (instrument_paths)
+        out["exec_paths"], out["exec_exits"] = aux["pr"], aux["pa"]
+        conf = path_conformance(cfg, json.load(open(os.path.join(GOLD, "configs.json"))), aux["pr"], aux["pa"])
+        out["conformant"] = conf & valid
+        extra = {"paths": True, "conformant_pixel_samples": int(out["conformant"].sum())}
     np.savez_compressed(os.path.join(GOLD, name + ".npz"), **out)
     v = samples[..., :3][valid]
-    return {"defines": defs, "constants": consts, "frames": list(range(1, frames + 1)), "width": W, "height": H,
+    return {**extra, "defines": defs, "constants": consts, "frames": list(range(1, frames + 1)), "width": W, "height": H,
             "restir": restir, "tiles": [tw, th], "thread_counts": tcs, "tiles_timed_out": timed_out,
             "tile_jobs": len(jobs), "valid_pixel_samples": int(valid.sum()),
             "nan_pixels": int(np.isnan(v).any(-1).sum()) if v.size else 0,

@@ -58,6 +58,25 @@ executor being thread-count dependent): shaders whose GLSL ES
      (inscatter_two_lights): the two-light departure is rule 8 (a scatter's
      `continue` precedes every in-scatter loop of a later bounce).
 
+QUAD CONTINUE (json key "quad_continue"; 2x2 images, ThreadCount=1): the
+reference's bounce loop reduced to its control flow (radiance(),
+raytracer.glsl:1994-2102 with intersection(), brdf() and the light loop cut
+away -- each cut kept the effect on the reference shader's own quads):
+depth-indexed `continue`s from the scatter block (2050, after its
+SCATTERING_EVENTS cap `break`, 2049), then a bounce update and the caps
+`break` (2100-2101).  Each lane has its own set of iterations that take the
+`continue`; the executor's loop-exit histories per lane:
+ 10. a lane that takes the `continue` in the loop's FIRST iteration is retired
+     there unless it is the quad's first lane (x, y even); with that lane not
+     covered (a scissor / primitive edge) every lane goes on.  Continues in
+     later iterations are honoured.  (continue_then_break above, a
+     different body, retires lane 0 too: the rule depends on the code shape,
+     so this case follows the reference's.)
+Measured on the reference shader itself (make_golden.py instrument_paths):
+this rule is one of several departures in its volumetric loop -- others make
+a lane repeat depth 0, and about a third of 2x2 quads never finish -- so the
+fixture keeps executor path records and marks the lanes that run as GLSL says.
+
 usage: python3 oracle/gen/mask_kat.py
 """
 import json
@@ -399,6 +418,91 @@ DEPARTURES = {
 }
 
 
+QUAD_LOOP = """
+struct Ray { vec3 o; vec3 d; };
+struct Hit { vec3 pos; vec3 n; };
+lowp int SCATTERING_EVENTS = 0;
+lowp int DIFF_BOUNCES = 0;
+const lowp int MAX_BOUNCES = 12;
+const lowp int MAX_SCATTERING_EVENTS = 12;
+float g_it = 0.0; float g_h = 0.0; float g_ev = 0.0;
+vec3 radiance(Ray r, float seed) {
+  vec3 acc = vec3(0.);
+  int lane = (int(gl_FragCoord.x) & 1) + 2 * (int(gl_FragCoord.y) & 1);
+  int cm = lane == 0 ? %d : lane == 1 ? %d : lane == 2 ? %d : %d;
+  for (int depth = 0; depth < MAX_BOUNCES; ++depth) {
+    g_it += 1.0; g_h = g_h * 16.0 + float(depth);
+    Hit hit;
+    float t = 2.0; hit.pos = r.o + t * r.d; hit.n = vec3(0.0, 1.0, 0.0);
+    {
+      float scatter_d = ((cm >> depth) & 1) != 0 ? 0.0 : 100.0;
+      if (scatter_d < t) {
+        r = Ray(r.o + scatter_d * r.d, normalize(r.d + vec3(0.1, 0.2, 0.3)));
+        ++SCATTERING_EVENTS;
+        if (SCATTERING_EVENTS >= MAX_SCATTERING_EVENTS) { g_ev = g_ev * 8.0 + 6.0; break; }
+        g_ev = g_ev * 8.0 + 1.0;
+        continue;
+      }
+    }
+    r.o = hit.pos + hit.n * 0.001; r.d = reflect(r.d, hit.n); ++DIFF_BOUNCES;
+    if (depth >= 5) { g_ev = g_ev * 8.0 + 5.0; break; }
+    g_ev = g_ev * 8.0 + 7.0;
+  }
+  return acc;
+}
+void main() {
+  vec3 a = radiance(Ray(vec3(0.0), vec3(0.0, 0.0, -1.0)), 0.5);
+  FragColor = vec4(a, 0.0);
+  ReSTIRData = vec4(g_it, g_ev, float(SCATTERING_EVENTS), float(DIFF_BOUNCES));
+  ReSTIRAux = vec4(0.0);
+}
+"""
+QUAD_EV = {1: "S", 5: "T", 6: "X", 7: "."}
+# (continue masks of lanes 0..3 over depth, covered lanes as a scissor x y w h or None)
+QUAD_CASES = [((cm0, cm1, cm2, cm3), cov)
+              for cov in (None, (0, 0, 2, 1), (1, 0, 1, 2), (0, 1, 2, 1))
+              for (cm0, cm1, cm2, cm3) in ((1, 1, 1, 1), (3, 1, 0, 0), (1, 3, 2, 0), (0, 1, 1, 1), (2, 2, 6, 5),
+                                           (0, 0, 0, 0), (5, 1, 9, 3))]
+
+
+def quad_glsl(cm):
+    """GLSL ES 3.00 exit history of QUAD_LOOP for a lane with continue mask cm."""
+    ev = ""
+    for d in range(12):
+        if (cm >> d) & 1:
+            ev += "S"
+            continue
+        if d >= 5:
+            return ev + "T"
+        ev += "."
+    return ev
+
+
+def run_quad(cms, cov, cwd):
+    frag = os.path.join(GEN, "quad_%s_%s.frag" % ("_".join(map(str, cms)), "all" if cov is None else "_".join(map(str, cov))))
+    with open(frag, "w") as f:
+        f.write(HEAD + QUAD_LOOP % tuple(cms))
+    prefix = frag[:-5]
+    cmd = [GLRUN, "--frag", frag, "--w", "2", "--h", "2", "--frames", "1", "--single", "--restir-out", "--out", prefix]
+    if cov is not None:
+        cmd += ["--scissor"] + [str(v) for v in cov]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, text=True, cwd=cwd, timeout=30)
+    except subprocess.TimeoutExpired:  # the executor did not finish the quad
+        return [{"lane": lane, "covered": None, "exec": "HANG", "glsl": quad_glsl(cms[lane])} for lane in range(4)]
+    c = np.fromfile("%s_f1_r.bin" % prefix, dtype=np.float32).reshape(2, 2, 4)[..., 1:]
+    out = []
+    for lane in range(4):
+        x, y = lane & 1, lane >> 1
+        covered = cov is None or (cov[0] <= x < cov[0] + cov[2] and cov[1] <= y < cov[1] + cov[3])
+        v, ev = int(round(float(c[y, x, 0]))) if covered else 0, ""
+        while v:
+            ev = QUAD_EV.get(v % 8, "?") + ev
+            v //= 8
+        out.append({"lane": lane, "covered": covered, "exec": ev if covered else None, "glsl": quad_glsl(cms[lane])})
+    return out
+
+
 def run_case(name, body, cwd=None):
     frag = os.path.join(GEN, name + ".frag")
     with open(frag, "w") as f:
@@ -438,6 +542,11 @@ def main():
                                    for r in rows]
         bad = sum(1 for r in out["departures"][name] if r["exec"] != r["glsl"])
         print("%s: %d of %d pixels depart from GLSL semantics" % (name, bad, len(rows)))
+    out["quad_continue"] = []
+    for cms, cov in QUAD_CASES:
+        rows = run_quad(cms, cov, t1)
+        out["quad_continue"].append({"cms": list(cms), "cov": list(cov) if cov else None, "lanes": rows})
+        print("quad_continue cms %s cov %s: %s" % (cms, cov, [r["exec"] for r in rows]))
     with open(os.path.join(REPO, "tests", "golden", "mask_kat.json"), "w") as f:
         json.dump(out, f, separators=(",", ":"))
 

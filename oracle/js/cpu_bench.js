@@ -18,6 +18,10 @@
 //                                          chain after each, until the deadline
 // ReSTIR modes keep the eight reservoir planes in SharedArrayBuffers; the
 // threads render one pass's rows each and meet between passes.
+// Options: --constants JSON (constant overrides); --tris FILE (the world-space
+// triangles of the config's TRIANGLE entries: int32 n, n x 9 f32 vertices,
+// n int32 owners, as bench.py / tests write them); --xspan X0 X1 (columns of
+// each row to render in the bench modes: a bounded sample of costly scenes).
 const os = require('os');
 const fs = require('fs');
 const path = require('path');
@@ -29,7 +33,16 @@ function makeRenderer(d) {
   const cfg = cfgs.configs.find((c) => c.name === d.config);
   if (!cfg) throw new Error('no config ' + d.config);
   if (d.constants) cfg.constants = Object.assign({}, cfg.constants || {}, d.constants);
-  return new CpuRenderer(cfg, cfgs.cornell_lines, cfgs.default_camera, d.W, d.H);
+  const r = new CpuRenderer(cfg, cfgs.cornell_lines, cfgs.default_camera, d.W, d.H);
+  if (d.tris) {
+    const b = fs.readFileSync(d.tris);
+    const n = b.readInt32LE(0);
+    const v9 = new Float32Array(b.buffer.slice(b.byteOffset + 4, b.byteOffset + 4 + 36 * n));
+    const own = new Int32Array(b.buffer.slice(b.byteOffset + 4 + 36 * n, b.byteOffset + 4 + 40 * n));
+    r.setTriangles(v9, own);
+  }
+  if (d.xspan) [r.x0, r.x1] = d.xspan;
+  return r;
 }
 
 // plane roles of the swap chain: [out main, out aux, back, back aux, hist1, hist1 aux, hist2, hist2 aux]
@@ -47,7 +60,7 @@ if (!isMainThread && workerData.mode && workerData.mode.startsWith('restir')) {
     const k = msg.roles;
     r.tex = [planes[k[2]], planes[k[3]], planes[k[4]], planes[k[5]], planes[k[6]], planes[k[7]]];
     r.renderPass(msg.frame, d.y0, d.y1, sample, planes[k[0]], planes[k[1]]);
-    parentPort.postMessage({ done: true, samples: (d.y1 - d.y0) * d.W });
+    parentPort.postMessage({ done: true, samples: (d.y1 - d.y0) * (d.xspan ? d.xspan[1] - d.xspan[0] : d.W) });
   });
 } else if (!isMainThread) {
   const d = workerData;
@@ -69,6 +82,11 @@ if (!isMainThread && workerData.mode && workerData.mode.startsWith('restir')) {
   const base = { configs: path.resolve(a[0]), config: a[1], W: +a[2], H: +a[3] };
   const ci = a.indexOf('--constants');  // optional JSON of constant overrides (bench workloads)
   if (ci >= 0) base.constants = JSON.parse(a[ci + 1]);
+  const ti = a.indexOf('--tris');
+  if (ti >= 0) base.tris = path.resolve(a[ti + 1]);
+  const xi = a.indexOf('--xspan');
+  if (xi >= 0) base.xspan = [+a[xi + 1], +a[xi + 2]];
+  const cols = base.xspan ? base.xspan[1] - base.xspan[0] : base.W;
   const threads = +a[4] || os.cpus().length;
   const mode = a[5];
   const split = (y0, y1) => {
@@ -131,7 +149,7 @@ if (!isMainThread && workerData.mode && workerData.mode.startsWith('restir')) {
     restir(y0, y1, 1 << 30, seconds, null).then((res) => {
       console.log(JSON.stringify({
         samples: res.samples, seconds: res.seconds, msamples_s: res.samples / res.seconds / 1e6, threads: res.threads,
-        passes: Math.round(res.samples / ((y1 - y0) * base.W)), cpu: os.cpus()[0].model, node: process.version,
+        passes: Math.round(res.samples / ((y1 - y0) * cols)), cpu: os.cpus()[0].model, node: process.version,
       }));
     }).catch((e) => { console.error(e); process.exit(1); });
   } else if (mode === 'image') {

@@ -14,12 +14,16 @@
 // configs -- planes, spheres, boxes, SDFs (every #sdf_meshes kind, sphere-traced
 // with calcNormal), every untextured material, sky, plain NEE, MIS, SDF lights,
 // homogeneous volumetrics (free-flight sampling, in-scatter NEE, HG phase, fog
-// transmittance), and ReSTIR in RENDER_MODE 0 (sampleLightsReSTIR with its
+// transmittance), ReSTIR in RENDER_MODE 0 (sampleLightsReSTIR with its
 // candidates, two-level temporal history, spatial taps, finalize, MRT packing:
 // renderPass() takes the six reservoir input planes and writes the two MRTs,
-// the caller runs index.js's swap chain), under GLSL semantics.  Spectral,
-// animated-mode, cubemap and texture configs are rejected (the C oracle covers
-// them).
+// the caller runs index.js's swap chain), spectral rendering (the hero
+// wavelength, Cauchy IOR of the MAT_SPECTRAL_* materials and the CIE fit,
+// 322-359, 1819-1824, 2153-2155) and TRIANGLE models (setTriangles: the
+// commented-out Moller-Trumbore iTriangle of 864-892 over every triangle, as
+// the C restatement runs it -- the reference has no triangle path at all),
+// under GLSL semantics.  Animated-mode, cubemap and texture configs are
+// rejected (the C oracle covers them).
 const f = Math.fround;
 
 // ------------------------------------------------------------------ RNG
@@ -149,7 +153,7 @@ function sampleHG(w, seed) {
 }
 
 // ------------------------------------------------------- scene grammar
-const T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_SDF = 3;
+const T_SPHERE = 0, T_PLANE = 1, T_BOX = 2, T_SDF = 3, T_TRIANGLE = 5;
 const M_LIGHT = 0, M_DIR_LIGHT = 1, M_DIFF = 2, M_SPEC = 3, M_REFR_FRESNEL = 4, M_REFR_SCHLICK = 5, M_COAT = 6;
 // Material table, raytracer.glsl:165-224 ([c, e, nt, type]; textured ones omitted)
 const MATS = {
@@ -178,8 +182,36 @@ const MATS = {
   MAT_COAT_NAVY: [[0, 0, 0.50196078431], [1, 1, 1], 1.4, M_COAT],
   MAT_COAT_PURPLE: [[0.50196078431, 0, 0.50196078431], [0, 0, 0], 1.4, M_COAT],
   MAT_COAT_WAX: [[0.9333, 0.6666, 0.6], [0.005, 0.005, 0.005], 1.4, M_COAT],
+  // spectral materials: nt < 0 = Cauchy A (220-224), dispersive under USE_SPECTRAL
+  MAT_SPECTRAL_FLINT: [[1, 1, 1], [0, 0, 0], -1.7167, M_REFR_FRESNEL],
+  MAT_SPECTRAL_DIAMOND: [[1, 1, 1], [0, 0, 0], -2.3991, M_REFR_FRESNEL],
 };
-const TYPES = { SPHERE: T_SPHERE, PLANE: T_PLANE, BOX: T_BOX, SDF: T_SDF };
+const TYPES = { SPHERE: T_SPHERE, PLANE: T_PLANE, BOX: T_BOX, SDF: T_SDF, TRIANGLE: T_TRIANGLE };
+
+// spectral rendering: Cauchy IOR (357) and the CIE 1931 fit -> sRGB (324-353)
+function spectralIOR(lambda, A) {
+  const lu = f(lambda * f(0.001));
+  return f(A + f(f(0.04) / f(lu * lu)));
+}
+const fexp = (x) => f(Math.exp(x));
+function lobe(l, c, lo, hi) { const t = f(f(l - c) * (l < c ? lo : hi)); return fexp(f(f(-0.5 * t) * t)); }
+function cmfX(l) {
+  return f(f(f(f(0.362) * lobe(l, f(442.0), f(0.0624), f(0.0374))) + f(f(1.056) * lobe(l, f(599.8), f(0.0264), f(0.0323))))
+    - f(f(0.065) * lobe(l, f(501.1), f(0.0490), f(0.0382))));
+}
+function cmfY(l) {
+  return f(f(f(0.821) * lobe(l, f(568.8), f(0.0213), f(0.0247))) + f(f(0.286) * lobe(l, f(530.9), f(0.0613), f(0.0322))));
+}
+function cmfZ(l) {
+  return f(f(f(1.217) * lobe(l, f(437.0), f(0.0845), f(0.0278))) + f(f(0.681) * lobe(l, f(459.0), f(0.0385), f(0.0725))));
+}
+function wavelengthToRGB(l) {
+  const X = cmfX(l), Y = cmfY(l), Z = cmfZ(l);
+  const r = f(f(f(f(3.2404542) * X) - f(f(1.5371385) * Y)) - f(f(0.4985314) * Z));
+  const g = f(f(f(f(-0.9692660) * X) + f(f(1.8760108) * Y)) + f(f(0.0415560) * Z));
+  const b = f(f(f(f(0.0556434) * X) - f(f(0.2040259) * Y)) + f(f(1.0572252) * Z));
+  return V(f(gmax(0, r) / f(0.378)), f(gmax(0, g) / f(0.298)), f(gmax(0, b) / f(0.285)));
+}
 
 // parse "vecN(a, b, ...)" with GLSL scalar broadcast
 function parseVec(s, n) {
@@ -207,13 +239,14 @@ function parseScene(lines) {
     });
   });
   if (lights.length === 0) lights.push(-1);
-  // meshes[NUM_MESHES + i] addresses SDF i: the SDF lines follow the quadrics
-  let nMeshes = meshes.length;
-  meshes.forEach((m, i) => {
-    if (m.t === T_SDF && nMeshes === meshes.length) nMeshes = i;
-    else if (m.t !== T_SDF && nMeshes < meshes.length) throw new Error('SDF meshes must follow the quadrics');
-  });
-  return { meshes, lights, nMeshes };
+  // meshes[NUM_MESHES + i] addresses SDF i: the SDF lines follow the quadrics,
+  // and the TRIANGLE entries (model instances) follow the SDFs
+  const rank = (t) => (t === T_SDF ? 1 : t === T_TRIANGLE ? 2 : 0);
+  for (let i = 1; i < meshes.length; i++)
+    if (rank(meshes[i].t) < rank(meshes[i - 1].t)) throw new Error('SDF meshes must follow the quadrics, TRIANGLE entries the SDFs');
+  const nMeshes = meshes.filter((m) => rank(m.t) === 0).length;
+  const nSdf = meshes.filter((m) => m.t === T_SDF).length;
+  return { meshes, lights, nMeshes, nSdf };
 }
 
 // ------------------------------------------------- ReSTIR (1264-1801)
@@ -254,8 +287,9 @@ class CpuRenderer {
   // cfg: a tests/golden/configs.json entry; cornell: cfgs.cornell_lines; camera default
   constructor(cfg, cornellLines, defaultCamera, width, height) {
     const defs = Object.assign({ USE_PROCEDURAL_SKY: true, USE_BIASED_SAMPLING: true }, cfg.defines || {});
-    for (const k of ['USE_SPECTRAL', 'USE_CUBEMAP'])
-      if (defs[k]) throw new Error(k + ' is outside the JS baseline');
+    if (defs.USE_CUBEMAP) throw new Error('USE_CUBEMAP is outside the JS baseline');
+    this.spectral = !!defs.USE_SPECTRAL;
+    this.hero = f(550);
     const c = Object.assign({
       MAX_BOUNCES: 12, MAX_DIFF_BOUNCES: 4, MAX_SPEC_BOUNCES: 4, MAX_TRANS_BOUNCES: 12, MAX_SCATTERING_EVENTS: 12,
       sample_lights: true, use_mis: false, use_restir: false, MARCHING_STEPS: 128, FUDGE_FACTOR: 0.9,
@@ -274,7 +308,9 @@ class CpuRenderer {
     this.sampleLights = !!c.sample_lights; this.mis = !!c.use_mis;
     const sc = parseScene(cfg.scene_lines || cornellLines);
     this.meshes = sc.meshes; this.lights = sc.lights;
-    this.nMeshes = sc.nMeshes; this.nSdf = sc.meshes.length - sc.nMeshes;
+    this.nMeshes = sc.nMeshes; this.nSdf = sc.nSdf;
+    this.nModels = sc.meshes.length - sc.nMeshes - sc.nSdf;
+    this.nTris = 0;  // setTriangles
     this.sdfKinds = Array.from({ length: this.nSdf }, (_, i) => ((cfg.sdf_kinds || [])[i] || 0));
     this.vol = !!defs.USE_VOLUMETRICS;
     this.marchSteps = c.MARCHING_STEPS; this.fudge = f(c.FUDGE_FACTOR);
@@ -285,6 +321,41 @@ class CpuRenderer {
     this.camParams = V(f(cam.fov), f(cam.aperture), f(cam.focalLength));
     this.nIsect = 0;
     this.nMap = 0;
+  }
+
+  // World-space triangles of the TRIANGLE entries: v9 = n x 9 floats (three
+  // vertices), model = owner entry k | (back-face culling, opts[3]) << 30 --
+  // the same soup the C restatement takes (or_set_triangles).
+  setTriangles(v9, model) {
+    const n = model.length;
+    this.nTris = n;
+    this.tri = new Float32Array(n * 13);  // v1, e0, e1, eps, cull
+    this.triModel = Int32Array.from(model);
+    for (let i = 0; i < n; i++) {
+      const q = 9 * i, v1 = V(f(v9[q]), f(v9[q + 1]), f(v9[q + 2]));
+      const e0 = sub(V(f(v9[q + 3]), f(v9[q + 4]), f(v9[q + 5])), v1), e1 = sub(V(f(v9[q + 6]), f(v9[q + 7]), f(v9[q + 8])), v1);
+      const eps = f(f(EPS * f(Math.sqrt(dot(e0, e0)))) * f(Math.sqrt(dot(e1, e1))));
+      this.tri.set([v1.x, v1.y, v1.z, e0.x, e0.y, e0.z, e1.x, e1.y, e1.z, eps, (model[i] >> 30) & 1], 13 * i);
+    }
+  }
+  // iTriangle (864-892, Moller-Trumbore) with the restatement's size-relative
+  // parallel-ray threshold (oracle/rt0_oracle.c iTriangle): t in (EPS, tmin) or -1
+  triHit(i, o, d, tmin) {
+    const T = this.tri, b = 13 * i;
+    const e0x = T[b + 3], e0y = T[b + 4], e0z = T[b + 5], e1x = T[b + 6], e1y = T[b + 7], e1z = T[b + 8];
+    const hx = f(f(d.y * e1z) - f(d.z * e1y)), hy = f(f(d.z * e1x) - f(d.x * e1z)), hz = f(f(d.x * e1y) - f(d.y * e1x));
+    const a = f(f(f(e0x * hx) + f(e0y * hy)) + f(e0z * hz));
+    const eps = T[b + 9];
+    if (T[b + 10] ? a < eps : (a > -eps && a < eps)) return -1;
+    const fa = f(1 / a);
+    const sx = f(o.x - T[b]), sy = f(o.y - T[b + 1]), sz = f(o.z - T[b + 2]);
+    const u = f(fa * f(f(f(sx * hx) + f(sy * hy)) + f(sz * hz)));
+    if (u < 0 || u > 1) return -1;
+    const qx = f(f(sy * e0z) - f(sz * e0y)), qy = f(f(sz * e0x) - f(sx * e0z)), qz = f(f(sx * e0y) - f(sy * e0x));
+    const v = f(fa * f(f(f(d.x * qx) + f(d.y * qy)) + f(d.z * qz)));
+    if (v < 0 || f(u + v) > 1) return -1;
+    const t = f(fa * f(f(f(e1x * qx) + f(e1y * qy)) + f(e1z * qz)));
+    return t > EPS && t < tmin ? t : -1;
   }
 
   // map(), raytracer.glsl:700-712 (+ the #sdf_meshes statements, index.html:702-717) -> [d, id]
@@ -362,6 +433,20 @@ class CpuRenderer {
           step(dd.x, dd.z) * step(dd.y, dd.z));
         n = normalize(mul(s, st));
         tmin = t; type = T_BOX; index = i;
+      }
+    }
+    if (this.nModels > 0) {  // every triangle, lowest index wins ties (strict <)
+      if (this.nTris === 0) throw new Error('TRIANGLE entries without setTriangles');
+      let best = -1;
+      for (let i = 0; i < this.nTris; i++) {
+        const t = this.triHit(i, o, d, tmin);
+        if (t >= 0) { tmin = t; best = i; }
+      }
+      if (best >= 0) {
+        const T = this.tri, b = 13 * best;
+        n = normalize(cross(V(T[b + 3], T[b + 4], T[b + 5]), V(T[b + 6], T[b + 7], T[b + 8])));
+        index = this.nMeshes + this.nSdf + (this.triModel[best] & 0x3fffffff);
+        type = T_TRIANGLE;
       }
     }
     if (this.nSdf > 0) {  // iSDF, 974-993
@@ -711,7 +796,9 @@ class CpuRenderer {
       const x = hit.pos, nl = prevNl, bounce = f(depth);
       const rdir = this.randomDirection(nl, f(f(f(seed + f(f(7.1) * fr)) + f(5681.123)) + f(bounce * f(92.13))));
       const rough = mul(e, rdir);
-      const nc = f(1.00029), nt = Math.abs(m.nt), mt = m.mt;
+      const nc = f(1.00029), mt = m.mt;
+      // USE_SPECTRAL: a negative IOR is Cauchy's A at the hero wavelength (1819-1824)
+      const nt = this.spectral && m.nt < 0 ? spectralIOR(this.hero, Math.abs(m.nt)) : Math.abs(m.nt);
       if (mt === M_DIFF) {
         ro = add(x, muls(nl, EPS)); rd = rdir; mask = mul(mask, c); diffB++; spec = false;
       } else if (mt === M_SPEC) {
@@ -808,6 +895,7 @@ class CpuRenderer {
     this.fr = EMPTY_RES();
     const stx = f(f(f(2 * fcx) / rx) - 1), sty = f(f(f(2 * fcy) / ry) - 1);
     const seed = hash(f(f(f(fcx * f(12.9898)) + f(fcy * f(78.233))) + f(f(1113.1) * f(frame))));
+    this.hero = this.spectral ? f(f(hash(f(seed + f(4821.73))) * 340) + 380) : f(550);  // 2123
     const uVLen = f(Math.tan(f(f(this.camParams.x * RAD) * 0.5)));
     const uULen = f(f(rx / ry) * uVLen);
     const w = normalize(this.camLook);
@@ -823,7 +911,8 @@ class CpuRenderer {
     const ang = f(hash(f(seed + f(496.4562))) * TWO_PI);
     const rad = f(hash(f(seed + f(249.1686))) * this.camParams.y);
     const ap = muls(add(muls(u, fcos(ang)), muls(v, fsin(ang))), rad);
-    return this.radiance(add(this.camPos, ap), normalize(sub(fp, ap)), seed, frame);
+    const col = this.radiance(add(this.camPos, ap), normalize(sub(fp, ap)), seed, frame);
+    return this.spectral ? mul(col, wavelengthToRGB(this.hero)) : col;  // 2152-2155
   }
 
   // One ReSTIR pass over rows [y0, y1): sample[y][x] = that pass's sample
@@ -832,8 +921,9 @@ class CpuRenderer {
   // Float32Arrays, rows bottom-up, or null for zeros).
   renderPass(frame, y0, y1, sample, main, aux) {
     const len1 = this.lights.length > 1 ? this.lights.length : 1;
+    const x0 = this.x0 || 0, x1 = this.x1 || this.w;  // column span (bench samples of costly scenes)
     for (let y = y0; y < y1; y++) {
-      for (let x = 0; x < this.w; x++) {
+      for (let x = x0; x < x1; x++) {
         const s = this.sample(x, y, frame), p = (y * this.w + x) * 4, r = this.fr, have = this.restirDef;
         sample[p] = s.x; sample[p + 1] = s.y; sample[p + 2] = s.z; sample[p + 3] = 0;
         main[p] = have ? r.pos.x : 0; main[p + 1] = have ? r.pos.y : 0; main[p + 2] = have ? r.pos.z : 0;
@@ -863,4 +953,4 @@ class CpuRenderer {
   }
 }
 
-module.exports = { CpuRenderer, hash, hash2, parseScene };
+module.exports = { CpuRenderer, hash, hash2, parseScene, wavelengthToRGB, spectralIOR };

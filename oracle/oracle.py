@@ -200,3 +200,15 @@ def hash2(x, y):
 
 def pixel_seed(fx, fy, frame):
     return lib().or_pixel_seed(fx, fy, frame)
+
+
+def write_tris(path, v9, owners):
+    """The triangle soup of oracle/js/cpu_bench.js --tris: int32 n, n x 9
+    float32 world-space vertices, n int32 owners (entry k | cull bit 30)."""
+    v = np.ascontiguousarray(v9, np.float32).reshape(-1, 9)
+    m = np.ascontiguousarray(owners, np.int32).reshape(-1)
+    with open(path, "wb") as f:
+        f.write(np.int32(len(m)).tobytes())
+        f.write(v.tobytes())
+        f.write(m.tobytes())
+

@@ -147,25 +147,24 @@ def test_deferred_walks_viewport_models(cfgs, gpu_required):
 
 @pytest.mark.gpu
 def test_deferred_buffers_follow_bounce_count(cfgs, gpu_required):
-    """One context renders the whole image at the fixture's MAX_BOUNCES, then
-    a 16x16 tile at MAX_BOUNCES 12: fewer record slots but more result planes
-    (one per call index, nee_out).  The tile must equal a fresh context's
-    render of it -- the buffers are re-sized for the plane count, not only for
-    the slot count (an out-of-bounds write before)."""
-    import ctypes
+    """One context renders the whole image at MAX_BOUNCES 2, then a 16x16
+    tile at MAX_BOUNCES 12: fewer record slots but more result planes (one
+    per call index, nee_out).  The tile must equal a fresh context's render
+    of it -- the buffers are re-sized for the plane count, not only for the
+    slot count (an out-of-bounds write before)."""
     cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
     vp = (24, 24, 16, 16)
 
-    def deep(r):
+    def bounces(r, n):
         c = r.get_config()
-        assert c.max_bounces < 12
-        c.max_bounces = 12
+        c.max_bounces = n
         r.set_config(c)
 
     r = rt0.Renderer(64, 64)
     configure(r, cfg, cfgs)
+    bounces(r, 2)
     r.render(1, 1)
-    deep(r)
+    bounces(r, 12)
     r.set_viewport(*vp)
     r.clear()
     for k in (1, 2):
@@ -173,7 +172,7 @@ def test_deferred_buffers_follow_bounce_count(cfgs, gpu_required):
     got = r.read_accum()
     f = rt0.Renderer(64, 64)
     configure(f, cfg, cfgs)
-    deep(f)
+    bounces(f, 12)
     f.set_viewport(*vp)
     for k in (1, 2):
         f.render(k, 1)
