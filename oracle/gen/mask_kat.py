@@ -69,9 +69,12 @@ SCATTERING_EVENTS cap `break`, 2049), then a bounce update and the caps
  10. a lane that takes the `continue` in the loop's FIRST iteration is retired
      there unless it is the quad's first lane (x, y even); with that lane not
      covered (a scissor / primitive edge) every lane goes on.  Continues in
-     later iterations are honoured.  (continue_then_break above, a
-     different body, retires lane 0 too: the rule depends on the code shape,
-     so this case follows the reference's.)
+     later iterations are honoured.  About a third of these quads never
+     finish (HANG, a 30 s limit; which ones depends on the code around the
+     loop: the same masks finished in a copy without the KAT header's
+     helpers).  (continue_then_break above, a different body, retires lane 0
+     too: the rule depends on the code shape, so this case follows the
+     reference's.)
 Measured on the reference shader itself (make_golden.py instrument_paths):
 this rule is one of several departures in its volumetric loop -- others make
 a lane repeat depth 0, and about a third of 2x2 quads never finish -- so the

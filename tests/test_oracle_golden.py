@@ -282,12 +282,20 @@ def test_mask_kat_quad_continue():
     """Rule 10 (mask_kat.py QUAD CONTINUE): in the reference's bounce-loop
     shape, a lane that takes the scatter `continue` in the loop's first
     iteration is retired -- unless it is the quad's first lane or that lane is
-    not covered -- and later continues are honoured."""
+    not covered -- and later continues are honoured.  Some of these quads
+    never finish (recorded as HANG: the executor spins in the loop, as in the
+    deep volumetric fixture's timed-out tiles); every quad that finishes
+    follows the rule."""
     Q = json.load(open(os.path.join(GOLD, "mask_kat.json")))["quad_continue"]
     assert len(Q) >= 20
-    retired = 0
+    retired = finished = hangs = 0
     for case in Q:
         lanes = case["lanes"]
+        if lanes[0]["exec"] == "HANG":
+            assert all(r["exec"] == "HANG" for r in lanes)
+            hangs += 1
+            continue
+        finished += 1
         lane0 = lanes[0]["covered"]
         for r in lanes:
             if not r["covered"]:
@@ -297,7 +305,11 @@ def test_mask_kat_quad_continue():
             retire = (cm & 1) == 1 and r["lane"] != 0 and lane0
             retired += retire
             assert r["exec"] == ("S" if retire else r["glsl"]), (case["cms"], case["cov"], r)
-    assert retired >= 10
+    assert finished >= 15 and retired >= 8 and hangs >= 1, (finished, retired, hangs)
+    # a quad where no covered lane continues in the first iteration runs as GLSL says
+    calm = [c for c in Q if c["lanes"][0]["exec"] != "HANG"
+            and not any(r["covered"] and c["cms"][r["lane"]] & 1 for r in c["lanes"])]
+    assert calm and all(r["exec"] in (None, r["glsl"]) for c in calm for r in c["lanes"])
 
 
 def _res_match(a, b):
