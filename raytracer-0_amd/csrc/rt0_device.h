@@ -90,14 +90,17 @@ struct BvhNode {
 struct NeeRec {
   float x, y, z;     // the shading point (hit.pos)
   float nx, ny, nz;  // nl
-  float sx, sy;      // sampleLightsReSTIR's two seeds (raytracer.glsl:1909/1943)
   float mr, mg, mb;  // the path's mask at the call
   int32_t pix;       // image pixel (y * W + x)
-  int32_t mat;       // the hit mesh (material of the shading point)
-  int32_t k;         // the call's index along the path (0-based)
-  int32_t pad;
+  uint32_t mkb;      // the hit mesh (material) | the call's index along the path << 8 | the bounce << 16
+  uint32_t pad;
+  // sampleLightsReSTIR's two seeds (raytracer.glsl:1909/1943) are recomputed
+  // from the pixel, the pass and the bounce (Integrator::restir_seeds)
+  __host__ __device__ int mat() const { return (int)(mkb & 0xffu); }
+  __host__ __device__ int k() const { return (int)((mkb >> 8) & 0xffu); }
+  __host__ __device__ int bounce() const { return (int)(mkb >> 16); }
 };
-static_assert(sizeof(NeeRec) == 60, "NeeRec is 15 words");
+static_assert(sizeof(NeeRec) == 48, "NeeRec is 12 words: three 16-B loads");
 
 // RT0_NEE_WALK (scenes with triangle models): a light-sampling call's
 // triangle occlusion queries go to rt0_jit_walk as WalkJobs, 32 B: the ray
