@@ -105,9 +105,6 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_NEE_WALK  // light-sampling calls' triangle occlusion queries in rt0_jit_walk (models scenes)
 #define RT0_NEE_WALK 0
 #endif
-#ifndef RT0_PK_GEOM  // A/B: intersection()'s plane and box pairs in packed FP32 (v_pk_*), scene-specialised kernels
-#define RT0_PK_GEOM 0
-#endif
 #ifndef RT0_BVH_STACK16  // BVH traversal stacks as 16-bit LDS entries + high bits in a register
 #define RT0_BVH_STACK16 0
 #endif
@@ -247,33 +244,11 @@ struct Hit {
 #ifndef RT0_MARCH_BUDGET
 #define RT0_MARCH_BUDGET 8
 #endif
-// RT0_MARCH_POOL 1: the pending marches of a whole workgroup are marched by
-// its first ceil(n/64) waves (pass_body's regen_pixel_pool), not by the lanes
-// that own them
-#ifndef RT0_MARCH_POOL
-#define RT0_MARCH_POOL 1
-#endif
 
 struct March {
   v3 o, d;
   float tmin, t, id;
   int i;
-  bool active, done;
-};
-// RT0_WALK_POOL (deferred ReSTIR pass kernels of scenes with triangle models):
-// a path's closest-hit BVH query is handed to the workgroup's walk pool like
-// a march (pass_body's walk rounds); `done` hands (best, tmin) back to
-// intersection(), which the caller repeats with the same ray
-#ifndef RT0_WALK_POOL
-#define RT0_WALK_POOL 0
-#endif
-#ifndef RT0_WALK_BUDGET  // BVH nodes per pooled walk slice
-#define RT0_WALK_BUDGET 8
-#endif
-struct Walk {
-  v3 o, d;
-  float tmin;
-  int best;
   bool active, done;
 };
 
@@ -385,25 +360,16 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
 // (the index's low half) and the high bits of every entry in one 64-bit
 // register -- 2 B of LDS per entry instead of 4, so the stack no longer caps
 // the waves per CU.  Pushed entries are inner nodes (>= 0).
-#if RT0_BVH_STACK16
-DEV uint16_t *bvh_stack_base() {
-  __shared__ uint16_t stk_base[RT0_BVH_STACK * 256];
-  return stk_base;
-}
-#else
-DEV int32_t *bvh_stack_base() {
-  __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
-  return stk_base;
-}
-#endif
 struct BvhStack {
 #if RT0_BVH_STACK16
   static constexpr int HB = 64 / RT0_BVH_STACK;
   static constexpr uint64_t HM = (1ull << HB) - 1ull;
   uint16_t *s;
   uint64_t hb = 0;
-  DEV BvhStack() { s = bvh_stack_base() + threadIdx.x; }
-  DEV explicit BvhStack(uint32_t slot) { s = bvh_stack_base() + slot; }  // a pooled walk's stack
+  DEV BvhStack() {
+    __shared__ uint16_t stk_base[RT0_BVH_STACK * 256];
+    s = stk_base + threadIdx.x;
+  }
   DEV void put(int sp, int v) {
     s[256 * sp] = (uint16_t)v;
     hb = (hb & ~(HM << (HB * sp))) | ((uint64_t)((uint32_t)v >> 16) << (HB * sp));
@@ -411,8 +377,10 @@ struct BvhStack {
   DEV int get(int sp) const { return (int)((uint32_t)s[256 * sp] | ((uint32_t)((hb >> (HB * sp)) & HM) << 16)); }
 #else
   int32_t *s;
-  DEV BvhStack() { s = bvh_stack_base() + threadIdx.x; }
-  DEV explicit BvhStack(uint32_t slot) { s = bvh_stack_base() + slot; }
+  DEV BvhStack() {
+    __shared__ int32_t stk_base[RT0_BVH_STACK * 256];
+    s = stk_base + threadIdx.x;
+  }
   DEV void put(int sp, int v) { s[256 * sp] = v; }
   DEV int get(int sp) const { return s[256 * sp]; }
 #endif
@@ -596,76 +564,6 @@ struct Geometry {
     return -1;
   }
 
-#if RT0_PK_GEOM
-  // Two consecutive meshes i, i+1 of a static scene that are both
-  // axis-aligned planes or both boxes, tested as one packed pair (v_pk_*_f32:
-  // two lanes' worth of FP32 per instruction); the arithmetic per mesh is
-  // prim()'s, candidate t with the bound INF_T (the caller reduces in index
-  // order: t < bound separates from every test).  false = not a packable pair.
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  template <class Cfg>
-  static DEV bool prim_pair(const Scene &sc, int i, v3 o, v3 m, v3 mo, float &t0, float &t1, int &ty0, int &ty1) {
-    const GeomRec a = sc.geom(i), b = sc.geom(i + 1);
-    if (a.j0 == 0.0f || b.j0 == 0.0f || a.type != b.type) return false;
-    if (a.type == T_PLANE) {
-      const int ax0 = axis_of(mk(a.px, a.py, a.pz)), ax1 = axis_of(mk(b.px, b.py, b.pz));
-      if (ax0 < 0 || ax1 < 0) return false;
-      auto pick = [](v3 v, int ax) { return ax == 0 ? v.x : (ax == 1 ? v.y : v.z); };
-      const f2 s = {pick(mk(a.px, a.py, a.pz), ax0), pick(mk(b.px, b.py, b.pz), ax1)};
-      const f2 oa = {pick(o, ax0), pick(o, ax1)}, ma = {pick(m, ax0), pick(m, ax1)};
-      const f2 d0 = {a.d0, b.d0};
-      const f2 t = (d0 - s * oa) * (s * ma);
-      t0 = t.x;
-      t1 = t.y;
-      ty0 = t0 > EPSILON ? (int)T_PLANE : -1;  // (t < bound: the caller's reduction)
-      ty1 = t1 > EPSILON ? (int)T_PLANE : -1;
-      return true;
-    }
-    if (a.type == T_BOX) {
-      const f2 gx = {a.px, b.px}, gy = {a.py, b.py}, gz = {a.pz, b.pz}, hd = {a.d0, b.d0};
-      const f2 nx = __builtin_elementwise_fma(f2{m.x, m.x}, gx, -f2{mo.x, mo.x});
-      const f2 ny = __builtin_elementwise_fma(f2{m.y, m.y}, gy, -f2{mo.y, mo.y});
-      const f2 nz = __builtin_elementwise_fma(f2{m.z, m.z}, gz, -f2{mo.z, mo.z});
-      const f2 kx = f2{fabsf(m.x), fabsf(m.x)} * hd, ky = f2{fabsf(m.y), fabsf(m.y)} * hd,
-               kz = f2{fabsf(m.z), fabsf(m.z)} * hd;
-      const f2 ax = nx - kx, bx = nx + kx, ay = ny - ky, by = ny + ky, az = nz - kz, bz = nz + kz;
-      const float tN0 = fmaxf(fmaxf(ax.x, ay.x), az.x), tF0 = fminf(fminf(bx.x, by.x), bz.x);
-      const float tN1 = fmaxf(fmaxf(ax.y, ay.y), az.y), tF1 = fminf(fminf(bx.y, by.y), bz.y);
-      t0 = (tN0 > 0.0f) ? tN0 : tF0;
-      t1 = (tN1 > 0.0f) ? tN1 : tF1;
-      ty0 = !(tN0 > tF0 || tF0 < 0.0f) && !(t0 < EPSILON) ? (int)T_BOX : -1;
-      ty1 = !(tN1 > tF1 || tF1 < 0.0f) && !(t1 < EPSILON) ? (int)T_BOX : -1;
-      return true;
-    }
-    return false;
-  }
-  // the closest-hit mesh loop of intersection() over packed pairs (0,1), (2,3), ...
-  template <int I, class Cfg>
-  static DEV void mesh_pairs(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, v3 m, v3 mo,
-                             float &tmin, int &type, int &index) {
-    if constexpr (I < Scene::kMeshes) {
-      auto take = [&](int k, float t, int ty) {
-        const bool ok = ty >= 0 && t < tmin;
-        tmin = ok ? t : tmin;
-        type = ok ? ty : type;
-        index = ok ? k : index;
-      };
-      float t0, t1;
-      int ty0, ty1;
-      if (I + 1 < Scene::kMeshes && prim_pair<Cfg>(sc, I, o, m, mo, t0, t1, ty0, ty1)) {
-        take(I, t0, ty0);
-        take(I + 1, t1, ty1);
-        mesh_pairs<I + 2, Cfg>(P, sc, C, o, d, m, mo, tmin, type, index);
-      } else {
-        float t;
-        const int ty = prim<Cfg>(P, sc, C, I, o, d, m, mo, tmin, t);
-        take(I, t, ty);
-        mesh_pairs<I + 1, Cfg>(P, sc, C, o, d, m, mo, tmin, type, index);
-      }
-    }
-  }
-#endif
-
   // intersection() as calcDirectLighting's shadow ray reads it (raytracer.glsl:
   // 1189-1196): only "is the closest hit a LIGHT, and which one" -- for
   // scene-specialised quadric scenes.  The closest hit of intersection() is the
@@ -761,8 +659,7 @@ struct Geometry {
   // recomputes the quadric tests (deterministic) and completes the hit.
   template <bool SDF, class Cfg>
   static DEV float intersect(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, Hit &hit,
-                             unsigned long long &nmap, March *ms = nullptr, unsigned long long *nbvh = nullptr,
-                             Walk *wk = nullptr) {
+                             unsigned long long &nmap, March *ms = nullptr, unsigned long long *nbvh = nullptr) {
     hit.n = mk(0.f, 0.f, 0.f);
     hit.index = 0;
     int type = -1;
@@ -775,11 +672,6 @@ struct Geometry {
     // waits on another lane's taken branch inside the mesh loop.  The box
     // normal of iBox (853-856) depends only on the winning box and its t, so
     // it is evaluated once after the loop for the winner.
-#if RT0_PK_GEOM
-    if constexpr (Scene::kStatic) {
-      mesh_pairs<0, Cfg>(P, sc, C, o, d, m, mo, tmin, type, hit.index);
-    } else
-#endif
     for_meshes(sc, [&](int i) {
       float t;
       const int ty = prim<Cfg>(P, sc, C, i, o, d, m, mo, tmin, t);
@@ -790,19 +682,7 @@ struct Geometry {
     });
     if constexpr (Scene::kMayHaveModels) {  // TRIANGLE models (after the quadrics, before the SDF march)
       if (sc.n_models() > 0 && P.n_tris > 0) {
-        int ti;
-        if (wk) {  // the workgroup's walk pool answers the query (RT0_WALK_POOL)
-          if (wk->active) return -1.0f;
-          if (!wk->done) {
-            *wk = Walk{o, d, tmin, -2, true, false};  // best -2: not yet in the pool
-            return -1.0f;
-          }
-          ti = wk->best;
-          tmin = wk->tmin;
-          wk->done = false;
-        } else {
-          ti = bvh_closest(P, o, d, m, tmin, nbvh);
-        }
+        const int ti = bvh_closest(P, o, d, m, tmin, nbvh);
         if (ti >= 0) {
           const TriDev T = P.tris[ti];
           const v3 e0 = mk(T.e0x, T.e0y, T.e0z), e1 = mk(T.e1x, T.e1y, T.e1z);
@@ -1297,9 +1177,9 @@ struct Integrator {
   // getAnimatedPosition (RENDER_MODE 1); the static position otherwise
   DEV v3 lpos(int i, const GeomRec &g) const { return flag(F_ANIM) ? anim_pos(P, i) : mk(g.px, g.py, g.pz); }
 
-  DEV float isect(v3 o, v3 d, Hit &h, March *ms = nullptr, Walk *wk = nullptr) {
+  DEV float isect(v3 o, v3 d, Hit &h, March *ms = nullptr) {
     if (COUNT) ++n_isect;
-    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map, ms, COUNT ? n_bvh : nullptr, wk);
+    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map, ms, COUNT ? n_bvh : nullptr);
   }
 
   // mix(mesh.mat.c, hit.texel.rgb, hit.texel.a) of a shadow ray's light hit
@@ -2082,15 +1962,7 @@ struct Integrator {
     int phase;  // SUSP only
     March ms;
     NeeCtx nc;
-    Walk wk;  // WSUSP only
   };
-  // deferred ReSTIR pass kernels of model scenes: closest-hit walks pooled (pass_body)
-  static constexpr bool WSUSP = RT0_WALK_POOL && RT0_DEFER_NEE && RESTIR && !SDF && !COUNT && Scene::kMayHaveModels;
-  DEV Walk *walk_slot(Path &ps) {
-    if constexpr (!WSUSP) return nullptr;
-    if (!(sc.n_models() > 0 && P.n_tris > 0)) return nullptr;
-    return &ps.wk;
-  }
   DEV March *march_slot(Path &ps) {
     if constexpr (!SUSP) return nullptr;
     // with triangle models the resumed call would walk the BVH again: no budget
@@ -2226,8 +2098,8 @@ struct Integrator {
     {
     if (COUNT) ++n_iter;
     Hit hit;
-    float t = isect(ro, rd, hit, march_slot(ps), walk_slot(ps));
-    if ((SUSP || WSUSP) && t < 0.0f) return true;  // march / walk pending: step() repeats this bounce once it is done
+    float t = isect(ro, rd, hit, march_slot(ps));
+    if (SUSP && t < 0.0f) return true;  // march pending: step() repeats this bounce once it is done
     if constexpr (VOL) {
       if (flag(F_VOL)) {
         float sd = -flog(fmaxf(hash(nc_addmul(seed + 4729.3f, (float)depth, 991.1f)), 1e-6f)) / VOL_SIGMA_T;
@@ -2590,239 +2462,6 @@ DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int 
   P.accum[apix] = a;
 }
 
-// Path regeneration with the workgroup's marches pooled (SUSP kernels,
-// RT0_MARCH_POOL): each round, every lane runs one bounce step of its own path
-// (or starts its next pass), then every march still pending in the workgroup
-// -- whichever ray it belongs to: camera, bounce, shadow, in-scatter -- is
-// listed in LDS and marched RT0_MARCH_BUDGET steps by threads 0..n-1, i.e. by
-// the first ceil(n/64) waves on full lanes while the others skip the slice,
-// instead of by its own lane beside 63 lanes that wait (C4 lanes were 26%
-// busy).  The steps are march_pending's, map() for map(): the same sequence of
-// evaluations per ray, so the image is bit-identical.  Every thread of the
-// workgroup, inside the viewport or not, runs the rounds until no thread has
-// work left (a workgroup-uniform exit: the loop holds barriers).
-template <class It, class Cfg>
-DEV void regen_pixel_pool(const LaunchParams &P, It &it, const Cfg &cfg, int px, int py, size_t apix, bool inside) {
-  __shared__ float pl_ox[256], pl_oy[256], pl_oz[256], pl_dx[256], pl_dy[256], pl_dz[256];
-  __shared__ float pl_tmin[256], pl_t[256], pl_id[256];
-  __shared__ int pl_i[256];
-  __shared__ uint16_t pl_list[256];
-  __shared__ uint32_t pl_wcnt[4];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  float4 a = inside ? P.accum[apix] : make_float4(0.f, 0.f, 0.f, 0.f);
-  typename It::Path ps;
-  ps.ms.active = false;
-  ps.ms.done = false;
-  int f = 0;
-  bool finished = !inside || P.nframes <= 0, alive = false;
-  if (!finished) {
-    it.frame = P.frame0;
-    it.begin(ps, px, py);
-    alive = cfg.max_bounces() > 0;
-  }
-  const int cap = cfg.marching_steps();
-  while (true) {
-    if (!finished) {
-      // a lane whose march is still pending skips step() (its bounce resumes once it is done)
-      if (alive && !ps.ms.active) alive = it.step(ps);
-      if (!alive) {
-        accumulate(it, P, a, it.finish(ps));
-        if (++f >= P.nframes) {
-          finished = true;
-        } else {
-          it.frame = P.frame0 + (uint32_t)f;
-          it.begin(ps, px, py);
-          alive = cfg.max_bounces() > 0;
-        }
-      }
-    }
-    const bool want = !finished && ps.ms.active;
-    if (want) {
-      pl_ox[tid] = ps.ms.o.x;
-      pl_oy[tid] = ps.ms.o.y;
-      pl_oz[tid] = ps.ms.o.z;
-      pl_dx[tid] = ps.ms.d.x;
-      pl_dy[tid] = ps.ms.d.y;
-      pl_dz[tid] = ps.ms.d.z;
-      pl_tmin[tid] = ps.ms.tmin;
-      pl_t[tid] = ps.ms.t;
-      pl_id[tid] = ps.ms.id;
-      pl_i[tid] = ps.ms.i;
-    }
-    const uint64_t b = __ballot(want);
-    if (lane == 0) pl_wcnt[wave] = (uint32_t)__popcll(b);
-    __syncthreads();
-    uint32_t base = 0, n = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < 4; ++w) {
-      const uint32_t c = pl_wcnt[w];
-      base += w < wave ? c : 0u;
-      n += c;
-    }
-    if (want) pl_list[base + (uint32_t)__popcll(b & lt)] = (uint16_t)tid;
-    __syncthreads();
-    if (tid < n) {  // march_pending's loop, on the listed slot
-      const uint32_t q = pl_list[tid];
-      const v3 o = mk(pl_ox[q], pl_oy[q], pl_oz[q]), d = mk(pl_dx[q], pl_dy[q], pl_dz[q]);
-      const float tmin = pl_tmin[q];
-      float t = pl_t[q], id = pl_id[q];
-      int i = pl_i[q];
-      const int lim = min(cap, i + RT0_MARCH_BUDGET);
-      bool stop = i >= cap;
-      for (; i < lim; ++i) {
-        float dist = It::G::map(it.sc, o + d * t, id, it.n_map);
-        float h = fabsf(dist);
-        if (h < EPSILON || t > tmin) {
-          stop = true;
-          break;
-        }
-        t += h * cfg.fudge();
-      }
-      if (i >= cap) stop = true;
-      pl_t[q] = t;
-      pl_id[q] = id;
-      pl_i[q] = stop ? (i | (int)0x80000000) : i;
-    }
-    __syncthreads();
-    if (want) {
-      const int iv = pl_i[tid];
-      ps.ms.t = pl_t[tid];
-      ps.ms.id = pl_id[tid];
-      ps.ms.i = iv & 0x7fffffff;
-      if (iv < 0) {
-        ps.ms.active = false;
-        ps.ms.done = true;
-      }
-    }
-    if (__syncthreads_count(finished ? 0 : 1) == 0) break;
-  }
-  if (inside) P.accum[apix] = a;
-}
-
-// RT0_WALK_POOL: the deferred ReSTIR pass of a scene with triangle models,
-// its closest-hit BVH queries pooled over the workgroup.  Each round every
-// lane runs one bounce step of its path; a step that needs the model's
-// closest hit registers the query (Walk) and returns; then every query still
-// open in the workgroup is listed in LDS and walked RT0_WALK_BUDGET nodes by
-// threads 0..n-1 -- bvh_closest's loop body verbatim on the query's own
-// stack slot and state -- so walks run on full waves.  Workgroup-uniform
-// rounds (barriers) until every path has ended.
-template <class It>
-DEV void walk_pool_round(const LaunchParams &P, bool want, typename It::Path &ps) {
-  __shared__ float wk_ox[256], wk_oy[256], wk_oz[256], wk_dx[256], wk_dy[256], wk_dz[256], wk_tmin[256];
-  __shared__ int wk_best[256], wk_node[256], wk_sp[256], wk_guard[256];
-  __shared__ uint32_t wk_hlo[256], wk_hhi[256];
-  __shared__ uint16_t wk_list[256];
-  __shared__ uint32_t wk_wcnt[4];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  if (want && ps.wk.best == -2) {  // a new query: its state goes to the lane's own slot
-    wk_ox[tid] = ps.wk.o.x;
-    wk_oy[tid] = ps.wk.o.y;
-    wk_oz[tid] = ps.wk.o.z;
-    wk_dx[tid] = ps.wk.d.x;
-    wk_dy[tid] = ps.wk.d.y;
-    wk_dz[tid] = ps.wk.d.z;
-    wk_tmin[tid] = ps.wk.tmin;
-    wk_best[tid] = -1;
-    wk_node[tid] = 0;
-    wk_sp[tid] = 0;
-    wk_guard[tid] = 0;
-    wk_hlo[tid] = 0u;
-    wk_hhi[tid] = 0u;
-    ps.wk.best = -1;
-  }
-  const uint64_t b = __ballot(want);
-  if (lane == 0) wk_wcnt[wave] = (uint32_t)__popcll(b);
-  __syncthreads();
-  uint32_t base = 0, n = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < 4; ++w) {
-    const uint32_t c = wk_wcnt[w];
-    base += w < wave ? c : 0u;
-    n += c;
-  }
-  if (want) wk_list[base + (uint32_t)__popcll(b & lt)] = (uint16_t)tid;
-  __syncthreads();
-  if (tid < n) {
-    const uint32_t q = wk_list[tid];
-    const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
-    const TriDev *__restrict__ tris = P.tris;
-    const v3 o = mk(wk_ox[q], wk_oy[q], wk_oz[q]), d = mk(wk_dx[q], wk_dy[q], wk_dz[q]);
-    const v3 inv = mk(frcp(d.x), frcp(d.y), frcp(d.z));
-    float tmin = wk_tmin[q];
-    int best = wk_best[q], node = wk_node[q], sp = wk_sp[q], guard = wk_guard[q];
-    BvhStack stk(q);
-#if RT0_BVH_STACK16
-    stk.hb = (uint64_t)wk_hlo[q] | ((uint64_t)wk_hhi[q] << 32);
-#endif
-    bool done = false;
-    for (int k = 0; k < RT0_WALK_BUDGET; ++k) {  // bvh_closest<false>'s loop body
-      const float4 a = nodes[4 * node], bb = nodes[4 * node + 1], c = nodes[4 * node + 2];
-      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
-      float tl = box_enter(a.x, a.y, a.z, bb.x, bb.y, bb.z, o, inv, tmin);
-      float tr = box_enter(a.w, bb.w, c.x, c.y, c.z, c.w, o, inv, tmin);
-      const int cl = lk.x, cr = lk.y;
-      int l0 = -1, l1 = -1;
-      if (tl != F_INF && cl < 0) {
-        l0 = ~cl;
-        tl = F_INF;
-      }
-      if (tr != F_INF && cr < 0) {
-        if (l0 < 0) l0 = ~cr;
-        else l1 = ~cr;
-        tr = F_INF;
-      }
-      if (l0 >= 0) {
-        float t;
-        if (tri_test(tris[l0], o, d, tmin, t)) {
-          tmin = t;
-          best = l0;
-        }
-        if (l1 >= 0 && tri_test(tris[l1], o, d, tmin, t)) {
-          tmin = t;
-          best = l1;
-        }
-      }
-      if (tl != F_INF && tr != F_INF) {
-        const bool lfirst = tl <= tr;
-        stk.put(sp, lfirst ? cr : cl);
-        sp = min(sp + 1, RT0_BVH_STACK - 1);
-        node = lfirst ? cl : cr;
-      } else if (tl != F_INF) {
-        node = cl;
-      } else if (tr != F_INF) {
-        node = cr;
-      } else if (sp == 0) {
-        done = true;
-      } else {
-        node = stk.get(--sp);
-      }
-      // a ray visits each node at most once: the cap only guarantees that
-      // the rounds end even on a corrupt tree
-      if (++guard > 2 * P.n_tris + 8) done = true;
-      if (done) break;
-    }
-    wk_tmin[q] = tmin;
-    wk_best[q] = best;
-    wk_node[q] = done ? -1 : node;
-    wk_sp[q] = sp;
-    wk_guard[q] = guard;
-#if RT0_BVH_STACK16
-    wk_hlo[q] = (uint32_t)stk.hb;
-    wk_hhi[q] = (uint32_t)(stk.hb >> 32);
-#endif
-  }
-  __syncthreads();
-  if (want && wk_node[tid] < 0) {  // answered: intersection() reads it at the step's repeat
-    ps.wk.tmin = wk_tmin[tid];
-    ps.wk.best = wk_best[tid];
-    ps.wk.active = false;
-    ps.wk.done = true;
-  }
-}
-
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -2830,65 +2469,6 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const int ly = (lane >> 3) + ((wave >> 1) << 3);
   const int px = P.vp_x0 + (int)blockIdx.x * 16 + lx;
   const int r = P.vp_y0 + (int)blockIdx.y * 16 + ly;
-  using ItT = Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>;
-  if constexpr (ItT::WSUSP) {
-    // the deferred pass with pooled closest-hit walks: every thread of the
-    // workgroup takes part in the rounds
-    const bool in_vp = px < P.vp_x1 && r < P.vp_y1;
-    const int py = in_vp ? image_row(P, r) : 0;
-    const bool inside = in_vp && py < P.height;
-    ItT it(P, sc, cfg);
-    const size_t pix = (size_t)py * P.width + px;
-    it.frame = P.frame0;
-    it.nee_pix = (int32_t)pix;
-    it.nee_wave = (blockIdx.y * gridDim.x + blockIdx.x) * 4u + (uint32_t)wave;
-    volatile uint32_t *wc = nee_wave_counter();
-    *wc = 0u;
-    typename ItT::Path ps;
-    ps.wk.active = false;
-    ps.wk.done = false;
-    ps.acc = mk(0.f, 0.f, 0.f);
-    it.hero = 550.0f;
-    it.nee_k = 0;
-    bool alive = false;
-    if (inside) {
-      it.begin(ps, px, py);
-      alive = cfg.max_bounces() > 0;
-    }
-    while (true) {
-      if (alive && !ps.wk.active) alive = it.step(ps);
-      walk_pool_round<ItT>(P, alive && ps.wk.active, ps);
-      if (__syncthreads_count(alive ? 1 : 0) == 0) break;
-    }
-    if (!inside) return;
-    const uint32_t total = *wc;
-    if (lane == __ffsll((long long)__ballot(1)) - 1) P.nee_count[it.nee_wave] = total;
-    P.nee_partial[pix] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, it.hero);
-    P.nee_n[pix] = it.nee_k;
-    if (it.nee_k > 0) return;
-    if (P.rout_main == nullptr || P.rout_aux == nullptr) return;
-    if (it.flag(F_RESTIR_DEF)) {
-      const Res &q = it.fin;
-      P.rout_main[pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
-      P.rout_aux[pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
-    } else {
-      P.rout_main[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
-      P.rout_aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    return;
-  }
-  if constexpr (ItT::SUSP && RT0_MARCH_POOL) {
-    if (!P.samples) {  // every thread of the workgroup takes part in the pooled rounds
-      const bool in_vp = px < P.vp_x1 && r < P.vp_y1;
-      const int py = in_vp ? image_row(P, r) : 0;
-      const bool inside = in_vp && py < P.height;
-      ItT it(P, sc, cfg);
-      const size_t pix = (size_t)py * P.width + px;
-      const size_t apix = P.compact ? (size_t)r * P.width + px : pix;
-      regen_pixel_pool(P, it, cfg, px, py, apix, inside);
-      return;
-    }
-  }
   if (px >= P.vp_x1 || r >= P.vp_y1) return;
   const int py = image_row(P, r);
   if (py >= P.height) return;

@@ -11,7 +11,7 @@ set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=$(mktemp -d)
 cp raytracer-0_amd/csrc/rt0_device.h raytracer-0_amd/csrc/rt0_integrator.h "$T/"
-patch -s -d "$T" -p3 < scripts/probes.patch
+patch -s -d "$T" -p3 < "${PROBES_PATCH:-scripts/probes.patch}"
 cat "$T/rt0_device.h" "$T/rt0_integrator.h" > "$T/rt0_jit_probe.src"
 export RT0_JIT_SOURCE="$T/rt0_jit_probe.src"
 "$@"
