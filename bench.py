@@ -56,7 +56,7 @@ PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
 # profiles/<dir>/ holding the PMC summaries (pmc_<config>.json) of each
 # workload, newest first (scripts/gpu_measure.sh writes them)
-PROFILE_ROUNDS = ("r03", "r02/final")
+PROFILE_ROUNDS = ("r04", "r03", "r02/final")
 BAND = 16
 
 
@@ -227,9 +227,10 @@ class ClockSampler:
     """Samples the GPU's current shader clock during the timed region (the C2
     kernel moves 5.26-5.45 ms with the box's clock, DESIGN 5.00, as much as most
     A/B deltas): the starred level of the amdgpu driver's pp_dpm_sclk for the
-    device's PCI address, read every 10 ms by a host thread (no GPU call).
-    Reports the median and range, or why it could not (the file missing or
-    unreadable for this user)."""
+    device's PCI address, read once right before and once right after the
+    timed region and every 25 ms in between by a host thread (no GPU call; a
+    sysfs read releases the GIL).  Reports the median and range, or why it
+    could not (the file missing or unreadable for this user)."""
 
     def __init__(self, torch, local):
         import glob
@@ -264,18 +265,22 @@ class ClockSampler:
             self.err = "%s: %s" % (self.path, e)
         return None
 
+    def sample(self):
+        if self.path is not None:
+            v = self._read()
+            if v is not None:
+                self.mhz.append(v)
+
     def start(self):
         import threading
         if self.path is None:
             return
+        self.sample()
         self._stop = threading.Event()
 
         def run():
-            while not self._stop.is_set():
-                v = self._read()
-                if v is not None:
-                    self.mhz.append(v)
-                self._stop.wait(0.01)
+            while not self._stop.wait(0.025):
+                self.sample()
         self._th = threading.Thread(target=run, daemon=True)
         self._th.start()
 
@@ -283,13 +288,14 @@ class ClockSampler:
         if self._th is not None:
             self._stop.set()
             self._th.join()
+        self.sample()
 
     def report(self):
         if not self.mhz:
             return {"median_mhz": None, "source": self.path, "error": self.err or "no samples"}
         m = sorted(self.mhz)
         return {"median_mhz": m[len(m) // 2], "min_mhz": m[0], "max_mhz": m[-1], "samples": len(m),
-                "source": self.path + " (current level, sampled every 10 ms over the timed region)"}
+                "source": self.path + " (current level: before, every 25 ms during and after the timed region)"}
 
 
 # ---------------------------------------------------------------- workloads

@@ -69,6 +69,11 @@ DEV v3 refract(v3 i, v3 n, float eta) {
 }
 DEV float fsin(float x) { return __sinf(x); }
 DEV float fcos(float x) { return __cosf(x); }
+// sin/cos(2*pi*t) for t in [0, 1): v_sin/v_cos take revolutions, so the
+// reference's angle = 2*pi*t (and __sinf's x * 1/(2*pi)) is two multiplies the
+// hardware undoes; the argument differs from sin(fl(2*pi*t)) by an ulp
+DEV float fsin_rev(float t) { return __builtin_amdgcn_sinf(t); }
+DEV float fcos_rev(float t) { return __builtin_amdgcn_cosf(t); }
 DEV float fexp(float x) { return __expf(x); }
 DEV float flog(float x) { return __logf(x); }
 
@@ -761,9 +766,9 @@ DEV void calc_binormals(v3 n, v3 &ox, v3 &oz) {
   ox = mk(1.0f + sig * n.x * n.x * a, sig * b, -sig * n.x);
   oz = mk(b, sig + n.y * n.y * a, -n.y);
 }
-DEV v3 frame_dir(v3 w, v3 u, v3 v, float rx, float ry) {
+DEV v3 frame_dir(v3 w, v3 u, v3 v, float rx, float ry) {  // rx: the angle in revolutions
   float om = fsqrt(1.0f - ry * ry);
-  return normalize((u * (fcos(rx) * om) + v * (fsin(rx) * om)) + w * ry);
+  return normalize((u * (fcos_rev(rx) * om) + v * (fsin_rev(rx) * om)) + w * ry);
 }
 // getSampleBiased(w, 1.0, seed), 1109-1120: pow(r.y, 1/2) == sqrt(r.y)
 DEV v3 sample_cosine(v3 w, float seed) {
@@ -771,7 +776,7 @@ DEV v3 sample_cosine(v3 w, float seed) {
   calc_binormals(w, u, v);
   float rx, ry;
   hash2(seed, seed, rx, ry);
-  return frame_dir(w, u, v, rx * TWO_PI, fsqrt(ry));
+  return frame_dir(w, u, v, rx, fsqrt(ry));
 }
 // getConeSample, 1122-1133
 DEV v3 sample_cone(v3 w, float extent, float seed) {
@@ -779,16 +784,14 @@ DEV v3 sample_cone(v3 w, float extent, float seed) {
   calc_binormals(w, u, v);
   float rx, ry;
   hash2(seed, seed, rx, ry);
-  return frame_dir(w, u, v, rx * TWO_PI, 1.0f - ry * extent);
+  return frame_dir(w, u, v, rx, 1.0f - ry * extent);
 }
 // randomSphereDirection, 1143-1147
 DEV v3 random_sphere_dir(float seed) {
   float rx, ry;
   hash2(seed, seed, rx, ry);
-  rx *= TWO_PI;
-  ry *= TWO_PI;
-  float sy = fsin(ry), cy = fcos(ry);
-  return mk(fsin(rx) * sy, fsin(rx) * cy, fcos(rx));
+  float sy = fsin_rev(ry), cy = fcos_rev(ry), sx = fsin_rev(rx);  // angles 2*pi*r
+  return mk(sx * sy, sx * cy, fcos_rev(rx));
 }
 // sampleHG, 1157-1171
 DEV v3 sample_hg(v3 w, float seed) {
@@ -798,10 +801,9 @@ DEV v3 sample_hg(v3 w, float seed) {
   float sqr = (1.0f - g * g) / (1.0f - g + 2.0f * g * ux);
   float cos_theta = (1.0f + g * g - sqr * sqr) / (2.0f * g);
   float sin_theta = fsqrt(fmaxf(0.0f, 1.0f - cos_theta * cos_theta));
-  float phi = TWO_PI * uy;
-  v3 t, b;
+  v3 t, b;  // phi = 2*pi*uy
   calc_binormals(w, t, b);
-  return normalize((t * (fcos(phi) * sin_theta) + b * (fsin(phi) * sin_theta)) + w * cos_theta);
+  return normalize((t * (fcos_rev(uy) * sin_theta) + b * (fsin_rev(uy) * sin_theta)) + w * cos_theta);
 }
 
 // powerHeuristic / cosineHemispherePdf / lightSamplingPdf, 1233-1262
@@ -2177,6 +2179,18 @@ struct Integrator {
     const GeomRec g = sc.geom(hit.index);
     const MatRec mt = sc.mat(hit.index);
     v3 c = mk(mt.cr, mt.cg, mt.cb), e = mk(mt.er, mt.eg, mt.eb);
+    // scene-specialised scenes without textures read c and e with their
+    // max(., 0.001) clamps applied at compile time (JitScene::mat_shade); the
+    // light sampling below still gets the material as the shader passes it
+    bool pre = false;
+    if constexpr (Scene::kStatic) {
+      if constexpr (!Scene::any_tex()) {
+        const MatRec ms = sc.mat_shade(hit.index);
+        c = mk(ms.cr, ms.cg, ms.cb);
+        e = mk(ms.er, ms.eg, ms.eb);
+        pre = true;
+      }
+    }
     if (sc.any_tex()) {  // raytracer.glsl:2071, 2077
       const TexRec tr = sc.tex(hit.index);
       if (tr.type >= 0 && (tr.opts & 3u)) {
@@ -2191,9 +2205,9 @@ struct Integrator {
         }
       }
     }
-    c = vmaxs(c, 0.001f);
+    if (!pre) c = vmaxs(c, 0.001f);
     float inside = -sgn(dot(rd, hit.n));
-    e = vmaxs(e, 0.001f);
+    if (!pre) e = vmaxs(e, 0.001f);
     if (mt.type == M_LIGHT) {
       mask = mask * c;
       float w = 1.0f;
@@ -2361,9 +2375,9 @@ struct Integrator {
     const v3 fp = normalize(((u * dx) * P.uULen + (v * dy) * P.uVLen) + w) * P.focal;
     v3 ro = mk(P.cam_px, P.cam_py, P.cam_pz), rd;
     if (P.aperture != 0.0f) {
-      const float ang = hash(seed + 496.4562f) * TWO_PI;
+      const float ang = hash(seed + 496.4562f);  // revolutions
       const float rad = hash(seed + 249.1686f) * P.aperture;
-      const v3 ap = (u * fcos(ang) + v * fsin(ang)) * rad;
+      const v3 ap = (u * fcos_rev(ang) + v * fsin_rev(ang)) * rad;
       ro = ro + ap;
       rd = normalize(fp - ap);
     } else {

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -103,6 +104,16 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "{" << fl(m.cr) << "," << fl(m.cg) << "," << fl(m.cb) << "," << m.type << "," << fl(m.er) << "," << fl(m.eg)
       << "," << fl(m.eb) << "," << fl(m.nt) << "},";
   }
+  // the same records with max(c, 0.001) and max(e, 0.001) applied
+  // (raytracer.glsl:2071, 2077): what the bounce step reads when no mesh has
+  // a texture, so the clamps cost no instructions per hit (JitScene::mat_shade)
+  o << "};\n__constant__ const MatRec kJitMatS[" << (nt > 0 ? nt : 1) << "] = {";
+  for (int i = 0; i < nt; i++) {
+    const MatRec &m = s.mat[i];
+    auto c = [](float v) { return fl(std::max(v, 0.001f)); };
+    o << "{" << c(m.cr) << "," << c(m.cg) << "," << c(m.cb) << "," << m.type << "," << c(m.er) << "," << c(m.eg)
+      << "," << c(m.eb) << "," << fl(m.nt) << "},";
+  }
   o << "};\n__constant__ const TexRec kJitTex[" << (nt > 0 ? nt : 1) << "] = {";
   for (int i = 0; i < nt; i++) {
     const TexRec &t = s.tex[i];
@@ -130,6 +141,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
        "  __device__ static constexpr int n_lights() { return kLights; }\n"
        "  __device__ static GeomRec geom(int i) { return kJitGeom[i]; }\n"
        "  __device__ static MatRec mat(int i) { return kJitMat[i]; }\n"
+       "  __device__ static MatRec mat_shade(int i) { return kJitMatS[i]; }\n"
        "  __device__ static float j3(int i) { return kJitJ3[i]; }\n"
        "  __device__ static int sdf_kind(int i) { return kJitSdfKind[i]; }\n"
        "  __device__ static int light(int i) { return kJitLights[i]; }\n"

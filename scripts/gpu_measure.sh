@@ -59,7 +59,7 @@ for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do
   skip=$((WARMUP * ${LPS[$cfg]}))
   if [ "${PROFILE:-1}" = "1" ]; then
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$cfg" -o run -- \
-      python bench.py --config $cfg --steps $STEPS --warmup $WARMUP --no-cpu-baseline > "$O/prof_$cfg.json" 2> "$O/prof_$cfg.err"
+      python bench.py --config $cfg --steps $STEPS --warmup $WARMUP --no-cpu-baseline --no-secondary > "$O/prof_$cfg.json" 2> "$O/prof_$cfg.err"
     rc=$?; echo "kernel trace $cfg rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$O/prof_$cfg.err"; exit $rc; }
     python3 scripts/kt_summary.py "$O/kt_$cfg.json" "$O/kt_$cfg" $skip
     find "$O/kt_$cfg" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_$cfg.csv" \;
@@ -67,7 +67,7 @@ for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do
   fi
   if [ "${PMC:-1}" = "1" ]; then
     # one warm-up step + one counted step; the warm-up's dispatches are skipped
-    CMD="python bench.py --config $cfg --steps 1 --warmup 1 --no-cpu-baseline"
+    CMD="python bench.py --config $cfg --steps 1 --warmup 1 --no-cpu-baseline --no-secondary"
     i=0; dirs=""
     for pass in "FETCH_SIZE" "WRITE_SIZE" \
         "SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
@@ -90,9 +90,9 @@ if [ -n "${AB:-}" ]; then
     for cfg in ${AB_CONFIGS:-${CONFIGS:-c2 c1 c3 c4 c5}}; do
       for v in "${VARS[@]}"; do
         name=${v%%:*}; envs=${v#*:}
-        timeout -k 10 300 env $envs python bench.py --config $cfg --steps $STEPS --warmup $WARMUP --no-cpu-baseline \
+        timeout -k 10 300 env $envs python bench.py --config $cfg --steps $STEPS --warmup $WARMUP --no-cpu-baseline --no-secondary \
           > "$O/ab_${cfg}_${name}_r$round.json" 2> "$O/ab_${cfg}_${name}_r$round.err"
-        rc=$?; echo "ab $cfg $name round $round rc=$rc: $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['kernel_ms_per_launch'], d['roofline']['events_per_sample'].get('bvh_node'))" "$O/ab_${cfg}_${name}_r$round.json" 2>/dev/null)"
+        rc=$?; echo "ab $cfg $name round $round rc=$rc: $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['kernel_ms_per_launch'], d['roofline']['events_per_sample'].get('bvh_node'), d.get('gpu_clock', {}).get('median_mhz'))" "$O/ab_${cfg}_${name}_r$round.json" 2>/dev/null)"
         stop_if_bad $rc
       done
     done

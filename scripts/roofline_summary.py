@@ -73,7 +73,9 @@ for c in ("c1", "c2", "c3", "c4", "c5"):
                frac_scalar=ach / PEAK_SCALAR, bench_frac=R["frac"])
     if pr:
         row["profiled_ms_per_step"] = pr["ms_per_step"]
-        row["check_kernel_x_launches_le_step"] = med * lps <= pr["ms_per_step"] * 1.0001
+        # the trace median covers every kept dispatch (warm-up steps included), ms_per_step only the timed ones:
+        # allow 1% run-to-run jitter between the two windows
+        row["check_kernel_x_launches_le_step"] = med * lps <= pr["ms_per_step"] * 1.01
     if pmc:
         clk = pmc.get("clock_ghz_median")
         row["clock_ghz"] = clk
@@ -107,7 +109,7 @@ print("FETCH_SIZE calibration, true bytes / counter bytes (scripts/fetch_calib.h
       ", ".join("%s x%s" % (k, v) for k, v in fac.items()))
 print()
 print("| config | Msamples/s | FLOP/sample | kernel ms/launch: rocprof median (min-max) / HIP events | launches x median <= "
-      "ms_per_step (profiled run) | TFLOP/s | frac of 157.3 | frac of scalar peak | clock GHz | VALU busy | "
+      "ms_per_step (profiled run, 1% jitter) | TFLOP/s | frac of 157.3 | frac of scalar peak | clock GHz | VALU busy | "
       "lane util | HBM bytes/launch est. (range) / algorithmic | GB/s | frac of 8 TB/s |")
 print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
 for r in rows:

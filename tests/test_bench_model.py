@@ -48,11 +48,12 @@ def test_committed_profiles_feed_the_bench_line():
         assert pmc["valu"]["SQ_INSTS_VALU"] > pmc["valu"]["SQ_INSTS_VALU_TRANS_F32"] > 0, c
 
 
-def test_roofline_summary_reproduces_committed_table(tmp_path):
-    """profiles/r03/roofline.md is what scripts/roofline_summary.py computes
+@pytest.mark.parametrize("rd", ["r03", "r04"])
+def test_roofline_summary_reproduces_committed_table(rd):
+    """profiles/<round>/roofline.md is what scripts/roofline_summary.py computes
     from the committed per-workload files (no hand edits)."""
     import subprocess
-    d = os.path.join(REPO, "profiles", "r03")
+    d = os.path.join(REPO, "profiles", rd)
     out = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "roofline_summary.py"), d],
                          capture_output=True, text=True, check=True).stdout
     assert out == open(os.path.join(d, "roofline.md")).read()
