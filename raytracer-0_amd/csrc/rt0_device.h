@@ -179,6 +179,10 @@ struct LaunchParams {
   // exchanged rows on either side of each; a fetch elsewhere bumps *halo_miss
   int32_t halo_rows;
   uint32_t *halo_miss;
+  // the same check without integer division (row_local): 1/band and
+  // 1/n_shards as floats, and the shards that own the bands next to ours
+  float band_inv, shards_inv;
+  int32_t shard_next, shard_prev;  // (shard + 1) % n_shards, (shard - 1) mod n_shards
   // Frame-chunked launch (few pixels per device, e.g. 8-way sharding): grid.z
   // = chunk index, each lane renders frames [z*frame_chunk, +frame_chunk) of
   // its pixel into samples[frame][launch pixel]; rt0_sum_kernel then adds them

@@ -669,6 +669,10 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.counters = c->d_counters;
   p.ema_alpha = 1.0f / (float)c->temporal_frames;  // raytracer.glsl:2164
   p.halo_rows = 0;
+  p.band_inv = 1.0f / (float)c->band;
+  p.shards_inv = 1.0f / (float)c->n_shards;
+  p.shard_next = (c->shard + 1) % c->n_shards;
+  p.shard_prev = (c->shard + c->n_shards - 1) % c->n_shards;
   if (c->n_shards > 1 && (long)c->band * c->n_shards >= c->H) {  // one contiguous block per shard
     const int lo = c->shard * c->band, hi = std::min(c->H, lo + c->band);
     p.valid_lo = std::max(0, lo - c->halo);

@@ -11,8 +11,8 @@
 // function).  Geometry and shading may be FMA-contracted (ulp-level); every
 // expression that feeds the RNG or the ReSTIR packing is evaluated in the
 // reference's operation order with contraction off (NC(...) helpers), so the
-// RNG stream is bit-identical to the reference; u2f() reproduces the reference
-// executor's uint->float.  Deviation: powerHeuristic's max(0, 0/0)
+// RNG stream is bit-identical to the reference; hash() reproduces the
+// reference executor's uint->float.  Deviation: powerHeuristic's max(0, 0/0)
 // is 0 (IEEE maxNum), not NaN.
 #pragma once
 #ifndef RT0_JIT
@@ -134,19 +134,22 @@ DEV float nc_seed3(float s, float a, float f, float c, float d) {
 }
 
 // ------------------------------------------------------------------- RNG
-// uint -> float with the reference executor's double rounding above 2^31
-// (the conversion the golden fixtures were produced with).
-DEV float u2f(uint32_t m) {
-#pragma clang fp contract(off)
-  if (m < 0x80000000u) return (float)(int32_t)m;
-  return (float)(int32_t)(m - 0x80000000u) + 2147483648.0f;
-}
-// raytracer.glsl:302-306
+// raytracer.glsl:302-306.  The last line converts m = (n >> 22) ^ n to float
+// the way the reference executor does (the conversion the golden fixtures
+// were produced with): float(m - 2^31) + 2^31 above 2^31, two roundings; times
+// 2^-32.  Evaluated as fma(float(m mod 2^31), 2^-32, m >= 2^31 ? 0.5 : 0):
+// the product is exact (a power of two), so the fma's one rounding is that
+// `+ 2^31` scaled by 2^-32 -- the same bits, without a second conversion,
+// compare and select
+// (5 instead of 7 VALU instructions per call; tests/test_kernel_identities.py)
 DEV float hash(float seed) {
 #pragma clang fp contract(off)
   uint32_t n = __float_as_uint(seed) * 747796405u + 2891336453u;
   n = ((n >> ((n >> 28u) + 4u)) ^ n) * 277803737u;
-  return (u2f((n >> 22u) ^ n) * 2.3283064365386963e-10f);
+  const uint32_t m = (n >> 22u) ^ n;
+  const float lo = (float)(int32_t)(m & 0x7fffffffu);
+  const float hi = __int_as_float((int32_t)m >> 31 & 0x3f000000);
+  return __builtin_fmaf(lo, 2.3283064365386963e-10f, hi);
 }
 // raytracer.glsl:308-312
 DEV void hash2(float sx, float sy, float &ox, float &oy) {
@@ -1132,6 +1135,7 @@ struct Integrator {
   Scene sc;
   Cfg C;
   float fcx, fcy;  // gl_FragCoord
+  float stx, sty;  // 2 * gl_FragCoord / resolution - 1 (set_pixel)
   uint32_t frame;
   float hero;
   int diff_b, spec_b, scat_ev;
@@ -1334,14 +1338,23 @@ struct Integrator {
   }
   // Sharded ReSTIR: does this shard hold reservoir row y (an own band, or
   // within halo_rows of one: the rows the exchange brings in)?
+  // The band b = y / band and its owner b % n_shards by float reciprocals
+  // (quot_small, exact far above any image height; tests/
+  // test_kernel_identities.py): the integer divisions they replace cost ~30
+  // VALU instructions each, four per row, two rows per reservoir tap.
   DEV bool row_local(int y) const {
     if (P.halo_rows <= 0) return y >= P.valid_lo && y < P.valid_hi;
-    const int b = y / P.band, off = y - b * P.band;
-    const bool own = b % P.n_shards == P.shard;
-    const bool below = b > 0 && (b - 1) % P.n_shards == P.shard && off < P.halo_rows;
-    const bool above = (b + 1) * P.band < P.height && (b + 1) % P.n_shards == P.shard && off >= P.band - P.halo_rows;
+    const int b = quot_small(y, P.band_inv), off = y - __mul24(b, P.band);
+    const int r = b - __mul24(quot_small(b, P.shards_inv), P.n_shards);  // b % n_shards
+    const bool own = r == P.shard;
+    const bool below = b > 0 && r == P.shard_next && off < P.halo_rows;  // band b-1 is ours
+    const bool above = __mul24(b + 1, P.band) < P.height && r == P.shard_prev && off >= P.band - P.halo_rows;
     return own || below || above;
   }
+  // floor(a / d) for 0 <= a < 2^21 from inv = fl(1/d): (a + 0.5) / d lies at
+  // least 0.5/d from an integer, and the two roundings move it by at most
+  // (a + 0.5)/d * 2^-23 < 0.5/d
+  DEV static int quot_small(int a, float inv) { return (int)(((float)a + 0.5f) * inv); }
   // GL LINEAR + CLAMP_TO_EDGE fetch of an RGBA32F plane (index.js:660-664)
   DEV float4 tex2d(const float4 *__restrict__ t, float u, float v) {
 #pragma clang fp contract(off)
@@ -2352,11 +2365,21 @@ struct Integrator {
     sx = nc_seed3(seed, 8652.1f, fr, b, 7895.13f);
     sy = nc_seed3(seed, 1234.567f, fr, b, 9876.54f);
   }
-  DEV void begin(Path &ps, int px, int py) {
+  // the pixel's gl_FragCoord and the camera offset that depends on it alone
+  // (once per pixel: path regeneration starts its samples with begin_sample)
+  DEV void set_pixel(int px, int py) {
     fcx = (float)px + 0.5f;
     fcy = (float)py + 0.5f;
+    stx = 2.0f * fcx / P.res_x - 1.0f;
+    sty = 2.0f * fcy / P.res_y - 1.0f;
+  }
+  DEV void begin(Path &ps, int px, int py) {
+    set_pixel(px, py);
+    begin_sample(ps);
+  }
+  // main()'s camera ray of this pixel and `frame` (raytracer.glsl:2118-2150)
+  DEV void begin_sample(Path &ps) {
     diff_b = spec_b = scat_ev = 0;
-    const float stx = 2.0f * fcx / P.res_x - 1.0f, sty = 2.0f * fcy / P.res_y - 1.0f;
     const float seed = pixel_seed();
     hero = 550.0f;
     if constexpr (SPECTRAL) {
@@ -2467,7 +2490,7 @@ DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int 
         accumulate(it, P, a, it.finish(ps));
         if (++f >= P.nframes) break;
         it.frame = P.frame0 + (uint32_t)f;
-        it.begin(ps, px, py);
+        it.begin_sample(ps);  // same pixel: set_pixel's values stand
         alive = cfg.max_bounces() > 0;
       }
       if constexpr (It::SUSP) it.march_pending(ps);

@@ -1,6 +1,16 @@
 set -o pipefail
-O=gpurun_out/r04; mkdir -p $O
 export TMPDIR=/tmp RT0_SEGV_TRACE=1
-timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
-rc=$?; tail -6 $O/pytest_gpu.log; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
-OUT=r04 TESTS=0 CONFIGS="${CONFIGS:-c2 c1 c3}" MIX=1 bash scripts/gpu_measure.sh
+O=gpurun_out/r4g; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+rc=$?; tail -4 $O/pytest_gpu.log; [ $rc -gt 1 ] && exit $rc
+for round in 1 2 3; do
+  for v in base prev; do
+    if [ $v = base ]; then
+      timeout -k 10 300 python bench.py --config c2 --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > $O/c2_${v}_$round.json 2> $O/c2_${v}_$round.err
+    else
+      timeout -k 10 300 env PROBES_PATCH=scripts/ab_r4_prev.patch bash scripts/probes.sh python bench.py --config c2 --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > $O/c2_${v}_$round.json 2> $O/c2_${v}_$round.err
+    fi
+    rc=$?; echo "$v $round rc=$rc $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['kernel_ms_per_launch'], d.get('gpu_clock', {}).get('median_mhz'))" $O/c2_${v}_$round.json 2>/dev/null)"
+    [ $rc -ne 0 ] && { tail -5 $O/c2_${v}_$round.err; exit $rc; }
+  done
+done
