@@ -1,16 +1,10 @@
 set -o pipefail
 export TMPDIR=/tmp RT0_SEGV_TRACE=1
-O=gpurun_out/r4g; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
-rc=$?; tail -4 $O/pytest_gpu.log; [ $rc -gt 1 ] && exit $rc
-for round in 1 2 3; do
-  for v in base prev; do
-    if [ $v = base ]; then
-      timeout -k 10 300 python bench.py --config c2 --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > $O/c2_${v}_$round.json 2> $O/c2_${v}_$round.err
-    else
-      timeout -k 10 300 env PROBES_PATCH=scripts/ab_r4_prev.patch bash scripts/probes.sh python bench.py --config c2 --steps 10 --warmup 3 --no-cpu-baseline --no-secondary > $O/c2_${v}_$round.json 2> $O/c2_${v}_$round.err
-    fi
-    rc=$?; echo "$v $round rc=$rc $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['kernel_ms_per_launch'], d.get('gpu_clock', {}).get('median_mhz'))" $O/c2_${v}_$round.json 2>/dev/null)"
-    [ $rc -ne 0 ] && { tail -5 $O/c2_${v}_$round.err; exit $rc; }
-  done
-done
+O=gpurun_out/r4i; mkdir -p $O
+RT0_PIX_QUEUE=4 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu_q4.log 2>&1
+rc=$?; tail -6 $O/pytest_gpu_q4.log; [ $rc -gt 1 ] && exit $rc
+OUT=r4i TESTS=0 BENCH=0 PROFILE=0 PMC=0 CONFIGS="c4 c2 c1" AB="q2:RT0_PIX_QUEUE=2;q4:RT0_PIX_QUEUE=4" ROUNDS=2 bash scripts/gpu_measure.sh || exit $?
+timeout -k 10 400 python -u scripts/restir_shard_sim.py c5 > $O/restir_shard_sim.txt 2>&1
+rc=$?; tail -12 $O/restir_shard_sim.txt; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u scripts/shard_sim.py > $O/shard_sim.txt 2>&1
+rc=$?; cat $O/shard_sim.txt; exit $rc
