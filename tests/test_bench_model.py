@@ -57,3 +57,23 @@ def test_roofline_summary_reproduces_committed_table(rd):
     out = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "roofline_summary.py"), d],
                          capture_output=True, text=True, check=True).stdout
     assert out == open(os.path.join(d, "roofline.md")).read()
+
+
+def test_clock_sampler_reads_the_starred_level(tmp_path):
+    """bench.ClockSampler (the bench line's gpu_clock): the starred line of an
+    amdgpu pp_dpm_sclk file is the current level; a sampler with no file
+    reports why instead of a clock."""
+    f = tmp_path / "pp_dpm_sclk"
+    f.write_text("0: 500Mhz\n1: 1900Mhz *\n2: 2400Mhz\n")
+    s = bench.ClockSampler.__new__(bench.ClockSampler)
+    s.path, s.err, s.mhz, s._stop, s._th = str(f), None, [], None, None
+    s.start()
+    f.write_text("0: 500Mhz\n1: 1900Mhz\n2: 2400Mhz *\n")
+    s.stop()
+    rep = s.report()
+    assert rep["min_mhz"] == 1900.0 and rep["max_mhz"] == 2400.0 and rep["samples"] >= 2
+    none = bench.ClockSampler.__new__(bench.ClockSampler)
+    none.path, none.err, none.mhz, none._stop, none._th = None, "no pp_dpm_sclk for PCI 0000:05", [], None, None
+    none.start()
+    none.stop()
+    assert none.report() == {"median_mhz": None, "source": None, "error": "no pp_dpm_sclk for PCI 0000:05"}
