@@ -1154,6 +1154,9 @@ struct Integrator {
   float gr_bounce;
   int gr_mat;
   bool gr_have, gr_spec;
+  // the light-sampling kernel's LDS copy of the ReSTIR candidates' light data
+  // (candidate_table), or null: read from the scene tables
+  const float4 *cand_lds = nullptr;
 
   DEV Integrator(const LaunchParams &p, Scene s, Cfg c)
       : P(p), sc(s), C(c), n_isect(0), n_iter(0), n_nee(0), n_map(0) {}
@@ -1483,13 +1486,23 @@ struct Integrator {
       float rvx, rvy;
       hash2(nc_addmul(sx, (float)i, 0.1f), nc_addmul(sy, (float)i, 0.2f), rvx, rvy);
       int ai = min(max((int)(rvx * (float)nl), 0), nl - 1);
-      int li = sc.light(ai);
-      if (li < 0 || li >= sc.n_meshes() + sc.n_sdfs()) continue;
-      const GeomRec lg = sc.geom(li);
-      const MatRec lmt = sc.mat(li);
+      int li;
+      v3 lp, lc;
+      if (cand_lds) {  // the same values, one LDS round trip instead of two dependent global ones
+        const float4 a = cand_lds[2 * ai], b = cand_lds[2 * ai + 1];
+        li = __float_as_int(b.z);
+        if (li < 0) continue;
+        lp = mk(a.x, a.y, a.z);
+        lc = mk(a.w, b.x, b.y);
+      } else {
+        li = sc.light(ai);
+        if (li < 0 || li >= sc.n_meshes() + sc.n_sdfs()) continue;
+        const GeomRec lg = sc.geom(li);
+        const MatRec lmt = sc.mat(li);
+        lp = lpos(li, lg);  // 1645
+        lc = mk(lmt.cr, lmt.cg, lmt.cb) * mk(lmt.er, lmt.eg, lmt.eb);
+      }
       if (COUNT) ++n_cand;
-      v3 lp = lpos(li, lg);  // 1645
-      v3 lc = mk(lmt.cr, lmt.cg, lmt.cb) * mk(lmt.er, lmt.eg, lmt.eb);
       float tv = target_fn(lp, lc, hp, hn, mat);
       if (tv > 0.0f) {  // updateReservoir, 1305-1326
         init.ws += tv;
@@ -2582,6 +2595,37 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 // lengths.  Same arguments, same arithmetic as the inline call;
 // the last call of a pixel writes its reservoir MRTs (g_final_reservoir,
 // raytracer.glsl:2171-2174).
+// The ReSTIR candidates' light data in LDS (scene-specialised, non-animated
+// scenes): per light slot k, (pos, c*e, the mesh index or -1 if the slot is
+// skipped) in two float4s, written by the workgroup's first threads before
+// its one barrier.  A candidate's light is picked per lane at random, so the
+// scene-table reads are two dependent per-lane loads (light_index[k], then
+// the mesh's geometry and material) for each of the up to 16 candidates of a
+// call; from LDS it is one short round trip (raytracer.glsl:1633-1650).
+// Returns null where the tables are read as before.
+template <class Scene, class Cfg>
+DEV const float4 *candidate_table(const Scene &sc, const Cfg &cfg) {
+  if constexpr (Scene::kStatic && Scene::kLights > 0) {
+    if constexpr ((Cfg::flags() & F_ANIM) == 0u) {
+      __shared__ float4 cand[2 * Scene::kLights];
+      for (int k = (int)threadIdx.x; k < Scene::kLights; k += (int)blockDim.x) {
+        const int li = sc.light(k);
+        const bool ok = li >= 0 && li < sc.n_meshes() + sc.n_sdfs();
+        const GeomRec lg = sc.geom(ok ? li : 0);
+        const MatRec lmt = sc.mat(ok ? li : 0);
+        const v3 lc = mk(lmt.cr, lmt.cg, lmt.cb) * mk(lmt.er, lmt.eg, lmt.eb);
+        cand[2 * k] = make_float4(lg.px, lg.py, lg.pz, lc.x);
+        cand[2 * k + 1] = make_float4(lc.y, lc.z, __int_as_float(ok ? li : -1), 0.f);
+      }
+      __syncthreads();
+      return cand;
+    }
+  }
+  (void)sc;
+  (void)cfg;
+  return nullptr;
+}
+
 template <class Scene, class Cfg, bool VOL, bool SDF, bool SPECTRAL>
 DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   // one wave per RT0_NEE_REGIONS consecutive regions: their records form one
@@ -2589,6 +2633,7 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   // ~68 records per region: one region per wave ran a 64-record chunk and a
   // 4-record chunk).  Measured 1 / 2 / 4 / 8 regions: C3 5326 / 5491 / 4627 /
   // 3320, C5 1467 / 1558 / 1513 / 1403 Msamples/s (profiles/r03/defer/)
+  const float4 *cand = candidate_table(sc, cfg);
   const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6))) *
                       RT0_NEE_REGIONS;
   if (r0 >= (uint32_t)P.nee_regions) return;
@@ -2612,6 +2657,7 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     return (size_t)(r0 + q) * (uint32_t)P.nee_cap + off;
   };
   auto setup = [&](It &it, const NeeRec &r) {
+    it.cand_lds = cand;
     it.frame = P.frame0;
     const int py = r.pix / P.width, px = r.pix - py * P.width;
     it.fcx = (float)px + 0.5f;
