@@ -1127,6 +1127,35 @@ DEV void unpack_alpha(float pa, int nlights, float &age, float &M, int &idx) {
   idx = (int)(nli * (float)len1) - 1;
 }
 
+// LDS copies of a scene-specialised kernel's geometry and material tables,
+// written by the workgroup's first threads before one barrier, for the
+// lookups at a per-lane index (the hit mesh's material each bounce, a
+// light-sampling record's material, the light a shadow ray reached): the
+// constant tables are read with a dependent per-lane global load there.
+// Loops over the meshes keep reading the constant tables (compile-time
+// indices fold to immediates).  All null for the ahead-of-time kernels.
+struct SceneTables {
+  const GeomRec *g;
+  const MatRec *m, *ms;
+};
+template <class Scene>
+DEV SceneTables scene_tables(const Scene &sc) {
+  if constexpr (Scene::kStatic) {
+    constexpr int n = Scene::kMeshes + Scene::kSdfs + Scene::kModels;
+    __shared__ GeomRec g[n > 0 ? n : 1];
+    __shared__ MatRec m[n > 0 ? n : 1], ms[n > 0 ? n : 1];
+    for (int k = (int)threadIdx.x; k < n; k += (int)blockDim.x) {
+      g[k] = sc.geom(k);
+      m[k] = sc.mat(k);
+      ms[k] = sc.mat_shade(k);
+    }
+    __syncthreads();
+    return SceneTables{g, m, ms};
+  }
+  (void)sc;
+  return SceneTables{nullptr, nullptr, nullptr};
+}
+
 // ----------------------------------------------------------- integrator
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 struct Integrator {
@@ -1157,6 +1186,29 @@ struct Integrator {
   // the light-sampling kernel's LDS copy of the ReSTIR candidates' light data
   // (candidate_table), or null: read from the scene tables
   const float4 *cand_lds = nullptr;
+  // LDS copies of the scene tables for lookups at a per-lane index (the hit
+  // mesh, a record's material, the lit light; scene_tables): every
+  // scene-specialised Integrator gets them (pass_body, nee_body)
+  const GeomRec *g_lds = nullptr;
+  const MatRec *m_lds = nullptr, *ms_lds = nullptr;
+  DEV GeomRec geom_at(int i) const {
+    if constexpr (Scene::kStatic) return g_lds[i];
+    else return sc.geom(i);
+  }
+  DEV MatRec mat_at(int i) const {
+    if constexpr (Scene::kStatic) return m_lds[i];
+    else return sc.mat(i);
+  }
+  DEV MatRec mat_shade_at(int i) const {
+    if constexpr (Scene::kStatic) return ms_lds[i];
+    else return sc.mat_shade(i);
+  }
+  template <class T>
+  DEV void use_tables(const T &t) {
+    g_lds = t.g;
+    m_lds = t.m;
+    ms_lds = t.ms;
+  }
 
   DEV Integrator(const LaunchParams &p, Scene s, Cfg c)
       : P(p), sc(s), C(c), n_isect(0), n_iter(0), n_nee(0), n_map(0) {}
@@ -1180,7 +1232,7 @@ struct Integrator {
           only = i;
         }
       });
-    return sc.mat(n == 1 ? only : il);
+    return n == 1 ? sc.mat(only) : mat_at(il);
   }
   // a light/sphere position as the reference reads it where it calls
   // getAnimatedPosition (RENDER_MODE 1); the static position otherwise
@@ -1255,7 +1307,7 @@ struct Integrator {
           *susp = true;
           return dl;
         }
-        const MatRec mh = sc.mat(hit.index);
+        const MatRec mh = mat_at(hit.index);
         if (mh.type == M_LIGHT) {
           float weight = 2.0f * (1.0f - cos_a_max);
           float T_fog = 1.0f;
@@ -1270,7 +1322,7 @@ struct Integrator {
           *susp = true;
           return dl;
         }
-        const MatRec mh = sc.mat(hit.index);
+        const MatRec mh = mat_at(hit.index);
         if (mh.type == M_LIGHT) {
           v3 c = vmaxs(light_color(hit, mh), 0.001f);
           dl = (c * mk(mh.er, mh.eg, mh.eb)) * fmaxf(0.001f, dot(sr, nl));
@@ -2202,8 +2254,8 @@ struct Integrator {
       }
       return false;
     }
-    const GeomRec g = sc.geom(hit.index);
-    const MatRec mt = sc.mat(hit.index);
+    const GeomRec g = geom_at(hit.index);
+    const MatRec mt = mat_at(hit.index);
     v3 c = mk(mt.cr, mt.cg, mt.cb), e = mk(mt.er, mt.eg, mt.eb);
     // scene-specialised scenes without textures read c and e with their
     // max(., 0.001) clamps applied at compile time (JitScene::mat_shade); the
@@ -2211,7 +2263,7 @@ struct Integrator {
     bool pre = false;
     if constexpr (Scene::kStatic) {
       if constexpr (!Scene::any_tex()) {
-        const MatRec ms = sc.mat_shade(hit.index);
+        const MatRec ms = mat_shade_at(hit.index);
         c = mk(ms.cr, ms.cg, ms.cb);
         e = mk(ms.er, ms.eg, ms.eb);
         pre = true;
@@ -2514,6 +2566,7 @@ DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int 
 
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  const SceneTables tabs = scene_tables(sc);  // (before any thread leaves: one barrier)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
   const int ly = (lane >> 3) + ((wave >> 1) << 3);
@@ -2523,6 +2576,7 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const int py = image_row(P, r);
   if (py >= P.height) return;
   Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT> it(P, sc, cfg);
+  it.use_tables(tabs);
   const size_t pix = (size_t)py * P.width + px;                        // image pixel (ReSTIR planes)
   const size_t apix = P.compact ? (size_t)r * P.width + px : pix;      // accumulator pixel
   if (!RESTIR && P.samples) {  // frame-chunked: samples out, rt0_sum_kernel accumulates
@@ -2634,6 +2688,7 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   // 4-record chunk).  Measured 1 / 2 / 4 / 8 regions: C3 5326 / 5491 / 4627 /
   // 3320, C5 1467 / 1558 / 1513 / 1403 Msamples/s (profiles/r03/defer/)
   const float4 *cand = candidate_table(sc, cfg);
+  const SceneTables tabs = scene_tables(sc);
   const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6))) *
                       RT0_NEE_REGIONS;
   if (r0 >= (uint32_t)P.nee_regions) return;
@@ -2658,6 +2713,7 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   };
   auto setup = [&](It &it, const NeeRec &r) {
     it.cand_lds = cand;
+    it.use_tables(tabs);
     it.frame = P.frame0;
     const int py = r.pix / P.width, px = r.pix - py * P.width;
     it.fcx = (float)px + 0.5f;
@@ -2691,7 +2747,7 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       setup(it, r);
       float sx, sy;
       it.restir_seeds(r.bounce(), sx, sy);
-      const auto sp = it.restir_split(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), sc.mat(r.mat()), sx, sy);
+      const auto sp = it.restir_split(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), it.mat_at(r.mat()), sx, sy);
       if (sp.done) {
         store(r, sp.c, it.fin);
       } else {
@@ -2728,7 +2784,7 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     setup(it, r);
     float sx, sy;
     it.restir_seeds(r.bounce(), sx, sy);
-    const v3 c = it.restir(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), sc.mat(r.mat()), sx, sy);
+    const v3 c = it.restir(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), it.mat_at(r.mat()), sx, sy);
     store(r, c, it.fin);
   }
 #endif
