@@ -1199,6 +1199,8 @@ struct Integrator {
     if constexpr (Scene::kStatic) return m_lds[i];
     else return sc.mat(i);
   }
+  // light_index[k] at a per-lane k: from the candidate table when the kernel has one
+  DEV int light_at(int k) const { return cand_lds ? __float_as_int(cand_lds[2 * k + 1].z) : sc.light(k); }
   DEV MatRec mat_shade_at(int i) const {
     if constexpr (Scene::kStatic) return ms_lds[i];
     else return sc.mat_shade(i);
@@ -1281,11 +1283,13 @@ struct Integrator {
     v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
     return (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
   }
+  // (dyn: li is a per-lane index -- ReSTIR's chosen light -- read from the
+  // LDS tables; otherwise a loop constant that folds)
   DEV v3 direct_light(int li, v3 x, v3 nl, float seed, March *ms = nullptr, bool *susp = nullptr,
-                      LightGeo *geo = nullptr) {
+                      LightGeo *geo = nullptr, bool dyn = false) {
     if (COUNT) ++n_nee;
-    const GeomRec g = sc.geom(li);
-    const MatRec lm = sc.mat(li);
+    const GeomRec g = dyn ? geom_at(li) : sc.geom(li);
+    const MatRec lm = dyn ? mat_at(li) : sc.mat(li);
     Hit hit;
     v3 dl = mk(0.f, 0.f, 0.f);
     if (lm.type == M_LIGHT) {
@@ -1793,11 +1797,11 @@ struct Integrator {
     fr.W = restir_weight(fr, tp);
     v3 f = mk(0.f, 0.f, 0.f);
     if (fr.W > 0.0f && fr.idx >= 0 && fr.idx < nl) {
-      const int act = sc.light(fr.idx);
+      const int act = light_at(fr.idx);
       if (act >= 0 && act < sc.n_meshes() + sc.n_sdfs()) {
         // direct_light(act, hp, hn, sx + 456.789f), 1174-1230, up to its triangle query
-        const GeomRec g = sc.geom(act);
-        const MatRec lm = sc.mat(act);
+        const GeomRec g = geom_at(act);
+        const MatRec lm = mat_at(act);
         const float ew = restir_ew(fr);
         const v3 o2 = hp + hn * EPSILON;
         if (lm.type == M_LIGHT && g.type == T_SPHERE) {  // 1185-1205
@@ -1854,12 +1858,12 @@ struct Integrator {
     fin = fr;
     if (GHOST) return mk(0.f, 0.f, 0.f);
     if (fr.W > 0.0f && fr.idx >= 0 && fr.idx < nl) {
-      int act = sc.light(fr.idx);
+      int act = light_at(fr.idx);
       if (act >= 0 && act < sc.n_meshes() + sc.n_sdfs()) {
         // RENDER_MODE 1 re-checks visibility of the light's current position
         // (1767-1776); g_final_reservoir was stored before that update
         if (flag(F_ANIM) && !visible(hp, lpos(act, sc.geom(act)))) return mk(0.f, 0.f, 0.f);
-        v3 lc = direct_light(act, hp, hn, sx + 456.789f);
+        v3 lc = direct_light(act, hp, hn, sx + 456.789f, nullptr, nullptr, nullptr, true);
         v3 fc = lc * restir_ew(fr);
         if (!finite_(fc.x) || !finite_(fc.y) || !finite_(fc.z)) return mk(0.f, 0.f, 0.f);
         return fc;
