@@ -646,15 +646,15 @@ struct Geometry {
                             float &tt) {
     const v3 mo = m * o;
     float tq = INF_T;
-    int iq = 0;
+    bool lq = sc.mat(0).type == M_LIGHT;  // the closest quadric is a light (mesh 0 on a miss)
     for_meshes(sc, [&](int i) {
       float t;
       const bool ok = prim<Cfg>(P, sc, C, i, o, d, m, mo, tq, t) >= 0;
       tq = ok ? t : tq;
-      iq = ok ? i : iq;
+      lq = ok ? sc.mat(i).type == M_LIGHT : lq;  // (a constant per mesh: no per-lane table read)
     });
     tt = fminf(tq, lim);
-    if (tq < lim) return sc.mat(iq).type == M_LIGHT;
+    if (tq < lim) return lq;
     return true;
   }
 
@@ -666,8 +666,15 @@ struct Geometry {
   // march loop has finished it (ms->done), the same call with the same ray
   // recomputes the quadric tests (deterministic) and completes the hit.
   template <bool SDF, class Cfg>
+  // gt: the LDS copy of the geometry table (scene-specialised kernels; the
+  // winner's normal reads it at a per-lane index), null otherwise
   static DEV float intersect(const LaunchParams &P, const Scene &sc, const Cfg &C, v3 o, v3 d, Hit &hit,
-                             unsigned long long &nmap, March *ms = nullptr, unsigned long long *nbvh = nullptr) {
+                             unsigned long long &nmap, March *ms = nullptr, unsigned long long *nbvh = nullptr,
+                             const GeomRec *gt = nullptr) {
+    auto geom_of = [&](int i) -> GeomRec {
+      if constexpr (Scene::kStatic) return gt[i];
+      else return sc.geom(i);
+    };
     hit.n = mk(0.f, 0.f, 0.f);
     hit.index = 0;
     int type = -1;
@@ -701,7 +708,7 @@ struct Geometry {
       }
     }
     if (type == T_BOX) {  // iBox's normal for the winning box, 853-856
-      const GeomRec g = sc.geom(hit.index);
+      const GeomRec g = geom_of(hit.index);
       v3 hp = (o + d * tmin) - mk(g.px, g.py, g.pz);
       v3 dd = vabs(hp) - mk(g.d0, g.d0, g.d0);
       v3 s = mk(sgn(hp.x), sgn(hp.y), sgn(hp.z));
@@ -742,10 +749,10 @@ struct Geometry {
     if (type >= 0) {
       hit.pos = d * tmin + o;
       if (type == T_SPHERE) {  // 1060
-        const GeomRec g = sc.geom(hit.index);
+        const GeomRec g = geom_of(hit.index);
         hit.n = normalize(hit.pos - ((C.flags() & F_ANIM) ? anim_pos(P, hit.index) : mk(g.px, g.py, g.pz)));
       } else if (type == T_PLANE) {
-        const GeomRec g = sc.geom(hit.index);
+        const GeomRec g = geom_of(hit.index);
         hit.n = normalize(mk(g.px, g.py, g.pz));
       }
     } else {
@@ -1242,7 +1249,7 @@ struct Integrator {
 
   DEV float isect(v3 o, v3 d, Hit &h, March *ms = nullptr) {
     if (COUNT) ++n_isect;
-    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map, ms, COUNT ? n_bvh : nullptr);
+    return G::template intersect<SDF>(P, sc, C, o, d, h, n_map, ms, COUNT ? n_bvh : nullptr, g_lds);
   }
 
   // mix(mesh.mat.c, hit.texel.rgb, hit.texel.a) of a shadow ray's light hit
