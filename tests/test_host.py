@@ -196,5 +196,12 @@ def test_jit_walk_module_for_model_scenes(cfgs, tmp_path, monkeypatch):
            re.finditer(r"\.group_segment_fixed_size:\s+(\d+)(?:.|\n)*?\.name:\s+(\S+)", notes)}
     assert {"rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve"} <= set(lds), lds
     assert lds["rt0_jit_walk"] == 256 * 24 * 2 + 16  # the stack + the wave counters
-    assert lds["rt0_jit_pass"] <= 256 * 24 * 2 + 16
-    assert lds["rt0_jit_nee"] == 0  # no BVH walk left in the light-sampling kernel
+    # the pass and light-sampling kernels also hold LDS copies of the scene
+    # tables (rt0_integrator.h scene_tables: geometry, material and clamped
+    # material, 32 B each per mesh) and the latter the ReSTIR candidates'
+    # light table (candidate_table: 32 B per light slot)
+    src = open(co[:-3] + ".hip").read()
+    k = {n: int(v) for n, v in re.findall(r"\b(kMeshes|kSdfs|kLights|kModels) = (\d+)", src)}
+    tables = 96 * (k["kMeshes"] + k["kSdfs"] + k["kModels"])
+    assert lds["rt0_jit_pass"] <= 256 * 24 * 2 + 16 + tables
+    assert lds["rt0_jit_nee"] == tables + 32 * k["kLights"]  # no BVH walk left in the light-sampling kernel
