@@ -101,6 +101,13 @@ struct NeeRec {
   __host__ __device__ int bounce() const { return (int)(mkb >> 16); }
 };
 static_assert(sizeof(NeeRec) == 48, "NeeRec is 12 words: three 16-B loads");
+// the packed fields' ranges: mat < RT0_MAX_MESH fits 8 bits; a path makes at
+// most one deferred call per bounce, so k < max_bounces and bounce <
+// max_bounces -- deferral is used only while max_bounces fits the 8-bit k
+// (rt0_host.cpp, rt0_jit_compile); deeper configs keep the inline calls
+#define RT0_NEE_MAX_BOUNCES 255
+static_assert(RT0_MAX_MESH <= 256, "NeeRec::mat is 8 bits");
+static_assert(RT0_NEE_MAX_BOUNCES <= 255 && RT0_NEE_MAX_BOUNCES < 65536, "NeeRec::k is 8 bits, bounce 16");
 
 // RT0_NEE_WALK (scenes with triangle models): a light-sampling call's
 // triangle occlusion queries go to rt0_jit_walk as WalkJobs, 32 B: the ray

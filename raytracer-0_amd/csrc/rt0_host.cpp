@@ -753,7 +753,9 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   // ReSTIR light sampling in its own kernel over the pass's appended calls
   // (rt0_integrator.h nee_body): scene-specialised kernels only; the executor
   // ghost (F_EXEC_GHOST) keeps the inline calls
-  const bool defer = restir && c->use_jit && !c->counting && !c->exec_compat && c->defer_nee && p.max_bounces > 0;
+  // (NeeRec packs the call index in 8 bits: deeper paths keep the inline calls)
+  const bool defer = restir && c->use_jit && !c->counting && !c->exec_compat && c->defer_nee && p.max_bounces > 0 &&
+                     p.max_bounces <= RT0_NEE_MAX_BOUNCES;
   // the occlusion-walk kernel (rt0_integrator.h walk_body) for scenes with
   // triangle models: quadric-only shadow geometry (no SDFs, no textured
   // lights) and RENDER_MODE 0 (Integrator::restir_split), and a grid whose

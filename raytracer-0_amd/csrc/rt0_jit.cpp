@@ -19,7 +19,6 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
-#include <fstream>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -79,17 +78,9 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // the halved round trips save (C5 22.95 vs 18.39 ms), so 1 there
   if (k.restir && s.n_models == 0) o << "#ifndef RT0_TAP_BATCH\n#define RT0_TAP_BATCH 2\n#endif\n";
   o << "using __hip_internal::int32_t; using __hip_internal::uint16_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
-  // RT0_JIT_SOURCE=<file>: the device source to compile instead of the
-  // embedded one (rt0_device.h + rt0_integrator.h concatenated) -- profiling
-  // probes only (scripts/probes.sh); part of the cache key like everything here
-  if (const char *f = getenv("RT0_JIT_SOURCE")) {
-    std::ifstream in(f);
-    std::stringstream ss;
-    ss << in.rdbuf();
-    o << strip_includes(ss.str().c_str());
-  } else {
-    o << strip_includes(rt0_jit_source_text);
-  }
+  // the embedded device source only: profiling probes build their own
+  // library from a patched copy (scripts/probes.sh), none is read at run time
+  o << strip_includes(rt0_jit_source_text);
   const int nt = s.n_total;
   o << "namespace rt0 {\n";
   o << "__constant__ const GeomRec kJitGeom[" << (nt > 0 ? nt : 1) << "] = {";
@@ -474,7 +465,7 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     rt0h::JitKey key = rt0h::make_jit_key(*cfg, ns);
     // the kernels rt0_render launches: deferred light sampling for ReSTIR (rt0_host.cpp)
     const char *d = getenv("RT0_DEFER_NEE");
-    key.defer = key.restir && key.max_bounces > 0 && (!d || atoi(d) != 0);
+    key.defer = key.restir && key.max_bounces > 0 && key.max_bounces <= RT0_NEE_MAX_BOUNCES && (!d || atoi(d) != 0);
     // (the host also needs a built BVH; here the scene's TRIANGLE entries decide)
     const char *wk = getenv("RT0_NEE_WALK");
     key.walk = key.defer && nm > 0 && ns == 0 && !s.any_tex && !(key.flags & F_ANIM) && (!wk || atoi(wk) != 0) ? 1 : 0;

@@ -1,17 +1,25 @@
 #!/bin/bash
-# Profiling probes (parity-breaking, never in the product source): applies
-# scripts/probes.patch to a scratch copy of the integrator, writes the JIT
-# device source (rt0_device.h + patched rt0_integrator.h, as tools_embed.py
-# concatenates them) and runs the given command with RT0_JIT_SOURCE pointing
-# at it.  Choose the probe with RT0_JIT_EXTRA, e.g.
+# Profiling probes (parity-breaking, never in the product source or the
+# product library): copies the repository to a scratch directory, applies
+# scripts/probes.patch (or $PROBES_PATCH) to that copy's integrator, builds the
+# copy's librt0.so there and runs the given command from inside the copy, so
+# the command loads the probe library and the product tree stays untouched.
+# Choose the probe with RT0_JIT_EXTRA, e.g.
 #   scripts/probes.sh env RT0_JIT_EXTRA=-DRT0_EXP_NO_NEE python scripts/exp_c4.py 1024 8 causes
 # Probes: RT0_EXP_NO_BVH_OCC, RT0_EXP_NO_SHADOW, RT0_EXP_SPATIAL_SELF,
 # RT0_EXP_NO_NEE, RT0_EXP_NO_VOL_NEE, RT0_NO_MIS_REUSE, RT0_FAST_SHADOW=0.
+# Output written under the copy's gpurun_out/ is copied back to this tree's.
 set -e
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
 T=$(mktemp -d)
-cp raytracer-0_amd/csrc/rt0_device.h raytracer-0_amd/csrc/rt0_integrator.h "$T/"
-patch -s -d "$T" -p3 < "${PROBES_PATCH:-scripts/probes.patch}"
-cat "$T/rt0_device.h" "$T/rt0_integrator.h" > "$T/rt0_jit_probe.src"
-export RT0_JIT_SOURCE="$T/rt0_jit_probe.src"
-"$@"
+tar -C "$ROOT" --exclude=./gpurun_out --exclude=./.git --exclude=./profiles --exclude='*.o' -cf - . | tar -C "$T" -xf -
+patch -s -d "$T" -p1 < "${PROBES_PATCH:-scripts/probes.patch}"
+make -s -j16 -C "$T/raytracer-0_amd" rt0/librt0.so
+mkdir -p "$T/gpurun_out"
+rc=0
+(cd "$T" && "$@") || rc=$?
+mkdir -p "$ROOT/gpurun_out"
+cp -r "$T/gpurun_out/." "$ROOT/gpurun_out/" 2>/dev/null || true
+rm -rf "$T"
+exit $rc

@@ -180,3 +180,24 @@ def test_deferred_buffers_follow_bounce_count(cfgs, gpu_required):
     assert np.isfinite(got).all()
     assert np.array_equal(got, want)
     assert got[vp[1]:vp[1] + 16, vp[0]:vp[0] + 16, :3].any()
+
+
+@pytest.mark.gpu
+def test_deferral_off_beyond_packed_call_index(cfgs, gpu_required):
+    """NeeRec packs a call's index along its path in 8 bits (rt0_device.h):
+    with MAX_BOUNCES above RT0_NEE_MAX_BOUNCES (255) the host keeps the inline
+    calls, so asking for deferral renders the same bits as not asking."""
+    cfg = cfg_by_name(cfgs, "c3_outdoor_restir")
+    out = []
+    for defer in (True, False):
+        r = rt0.Renderer(32, 32)
+        configure(r, cfg, cfgs)
+        c = r.get_config()
+        c.max_bounces = 300
+        r.set_config(c)
+        r.set_defer_light_sampling(defer)
+        for k in (1, 2):
+            r.render(k, 1)
+        out.append(r.read_accum())
+    assert np.isfinite(out[0]).all()
+    assert np.array_equal(out[0], out[1])
