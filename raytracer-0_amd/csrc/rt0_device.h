@@ -231,5 +231,27 @@ struct LaunchParams {
   WalkJob *walk_jobs;
   uint32_t *walk_count, *walk_res;
   int32_t walk_waves;
+  // Wavefront SDF renders (RT0_WAVEFRONT modules: rt0_jit_wf_shade +
+  // rt0_jit_wf_march, rt0_integrator.h "wavefront SDF renders").  A launch's
+  // samples are `wf_slots` path slots (frame-major, then the pass grid's tile
+  // order, wf_apad slots per frame, frames [wf_f0, wf_f0 + wf_slots /
+  // wf_apad) of the launch); region w = slots [w * wf_R, (w + 1) * wf_R) is
+  // one shade wave's.  Per round: the shade kernel reads region w of the
+  // previous round's march list (wf_in: 2 float4 per entry = ray + bound,
+  // direction + slot; wf_in_cnt[w] entries) and its results (wf_res, same
+  // index), and writes region w of this round's march list (wf_out,
+  // wf_out_cnt) and shadow list (wf_sh: 3 float4 per entry, capacity wf_R *
+  // wf_L per region, wf_sh_cnt); the march kernel takes regions off
+  // *wf_ctr and answers them (wf_res; wf_shres[light * wf_slots + slot]).
+  // Path state between rounds: wf_state[k * wf_slots + slot].
+  int32_t wf_round, wf_R, wf_L, wf_nregions, wf_f0;
+  uint32_t wf_apad, wf_slots, wf_gx;
+  uint32_t *wf_ctr;
+  float4 *wf_state;
+  float4 *wf_in, *wf_out;
+  uint32_t *wf_in_cnt, *wf_out_cnt, *wf_sh_cnt;
+  float4 *wf_res;
+  float *wf_res_id;
+  float4 *wf_sh, *wf_shres;
   float4 apos[RT0_MAX_MESH];
 };

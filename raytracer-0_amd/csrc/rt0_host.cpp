@@ -95,6 +95,7 @@ struct rt0_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = 0.f;
   int last_launches = 0;
+  int last_path = 0;  // RT0_PATH_* of the last render
   int shard = 0, n_shards = 1, band = 16;
   int halo = 0;                  // rows of exchanged reservoir halo (sharded ReSTIR)
   bool ext_restir = false;       // reservoir planes owned by the caller (rt0_set_restir_buffers)
@@ -128,6 +129,12 @@ struct rt0_ctx {
   size_t nee_waves = 0;  // entries of d_nee_count
   size_t nee_pixels = 0;
   size_t nee_planes = 0;  // float4 planes of the image d_nee_out holds (one per call index)
+  // wavefront SDF rounds (rt0_integrator.h wf_shade_body; LaunchParams::wf_*):
+  // one allocation carved into the path state, two march lists, the march
+  // answers, the shadow list and its answers, sized for wf_bytes
+  void *d_wf = nullptr;
+  size_t wf_bytes = 0;
+  bool wavefront = true;  // rt0_set_wavefront (RT0_WAVEFRONT=0 at rt0_create: off)
   std::string jit_err;
   std::string err;
 };
@@ -247,6 +254,7 @@ int rt0_create(int width, int height, int device, rt0_ctx **out) {
   c->device = device;
   if (const char *e = getenv("RT0_JIT")) c->use_jit = atoi(e) != 0;
   if (const char *e = getenv("RT0_DEFER_NEE")) c->defer_nee = atoi(e) != 0;
+  if (const char *e = getenv("RT0_WAVEFRONT")) c->wavefront = atoi(e) != 0;
   rt0h::default_config(c->cfg);
   int rc;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -278,7 +286,7 @@ void rt0_destroy(rt0_ctx *c) {
   for (void *q : {(void *)c->d_walk_jobs, (void *)c->d_walk_count, (void *)c->d_walk_res})
     if (q) (void)hipFree(q);
   for (void *q : {(void *)c->d_nee_rec, (void *)c->d_nee_count, (void *)c->d_nee_out, (void *)c->d_nee_partial,
-                  (void *)c->d_nee_n})
+                  (void *)c->d_nee_n, c->d_wf})
     if (q) (void)hipFree(q);
   for (auto &t : c->d_tex)
     if (t) (void)hipFree(t);
@@ -699,6 +707,95 @@ static int choose_variant(const rt0_ctx *c) {
   return 0;
 }
 
+// Wavefront SDF rounds (rt0_integrator.h wf_shade_body) serve the
+// scene-specialised renders of SDF scenes without ReSTIR or triangle models,
+// whose light-sampling shadow rays are decided by quadric lights: no SDF
+// entry is a light or is sampled as one (direct_light's WfShadow), at most 32
+// light slots (one bit each in the path state), 1..127 bounces (the state's
+// 7-bit counters).  rt0_set_wavefront(0) keeps the pass kernel.
+static bool wf_eligible(const rt0_ctx *c) {
+  const SceneDev &s = c->host_scene;
+  const rt0_config &g = c->cfg;
+  if (!c->wavefront || !c->use_jit || c->counting || (g.defines & RT0_USE_RESTIR)) return false;
+  if (s.n_sdfs <= 0 || s.n_models > 0 || s.n_lights > 32 || g.max_bounces < 1 || g.max_bounces > 127) return false;
+  for (int i = s.n_meshes; i < s.n_meshes + s.n_sdfs; i++)
+    if (s.mat[i].type == 0 /* LIGHT */) return false;
+  for (int i = 0; i < s.n_lights; i++)
+    if (s.light_index[i] >= s.n_meshes) return false;
+  return true;
+}
+
+// One launch of frames [p.frame0, p.frame0 + p.nframes) as wavefront rounds:
+// frame chunks of as many frames as wf_bytes holds, each MAX_BOUNCES + 2
+// rounds of the shade and march kernels; the samples land in p.samples and
+// rt0_sum_kernel adds them in frame order (the caller launches it).
+static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
+  constexpr uint32_t kR = 512;  // slots per region (one shade wave)
+  const uint32_t L = (uint32_t)std::max(1, c->host_scene.n_lights);
+  const bool extra = (p.flags & F_MIS) || ((p.flags & F_SPECTRAL) && (c->cfg.defines & RT0_USE_SPECTRAL));
+  // bytes per slot: state, two march-list entries, the answer + id, L shadow entries + answers
+  const size_t per_slot = (extra ? 48 : 32) + 2 * 32 + 16 + 4 + (size_t)L * (48 + 16);
+  const size_t budget = getenv("RT0_WF_BYTES") ? (size_t)atoll(getenv("RT0_WF_BYTES")) : (size_t)8 << 30;
+  const size_t apad = (size_t)grid.x * grid.y * 256;
+  const int fc = (int)std::max<size_t>(1, std::min<size_t>((size_t)p.nframes, budget / (apad * per_slot)));
+  const size_t S = apad * (size_t)fc;
+  if (S * L >= (1ull << 32)) return fail(c, RT0_E_UNSUPPORTED, "wavefront render: too many path slots");
+  const size_t NR = (S + kR - 1) / kR, cap = NR * kR;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_state = al(cap * (extra ? 3 : 2) * 16), b_list = al(cap * 32), b_res = al(cap * 16),
+               b_id = al(cap * 4), b_sh = al(cap * L * 48), b_shres = al(cap * L * 16), b_cnt = al(NR * 4);
+  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 3 * b_cnt + 256;
+  if (need > c->wf_bytes) {
+    if (c->d_wf) HIPCHK(c, hipFree(c->d_wf));
+    c->d_wf = nullptr;
+    c->wf_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->d_wf, need));
+    c->wf_bytes = need;
+  }
+  char *m = (char *)c->d_wf;
+  auto take = [&](size_t b) {
+    char *q = m;
+    m += b;
+    return q;
+  };
+  p.wf_state = (float4 *)take(b_state);
+  float4 *lists[2] = {(float4 *)take(b_list), (float4 *)take(b_list)};
+  p.wf_res = (float4 *)take(b_res);
+  p.wf_res_id = (float *)take(b_id);
+  p.wf_sh = (float4 *)take(b_sh);
+  p.wf_shres = (float4 *)take(b_shres);
+  uint32_t *cnts[2] = {(uint32_t *)take(b_cnt), (uint32_t *)take(b_cnt)};
+  p.wf_sh_cnt = (uint32_t *)take(b_cnt);
+  p.wf_ctr = (uint32_t *)take(256);
+  p.wf_R = (int32_t)kR;
+  p.wf_L = (int32_t)L;
+  p.wf_nregions = (int32_t)NR;
+  p.wf_apad = (uint32_t)apad;
+  p.wf_gx = grid.x;
+  const unsigned march_blocks = (unsigned)std::min<size_t>((size_t)c->jit.wf_march_blocks, (NR + 15) / 16);
+  const int rounds = p.max_bounces + 2;
+  for (int f0 = 0; f0 < p.nframes; f0 += fc) {
+    p.wf_f0 = f0;
+    p.wf_slots = (uint32_t)(apad * (size_t)std::min(fc, p.nframes - f0));
+    p.wf_nregions = (int32_t)((p.wf_slots + kR - 1) / kR);
+    for (int r = 0; r < rounds; r++) {
+      p.wf_round = r;
+      p.wf_in = lists[r & 1];
+      p.wf_in_cnt = cnts[r & 1];
+      p.wf_out = lists[(r + 1) & 1];
+      p.wf_out_cnt = cnts[(r + 1) & 1];
+      HIPCHK(c, rt0h::jit_launch(c->jit.wf_shade, &p, (unsigned)((p.wf_nregions + 3) / 4), 1, 1, c->stream) == RT0_OK
+                    ? hipSuccess
+                    : hipErrorLaunchFailure);
+      if (r + 1 < rounds)  // (the last round only finishes samples: nothing to march)
+        HIPCHK(c, rt0h::jit_launch(c->jit.wf_march, &p, std::max(1u, march_blocks), 1, 1, c->stream) == RT0_OK
+                      ? hipSuccess
+                      : hipErrorLaunchFailure);
+    }
+  }
+  return RT0_OK;
+}
+
 static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sync) {
   if (!c || n < 0) return RT0_E_ARG;
   if (!c->has_scene) return fail(c, RT0_E_STATE, "rt0_render before rt0_set_scene*");
@@ -764,9 +861,10 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   const bool want_walk = defer && nee_walk_enabled() && c->host_scene.n_models > 0 && c->n_tris > 0 &&
                          c->host_scene.n_sdfs == 0 && !c->host_scene.any_tex && c->cfg.render_mode == 0 &&
                          (size_t)grid.x * grid.y * 4 * 64 * (size_t)p.max_bounces < (1u << 29) - 1u;
+  const bool want_wf = wf_eligible(c);
   if (c->use_jit && !c->counting) {
-    if (c->jit_dirty || !c->jit.pass || (defer != (c->jit.nee != nullptr)) ||
-        (defer && want_walk != (c->jit.walk != nullptr))) {
+    if (c->jit_dirty || !(c->jit.pass || c->jit.wf_shade) || (defer != (c->jit.nee != nullptr)) ||
+        (defer && want_walk != (c->jit.walk != nullptr)) || want_wf != (c->jit.wf_shade != nullptr)) {
       rt0h::JitKey key = rt0h::make_jit_key(c->cfg, c->n_sdfs);
       if (c->exec_compat) key.flags |= F_EXEC_GHOST;
       key.halo_check = c->n_shards > 1 ? 1 : 0;
@@ -782,12 +880,15 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       }
       key.nee_regions = (int)nee_regions_per_wave();
       key.walk = want_walk ? 1 : 0;
+      key.wf = want_wf ? 1 : 0;
       int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
       c->jit_dirty = false;
     }
     jit_fn = c->jit.pass;
   }
+  // the module's kernels are the wavefront rounds (no pass kernel) for an eligible SDF scene
+  const bool wf_run = c->use_jit && !c->counting && c->jit.wf_shade != nullptr;
   const size_t pass_waves = (size_t)grid.x * grid.y * 4;
   if (defer) {
     // a region of 64 lanes x max_bounces records per pass wave: a path makes
@@ -919,6 +1020,23 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       p.frame0 = first + (uint32_t)k;
       p.nframes = (n - k) < c->max_frames_per_launch ? (n - k) : c->max_frames_per_launch;
       int chunks = std::min(want, p.nframes);
+      if (wf_run) {  // wavefront rounds: samples out, rt0_sum_kernel accumulates
+        const size_t need = (size_t)p.nframes * (p.vp_x1 - p.vp_x0) * (p.vp_y1 - p.vp_y0) * sizeof(float4);
+        if (need > c->samples_bytes) {
+          if (c->d_samples) HIPCHK(c, hipFree(c->d_samples));
+          c->d_samples = nullptr;
+          c->samples_bytes = 0;
+          HIPCHK(c, hipMalloc(&c->d_samples, need));
+          c->samples_bytes = need;
+        }
+        p.samples = c->d_samples;
+        p.frame_chunk = p.nframes;
+        int rc = wf_render(c, p, grid);
+        if (rc != RT0_OK) return rc;
+        HIPCHK(c, rt0_launch_sum(&p, grid, c->stream));
+        launches++;
+        continue;
+      }
       if (chunks > 1) {
         p.frame_chunk = (p.nframes + chunks - 1) / chunks;
         chunks = (p.nframes + p.frame_chunk - 1) / p.frame_chunk;
@@ -945,6 +1063,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   c->last_launches = launches;
+  c->last_path = wf_run ? RT0_PATH_WAVEFRONT : defer ? RT0_PATH_DEFERRED : jit_fn ? RT0_PATH_PASS : RT0_PATH_AOT;
   if (sync) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
@@ -1088,6 +1207,12 @@ int rt0_set_jit(rt0_ctx *c, int enable) {
   return RT0_OK;
 }
 
+int rt0_set_wavefront(rt0_ctx *c, int enable) {
+  if (!c) return RT0_E_ARG;
+  c->wavefront = enable != 0;  // the next render picks the matching JIT module
+  return RT0_OK;
+}
+
 int rt0_set_defer_light_sampling(rt0_ctx *c, int enable) {
   if (!c) return RT0_E_ARG;
   c->defer_nee = enable != 0;  // the next render picks the matching JIT module
@@ -1187,6 +1312,8 @@ int rt0_scratch_bytes(const rt0_ctx *c, size_t *bytes) {
   *bytes = c->samples_bytes;
   return RT0_OK;
 }
+
+int rt0_last_render_path(const rt0_ctx *c) { return c ? c->last_path : RT0_E_ARG; }
 
 int rt0_last_kernel_ms(const rt0_ctx *c, float *ms, int *launches) {
   if (!c) return RT0_E_ARG;

@@ -113,6 +113,12 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_BVH_STACK16  // BVH traversal stacks as 16-bit LDS entries + high bits in a register
 #define RT0_BVH_STACK16 0
 #endif
+// Wavefront SDF renders (rt0_jit_wf_shade / rt0_jit_wf_march, see
+// wf_shade_body): the scene-specialised modules of SDF scenes without ReSTIR
+// are compiled with 1 (rt0_jit.cpp JitKey::wf)
+#ifndef RT0_WAVEFRONT
+#define RT0_WAVEFRONT 0
+#endif
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
   return x - floorf(x);
@@ -258,7 +264,15 @@ struct March {
   float tmin, t, id;
   int i;
   bool active, done;
+  v3 n;  // RT0_WAVEFRONT: calcNormal at the hit, evaluated by the march kernel
 };
+
+// o + d*t as every march step and normal probe evaluates it: one fused
+// multiply-add per axis, written out so that every kernel (the pass kernel's
+// march, the wavefront march kernel) rounds it the same way
+DEV v3 ray_at(v3 o, v3 d, float t) {
+  return v3{__builtin_fmaf(d.x, t, o.x), __builtin_fmaf(d.y, t, o.y), __builtin_fmaf(d.z, t, o.z)};
+}
 
 // SDF primitives, raytracer.glsl:496-528, 642-698
 DEV float sdBox(v3 p, v3 b) {
@@ -397,6 +411,23 @@ struct BvhStack {
 DEV uint32_t *nee_wave_counter() {
   __shared__ uint32_t cnt[4];
   return cnt + (threadIdx.x >> 6);
+}
+// the wavefront shade kernel's append counters of this wave's region:
+// k = 0 the round's march list, 1 its shadow list
+DEV uint32_t *wf_wave_counter(int k) {
+  __shared__ uint32_t cnt[8];
+  return cnt + 4 * k + (threadIdx.x >> 6);
+}
+// append `n` entries for the active lanes of a (possibly divergent) call
+// site: one LDS add by the first active lane; returns this lane's position
+DEV uint32_t wave_append(uint32_t *ctr) {
+  const unsigned long long act = __ballot(1);
+  const int lane = (int)(threadIdx.x & 63u);
+  const int leader = __ffsll((long long)act) - 1;
+  const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(act));
+  return (uint32_t)__shfl((int)base, leader) + rank;
 }
 // closest triangle hit along (o, d) before tmin: depth-first, nearer child
 // first, the far child on the per-lane LDS stack.  Returns the leaf-order
@@ -720,25 +751,27 @@ struct Geometry {
       if (sc.n_sdfs() > 0) {  // iSDF, 974-993
         float t = EPSILON * 4.0f;
         float id = 0.f;
+        bool have_n = false;  // the wavefront march kernel's normal
         if (ms) {
           if (ms->active) return -1.0f;  // still being marched
           if (!ms->done) {
-            *ms = March{o, d, tmin, t, id, 0, true, false};
+            *ms = March{o, d, tmin, t, id, 0, true, false, mk(0.f, 0.f, 0.f)};
             return -1.0f;
           }
           t = ms->t;
           id = ms->id;
           ms->done = false;
+          have_n = RT0_WAVEFRONT != 0;
         } else {
           for (int i = 0; i < C.marching_steps(); ++i) {
-            float dist = map(sc, o + d * t, id, nmap);
+            float dist = map(sc, ray_at(o, d, t), id, nmap);
             float h = fabsf(dist);
             if (h < EPSILON || t > tmin) break;
-            t += h * C.fudge();
+            t = __builtin_fmaf(h, C.fudge(), t);  // (written out: every march kernel rounds it alike)
           }
         }
         if (!(t > tmin)) {
-          hit.n = calcNormal(sc, o + d * t, nmap);
+          hit.n = have_n ? ms->n : calcNormal(sc, ray_at(o, d, t), nmap);
           hit.index = sc.n_meshes() + (int)id;
           tmin = t;
           type = T_SDF;
@@ -1198,6 +1231,11 @@ struct Integrator {
   // scene-specialised Integrator gets them (pass_body, nee_body)
   const GeomRec *g_lds = nullptr;
   const MatRec *m_lds = nullptr, *ms_lds = nullptr;
+  // wavefront shade kernel (WF): this sample's path slot and region, and the
+  // light-sampling calls this bounce handed to the march kernel (one bit per
+  // light slot; wf_kind 1 = brdf()'s surface loop, 2 = the in-scatter loop)
+  uint32_t wf_slot = 0, wf_region = 0, wf_bits = 0;
+  int wf_kind = 0;
   DEV GeomRec geom_at(int i) const {
     if constexpr (Scene::kStatic) return g_lds[i];
     else return sc.geom(i);
@@ -1290,10 +1328,28 @@ struct Integrator {
     v3 c = vmaxs(mk(mh.cr, mh.cg, mh.cb), 0.001f);
     return (((c * mk(mh.er, mh.eg, mh.eb)) * weight) * fmaxf(0.001f, dot(sr, nl))) * T_fog;
   }
+  // The shadow ray of a wavefront shade kernel's light-sampling call
+  // (RT0_WAVEFRONT): direct_light evaluates the call with the ray's closest
+  // QUADRIC hit and returns the contribution that gives; the ray, that hit's
+  // t (the SDF march's bound) and whether a march that stops exactly at INF_T
+  // still lights it (a directional light) go to the march kernel, which keeps
+  // the contribution only if the march finds no SDF surface before the bound
+  // (wf_march_body).  Exact because no SDF of these scenes is a light
+  // (rt0_host.cpp wf_eligible): a winning SDF surface is never lit, and when
+  // the quadric hit gives nothing the SDF cannot give anything either.
+  struct WfShadow {
+    v3 o, d;
+    float tq;
+    bool dirl;
+  };
+  // the closest quadric hit only (intersection()'s mesh loop, no SDF march)
+  DEV float isect_q(v3 o, v3 d, Hit &h) {
+    return G::template intersect<false>(P, sc, C, o, d, h, n_map, nullptr, nullptr, g_lds);
+  }
   // (dyn: li is a per-lane index -- ReSTIR's chosen light -- read from the
   // LDS tables; otherwise a loop constant that folds)
   DEV v3 direct_light(int li, v3 x, v3 nl, float seed, March *ms = nullptr, bool *susp = nullptr,
-                      LightGeo *geo = nullptr, bool dyn = false) {
+                      LightGeo *geo = nullptr, bool dyn = false, WfShadow *wj = nullptr) {
     if (COUNT) ++n_nee;
     const GeomRec g = dyn ? geom_at(li) : sc.geom(li);
     const MatRec lm = dyn ? mat_at(li) : sc.mat(li);
@@ -1313,7 +1369,14 @@ struct Integrator {
           const int il = G::template shadow_light<Cfg>(P, sc, C, x + nl * EPSILON, sr, t, COUNT ? n_bvh : nullptr);
           return sphere_light_lit(il, t, cos_a_max, sr, nl);
         }
-        float t = isect(x + nl * EPSILON, sr, hit, ms);
+        const v3 so = x + nl * EPSILON;
+        float t;
+        if (wj) {
+          t = isect_q(so, sr, hit);
+          *wj = WfShadow{so, sr, t, false};
+        } else {
+          t = isect(so, sr, hit, ms);
+        }
         if (ms && t < 0.0f) {
           *susp = true;
           return dl;
@@ -1341,7 +1404,14 @@ struct Integrator {
       }
     } else if (lm.type == M_DIR_LIGHT) {
       v3 ld = mk(g.px, g.py, g.pz);
-      float t = isect(x + nl * EPSILON, ld, hit, ms);
+      const v3 so = x + nl * EPSILON;
+      float t;
+      if (wj) {
+        t = isect_q(so, ld, hit);
+        *wj = WfShadow{so, ld, t, true};
+      } else {
+        t = isect(so, ld, hit, ms);
+      }
       if (ms && t < 0.0f) {
         *susp = true;
         return dl;
@@ -2024,6 +2094,85 @@ struct Integrator {
   }
   DEV bool ghost_on() const { return RESTIR && (C.flags() & F_EXEC_GHOST) != 0; }
 
+  // ---- wavefront SDF renders (WF): light sampling as march jobs
+  // One shadow ray of light slot l whose answer matters: appended to this
+  // wave's region of the round's shadow list through the wave's LDS counter
+  // (any subset of lanes may append: one LDS add per call site).  c = the
+  // contribution if the march finds no SDF surface before tq (WfShadow).
+  DEV void wf_emit_shadow(int l, v3 o, v3 d, float tq, v3 c, bool dirl) {
+    const uint32_t i = wave_append(wf_wave_counter(1));  // < wf_R * wf_L: one job per light per slot
+    float4 *e = P.wf_sh + 3 * ((size_t)wf_region * (uint32_t)P.wf_R * (uint32_t)P.wf_L + i);
+    e[0] = make_float4(o.x, o.y, o.z, tq);
+    e[1] = make_float4(d.x, d.y, d.z, __uint_as_float((uint32_t)l * P.wf_slots + wf_slot));
+    e[2] = make_float4(c.x, c.y, c.z, dirl ? 1.0f : 0.0f);
+    wf_bits |= 1u << l;
+  }
+  // brdf()'s non-specular light sampling (raytracer.glsl:1899-1976, plain or
+  // MIS; ReSTIR is not in these modules): sample_lights' calls, each with
+  // its quadric answer, the surviving ones as march jobs
+  DEV void wf_nee_surface(v3 x, v3 nl, float seed, float bounce) {
+    if (flag(F_RESTIR)) return;  // (sample_lights: use_restir without USE_RESTIR adds nothing)
+    const float fr = (float)frame;
+    const float base = nc_seed4(seed, 8652.1f, fr, 5681.123f, bounce, 7895.13f);
+    wf_kind = 1;
+    for_lights(sc, [&](int i) {
+      const int idx = sc.light(i);
+      if (idx < 0) return;
+      WfShadow wj{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), -1.0f, false};
+      if (flag(F_MIS)) {
+        const GeomRec lg = sc.geom(idx);
+        const MatRec lmt = sc.mat(idx);
+        if (lmt.type != M_LIGHT) return;
+        LightGeo geo{false, 0.f, 0.f, 0.f, mk(0.f, 0.f, 0.f)};
+        const v3 ls = direct_light(idx, x, nl, nc_addmul(base, (float)i, 123.456f), nullptr, nullptr, &geo, false, &wj);
+        if (!(dot(ls, ls) > 0.000001f) || wj.tq < 0.0f) return;
+        float w;
+        if (geo.sphere && !flag(F_ANIM)) {  // (sample_lights' reuse of the sampling's d², cos θmax, direction)
+          float lp = 0.0f;
+          if (geo.d2 > geo.r2 && 1.0f - geo.cam >= 1e-6f) lp = frcp(TWO_PI * (1.0f - geo.cam));
+          w = power_heuristic(lp, cos_pdf(geo.ld, nl));
+        } else {
+          const v3 ld = normalize(lpos(idx, lg) - x);
+          w = power_heuristic(light_pdf(lg, lmt, x), cos_pdf(ld, nl));
+        }
+        wf_emit_shadow(i, wj.o, wj.d, wj.tq, ls * w, wj.dirl);
+      } else {
+        const v3 dl = direct_light(idx, x, nl, base, nullptr, nullptr, nullptr, false, &wj);
+        if ((dl.x != 0.0f || dl.y != 0.0f || dl.z != 0.0f) && wj.tq >= 0.0f) wf_emit_shadow(i, wj.o, wj.d, wj.tq, dl, wj.dirl);
+      }
+    });
+  }
+  // the in-scatter light loop of a volume event (raytracer.glsl:2011-2044):
+  // each light's term with its quadric answer, the lit ones as march jobs
+  DEV void wf_nee_volume(v3 sp, v3 rd, v3 mask, float seed, int depth) {
+    wf_kind = 2;
+    for_lights(sc, [&](int li) {
+      const int lidx = sc.light(li);
+      if (lidx < 0) return;
+      const GeomRec lg = sc.geom(lidx);
+      const MatRec lmt = sc.mat(lidx);
+      if (lmt.type != M_LIGHT || lg.type != T_SPHERE) return;
+      v3 dlc = mk(lg.px, lg.py, lg.pz) - sp;
+      float dc = length(dlc);
+      float cam = fsqrt(1.0f - fminf(fmaxf(fdiv(lg.d0, dc * dc), 0.0f), 1.0f));
+      float idc = frcp(dc);
+      v3 dir = sample_cone(mk(dlc.x * idc, dlc.y * idc, dlc.z * idc), 1.0f - cam,
+                           nc_addmul(nc_addmul(seed + 2341.7f, (float)li, 917.3f), (float)depth, 199.1f));
+      Hit sh;
+      const v3 so = sp + dir * (EPSILON * 20.0f);
+      float ts = isect_q(so, dir, sh);
+      if (sh.index != lidx) return;  // an SDF surface would only hide it
+      float omega = 2.0f * (1.0f - cam);
+      float ct = dot(rd, dir);
+      constexpr float g2 = VOL_G * VOL_G;
+      float den = 1.0f + g2 - 2.0f * VOL_G * ct;
+      float phase = fdiv(1.0f - g2, FOUR_PI * den * fsqrt(den));
+      float Tf = fexp(-VOL_SIGMA_T * ts);
+      const v3 c = ((((mask * mk(lmt.cr, lmt.cg, lmt.cb)) * mk(lmt.er, lmt.eg, lmt.eb)) * phase) * Tf) * (PI_F * omega);
+      wf_emit_shadow(li, so, dir, ts, c, false);
+    });
+  }
+
   // radiance() + brdf(), raytracer.glsl:1986-2105 and 1804-1980, as a step
   // function: one iteration of the bounce loop per call, so that a lane whose
   // path ended can start its next sample while the rest of its wave is still
@@ -2038,7 +2187,12 @@ struct Integrator {
   // phases: 0 = its ray (and the shading that follows), 1 = its light
   // sampling (one shadow ray per light), each resumable; every lane still
   // performs exactly the operations of the uninterrupted loop, in order.
-  static constexpr bool SUSP = SDF && !RESTIR && !COUNT;
+  // WF (RT0_WAVEFRONT modules): the same bounce step in the wavefront shade
+  // kernel -- a pending march parks the path (wf_shade_body) instead of
+  // suspending it, and the light-sampling calls' shadow rays become march
+  // jobs (wf_nee_surface / wf_nee_volume)
+  static constexpr bool WF = RT0_WAVEFRONT != 0 && SDF && !RESTIR && !COUNT;
+  static constexpr bool SUSP = SDF && !RESTIR && !COUNT && !WF;
   struct NeeCtx {
     v3 x, n, acc;  // surface: hit point, nl, sum over lights; volume: scatter point, incoming rd
     float seed;    // surface: the light-sampling seed base; volume: the path seed
@@ -2055,7 +2209,7 @@ struct Integrator {
     NeeCtx nc;
   };
   DEV March *march_slot(Path &ps) {
-    if constexpr (!SUSP) return nullptr;
+    if constexpr (!SUSP && !WF) return nullptr;
     // with triangle models the resumed call would walk the BVH again: no budget
     if constexpr (Scene::kMayHaveModels)
       if (sc.n_models() > 0 && P.n_tris > 0) return nullptr;
@@ -2074,13 +2228,13 @@ struct Integrator {
     const int lim = min(cap, i + RT0_MARCH_BUDGET);
     bool stop = i >= cap;
     for (; i < lim; ++i) {
-      float dist = G::map(sc, m.o + m.d * t, id, n_map);
+      float dist = G::map(sc, ray_at(m.o, m.d, t), id, n_map);
       float h = fabsf(dist);
       if (h < EPSILON || t > m.tmin) {
         stop = true;
         break;
       }
-      t += h * C.fudge();
+      t = __builtin_fmaf(h, C.fudge(), t);
     }
     if (i >= cap) stop = true;
     m.t = t;
@@ -2190,13 +2344,23 @@ struct Integrator {
     if (COUNT) ++n_iter;
     Hit hit;
     float t = isect(ro, rd, hit, march_slot(ps));
-    if (SUSP && t < 0.0f) return true;  // march pending: step() repeats this bounce once it is done
+    if ((SUSP || WF) && t < 0.0f) return true;  // march pending: step() repeats this bounce once it is done
     if constexpr (VOL) {
       if (flag(F_VOL)) {
         float sd = -flog(fmaxf(hash(nc_addmul(seed + 4729.3f, (float)depth, 991.1f)), 1e-6f)) / VOL_SIGMA_T;
         if (sd < fminf(INF_T, t)) {
           v3 sp = ro + rd * sd;
           mask = mask * (VOL_SIGMA_S / VOL_SIGMA_T);
+          if constexpr (WF) {  // the in-scatter light loop's shadow rays become march jobs
+            const v3 rd_in = rd;
+            rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
+            ro = sp;
+            spec = false;
+            ++scat_ev;
+            const bool stop = scat_ev >= C.max_scatter() || vmaxc(mask) < 0.01f;
+            if (flag(F_SAMPLE_LIGHTS)) wf_nee_volume(sp, rd_in, mask, seed, depth);
+            return stop ? false : ++ps.depth < C.max_bounces();
+          }
           if constexpr (SUSP) {  // the in-scatter NEE becomes phase 1 (it reads sp, the incoming rd and mask)
             const v3 rd_in = rd;
             rd = sample_hg(rd, nc_addmul(seed + 8293.7f, (float)depth, 773.3f));
@@ -2381,6 +2545,12 @@ struct Integrator {
         const T4 cm = cube_sample(P, sr);
         acc = acc + mask * mk(cm.r, cm.g, cm.b);
       }
+    }
+    if constexpr (WF) {  // light sampling's shadow rays become march jobs; the end tests do not depend on them
+      const bool end = vmaxc(mask) < 0.01f || diff_b >= C.max_diff() || spec_b >= C.max_spec() || 0 >= C.max_trans() ||
+                       scat_ev >= C.max_scatter();
+      if (!spec && flag(F_SAMPLE_LIGHTS)) wf_nee_surface(x, nl, seed, bounce);
+      return end ? false : ++ps.depth < C.max_bounces();
     }
     if constexpr (SUSP) {  // light sampling becomes phase 1; the end tests below do not depend on it
       const bool end = vmaxc(mask) < 0.01f || diff_b >= C.max_diff() || spec_b >= C.max_spec() || 0 >= C.max_trans() ||
@@ -2577,6 +2747,10 @@ DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int 
 
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  // (a wavefront module parks pending marches for its march kernel: its SDF
+  // paths cannot run here)
+  static_assert(!Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::WF,
+                "RT0_WAVEFRONT modules render SDF scenes through wf_shade_body / wf_march_body");
   const SceneTables tabs = scene_tables(sc);  // (before any thread leaves: one barrier)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
@@ -2969,6 +3143,297 @@ DEV void sum_body(const LaunchParams &P) {
     }
   }
   P.accum[pix] = a;
+}
+
+// ================================================== wavefront SDF renders
+// SDF scenes without ReSTIR (C4: the Mandelbulb in a medium) spend ~93% of
+// their FLOP in map() (raytracer.glsl:700-712), 17.7 calls per march
+// (iSDF, 974-993, plus calcNormal's 4, 714-722).  In the pass kernel the
+// marches run at a quarter of the lanes: a wave's lanes march rays of
+// different lengths, or shade, at the same time.  Here a pass is split into
+// rounds of two kernels over path slots (one slot = one pixel and frame of
+// the launch, so a launch's frames run side by side):
+//   rt0_jit_wf_shade: per slot, the bounce step of the pass kernel
+//     (Integrator::step) up to the next pending march: it consumes the
+//     previous round's march answers, adds the light-sampling results the
+//     march kernel returned, shades, and parks the path (its state in
+//     wf_state, its next ray as an entry of the region's march list, its
+//     light-sampling shadow rays as entries of the shadow list);
+//   rt0_jit_wf_march: persistent waves take regions off a device counter
+//     (one atomic per kRegionGroup regions) and march their entries with
+//     lanes that never wait for each other -- a lane whose march (or normal)
+//     is done takes the queue's next entry (ballot + prefix count), and every
+//     lane evaluates map() at one program point per loop trip, be it a
+//     sphere-tracing step or one of calcNormal's four probes.
+// A path takes one round per bounce, so a launch is MAX_BOUNCES + 2 rounds.
+// Every map() evaluation, the march's bound and stop tests and calcNormal's
+// sum are the pass kernel's (bit-identical steps); the light-sampling sums
+// are formed in call order in the next round (wf_apply_nee).  Samples go to
+// the frame-chunk planes and rt0_sum_kernel adds them in frame order.
+//
+// Path state, wf_state[k * wf_slots + slot]:
+//   k = 0: acc.xyz, mask.x;  1: mask.yz, packed bounce counters, light bits;
+//   2 (MIS or spectral): the previous bounce's normal, hero wavelength.
+// packed = depth | spec << 7 | diff_b << 8 | spec_b << 15 | scat_ev << 22 |
+//          kind << 29 (7-bit counters: MAX_BOUNCES <= 127, rt0_host.cpp)
+template <class Cfg, bool SPECTRAL>
+DEV constexpr bool wf_extra_state() {
+  return (Cfg::flags() & F_MIS) != 0u || (SPECTRAL && (Cfg::flags() & F_SPECTRAL) != 0u);
+}
+
+template <class Scene, class Cfg, bool VOL, bool SPECTRAL>
+DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  const SceneTables tabs = scene_tables(sc);  // (one barrier, before any wave leaves)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *P.wf_ctr = 0u;  // the march kernel's region counter
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
+  if (w >= (uint32_t)P.wf_nregions) return;
+  using It = Integrator<Scene, Cfg, false, VOL, true, SPECTRAL, false>;
+  constexpr bool kExtra = wf_extra_state<Cfg, SPECTRAL>();
+  const uint32_t R = (uint32_t)P.wf_R, S = P.wf_slots;
+  *(volatile uint32_t *)wf_wave_counter(0) = 0u;  // (every lane stores the same 0)
+  *(volatile uint32_t *)wf_wave_counter(1) = 0u;
+  const uint32_t n = P.wf_round == 0 ? R : P.wf_in_cnt[w];
+  const size_t rbase = (size_t)w * R;
+  for (uint32_t b = 0; b < n; b += 64u) {
+    const uint32_t e = b + lane;
+    if (e >= n) continue;
+    uint32_t slot;
+    v3 ro = mk(0.f, 0.f, 0.f), rd = ro;
+    bool marched = false;
+    if (P.wf_round == 0) {
+      slot = (uint32_t)rbase + e;
+      if (slot >= S) continue;
+    } else {
+      const float4 j0 = P.wf_in[2 * (rbase + e)], j1 = P.wf_in[2 * (rbase + e) + 1];
+      slot = __float_as_uint(j1.w);
+      ro = mk(j0.x, j0.y, j0.z);
+      rd = mk(j1.x, j1.y, j1.z);
+      marched = j0.w >= 0.0f;
+    }
+    // the slot's frame and pixel (pass_body's tile order within a frame)
+    const uint32_t f = slot / P.wf_apad, loc = slot - f * P.wf_apad;
+    const uint32_t tile = loc >> 8, tx = tile % P.wf_gx, ty = tile / P.wf_gx, wv = (loc >> 6) & 3u, ln = loc & 63u;
+    const int px = P.vp_x0 + (int)(tx * 16u + (ln & 7u) + ((wv & 1u) << 3));
+    const int r = P.vp_y0 + (int)(ty * 16u + (ln >> 3) + ((wv >> 1) << 3));
+    if (px >= P.vp_x1 || r >= P.vp_y1) continue;
+    const int py = image_row(P, r);
+    if (py >= P.height) continue;
+    It it(P, sc, cfg);
+    it.use_tables(tabs);
+    it.set_pixel(px, py);
+    it.frame = P.frame0 + (uint32_t)P.wf_f0 + f;
+    it.wf_slot = slot;
+    it.wf_region = w;
+    typename It::Path ps;
+    bool alive = true;
+    if (P.wf_round == 0) {
+      it.begin_sample(ps);
+      ps.phase = 0;
+      ps.ms.active = ps.ms.done = false;
+    } else {
+      const float4 s0 = P.wf_state[slot], s1 = P.wf_state[(size_t)S + slot];
+      const uint32_t pk = __float_as_uint(s1.z), bits = __float_as_uint(s1.w);
+      ps.ro = ro;
+      ps.rd = rd;
+      ps.acc = mk(s0.x, s0.y, s0.z);
+      ps.mask = mk(s0.w, s1.x, s1.y);
+      ps.prev_nl = mk(0.f, 1.f, 0.f);
+      if constexpr (kExtra) {
+        const float4 s2 = P.wf_state[2 * (size_t)S + slot];
+        ps.prev_nl = mk(s2.x, s2.y, s2.z);
+        it.hero = s2.w;
+      } else {
+        it.hero = 550.0f;
+      }
+      ps.seed = it.pixel_seed();
+      ps.depth = (int)(pk & 127u);
+      ps.spec = ((pk >> 7) & 1u) != 0u;
+      ps.phase = 0;
+      it.diff_b = (int)((pk >> 8) & 127u);
+      it.spec_b = (int)((pk >> 15) & 127u);
+      it.scat_ev = (int)((pk >> 22) & 127u);
+      // the previous bounce's light sampling, in call order (sample_lights:
+      // sum then x mask; the in-scatter loop: each term in turn)
+      if (bits) {
+        const int kind = (int)(pk >> 29);
+        v3 sum = mk(0.f, 0.f, 0.f);
+        for_lights(sc, [&](int l) {
+          if (!(bits & (1u << l))) return;
+          const float4 q = P.wf_shres[(size_t)l * S + slot];
+          if (kind == 2) ps.acc = ps.acc + mk(q.x, q.y, q.z);
+          else sum = sum + mk(q.x, q.y, q.z);
+        });
+        if (kind == 1) ps.acc = ps.acc + sum * ps.mask;
+      }
+      ps.ms.active = false;
+      ps.ms.done = marched;
+      if (marched) {
+        const float4 q = P.wf_res[rbase + e];
+        ps.ms.t = q.x;
+        ps.ms.n = mk(q.y, q.z, q.w);
+        ps.ms.id = Scene::kSdfs > 1 ? P.wf_res_id[rbase + e] : 0.0f;
+      }
+      alive = marched;
+    }
+    // the bounce this march answers, then the next bounce up to its march
+    if (alive) {
+      alive = it.step(ps);
+      if (alive && !ps.ms.active) alive = it.step(ps);
+    }
+    const bool pending = alive && ps.ms.active;
+    if (pending || it.wf_bits) {
+      const uint32_t pk = (uint32_t)ps.depth | (ps.spec ? 1u << 7 : 0u) | ((uint32_t)it.diff_b << 8) |
+                          ((uint32_t)it.spec_b << 15) | ((uint32_t)it.scat_ev << 22) | ((uint32_t)it.wf_kind << 29);
+      P.wf_state[slot] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, ps.mask.x);
+      P.wf_state[(size_t)S + slot] = make_float4(ps.mask.y, ps.mask.z, __uint_as_float(pk), __uint_as_float(it.wf_bits));
+      if constexpr (kExtra) P.wf_state[2 * (size_t)S + slot] = make_float4(ps.prev_nl.x, ps.prev_nl.y, ps.prev_nl.z, it.hero);
+      // the next round's entry: the march (bound < 0: none, only light sampling to add)
+      const uint32_t o = wave_append(wf_wave_counter(0));
+      const March &m = ps.ms;
+      P.wf_out[2 * (rbase + o)] = pending ? make_float4(m.o.x, m.o.y, m.o.z, m.tmin) : make_float4(0.f, 0.f, 0.f, -1.0f);
+      P.wf_out[2 * (rbase + o) + 1] = make_float4(m.d.x, m.d.y, m.d.z, __uint_as_float(slot));
+    } else {
+      const v3 col = it.finish(ps);
+      P.samples[(size_t)(P.wf_f0 + (int)f) * sample_plane(P) + sample_index(P, px, r)] = make_float4(col.x, col.y, col.z, 0.f);
+    }
+  }
+  // (the wave has reconverged: every append is counted)
+  if (lane == 0) {
+    P.wf_out_cnt[w] = *(volatile uint32_t *)wf_wave_counter(0);
+    P.wf_sh_cnt[w] = *(volatile uint32_t *)wf_wave_counter(1);
+  }
+}
+
+// The march kernel: persistent waves over the round's march and shadow lists.
+// A lane holds one entry: a closest-hit march (then, on a hit, calcNormal's
+// four probes) or a shadow march.  Each loop trip every busy lane evaluates
+// map() once; a lane that is done writes its answer and is refilled from the
+// wave's queue before the next trip.  The queue walks kRegionGroup regions
+// per device-counter grab; each region's march entries, then its shadow
+// entries.
+template <class Scene, class Cfg>
+DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  using G = Geometry<Scene>;
+  constexpr uint32_t kRegionGroup = 4;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t R = (uint32_t)P.wf_R, NR = (uint32_t)P.wf_nregions, RL = R * (uint32_t)P.wf_L;
+  const int cap = cfg.marching_steps();
+  const float fud = cfg.fudge();
+  // the wave's queue (wave-uniform): region reg of [reg, reg_end), entry q of its nall
+  uint32_t reg = 0, reg_end = 0, q = 0, nc = 0, nall = 0;
+  auto grab = [&]() {
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(P.wf_ctr, 1u);
+    g = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)g, 0));
+    reg = g * kRegionGroup;
+    reg_end = min(reg + kRegionGroup, NR);
+  };
+  auto open = [&]() {
+    q = 0;
+    nc = nall = 0;
+    if (reg < NR) {
+      nc = P.wf_out_cnt[reg];
+      nall = nc + P.wf_sh_cnt[reg];
+    }
+  };
+  grab();
+  open();
+  bool busy = false, shadow = false, dirl = false;
+  v3 o = mk(0.f, 0.f, 0.f), d = o, c = o, na = o;
+  float tmin = 0.f, t = 0.f, id = 0.f;
+  int i = 0, ph = 4;  // ph 4: sphere tracing; 0..3: calcNormal's probe ph
+  uint32_t idx = 0;
+  // a march has stopped (iSDF's loop exit): a closest-hit march that found
+  // the surface goes on to its normal, every other entry is answered
+  auto stopped = [&]() {
+    const bool hit = !(t > tmin);
+    if (!shadow && hit) {
+      ph = 0;
+      return;
+    }
+    if (shadow) {
+      const bool lit = !hit || (dirl && t == INF_T);
+      P.wf_shres[idx] = lit ? make_float4(c.x, c.y, c.z, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      P.wf_res[idx] = make_float4(t, 0.f, 0.f, 0.f);
+    }
+    busy = false;
+  };
+  while (true) {
+    uint64_t fr = __ballot(!busy);
+    while (fr != 0ull && reg < NR) {
+      if (q >= nall) {
+        if (++reg >= reg_end) grab();
+        open();
+        continue;
+      }
+      const uint32_t take = min((uint32_t)__popcll(fr), nall - q);
+      const uint32_t rank = (uint32_t)__popcll(fr & lt);
+      if (!busy && rank < take) {
+        const uint32_t j = q + rank;
+        if (j < nc) {
+          const size_t b = (size_t)reg * R + j;
+          const float4 j0 = P.wf_out[2 * b], j1 = P.wf_out[2 * b + 1];
+          o = mk(j0.x, j0.y, j0.z);
+          tmin = j0.w;
+          d = mk(j1.x, j1.y, j1.z);
+          idx = (uint32_t)b;
+          shadow = false;
+          busy = tmin >= 0.0f;  // (an entry without a march: only its light sampling goes on)
+        } else {
+          const size_t b = 3 * ((size_t)reg * RL + (j - nc));
+          const float4 e0 = P.wf_sh[b], e1 = P.wf_sh[b + 1], e2 = P.wf_sh[b + 2];
+          o = mk(e0.x, e0.y, e0.z);
+          tmin = e0.w;
+          d = mk(e1.x, e1.y, e1.z);
+          idx = __float_as_uint(e1.w);
+          c = mk(e2.x, e2.y, e2.z);
+          dirl = e2.w != 0.0f;
+          shadow = true;
+          busy = true;
+        }
+        t = EPSILON * 4.0f;
+        id = 0.0f;
+        i = 0;
+        ph = 4;
+        if (busy && cap <= 0) stopped();  // (MARCHING_STEPS 0: no step at all)
+      }
+      q += take;
+      fr = __ballot(!busy);
+    }
+    if (__ballot(busy) == 0ull) break;  // the queue is dry and every lane answered
+    if (busy) {
+      const v3 hp = ray_at(o, d, t);
+      // calcNormal's probe ph: pos + (s.x, s.y, s.z) * EPSILON, times the same signs
+      const float sx = (ph == 0 || ph == 3) ? 1.0f : -1.0f, sy = ph >= 2 ? 1.0f : -1.0f,
+                  sz = (ph == 1 || ph == 3) ? 1.0f : -1.0f;
+      const v3 p = ph < 4 ? mk(hp.x + sx * EPSILON, hp.y + sy * EPSILON, hp.z + sz * EPSILON) : hp;
+      float idm;
+      unsigned long long nm = 0;
+      const float dist = G::map(sc, p, idm, nm);
+      if (ph == 4) {
+        id = idm;
+        const float h = fabsf(dist);
+        bool stop = h < EPSILON || t > tmin;
+        if (!stop) {
+          t = __builtin_fmaf(h, fud, t);
+          stop = ++i >= cap;
+        }
+        if (stop) stopped();
+      } else {
+        const v3 sv = mk(sx, sy, sz) * dist;
+        na = ph == 0 ? sv : na + sv;
+        if (++ph == 4) {
+          const v3 n = normalize(na);
+          P.wf_res[idx] = make_float4(t, n.x, n.y, n.z);
+          if constexpr (Scene::kSdfs > 1) P.wf_res_id[idx] = id;
+          busy = false;
+        }
+      }
+    }
+  }
 }
 
 }  // namespace rt0

@@ -72,6 +72,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
   if (k.defer && k.walk) o << "#define RT0_NEE_WALK 1\n";
   if (k.bvh_stack > 0 && k.stack16) o << "#define RT0_BVH_STACK16 1\n";
+  if (k.wf) o << "#define RT0_WAVEFRONT 1\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
   // occupancy target below); with a BVH the extra registers cost more than
@@ -170,6 +171,17 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "__attribute__((amdgpu_waves_per_eu(" << (k.stack16 && k.bvh_stack > 0 ? 8 : 6) << "))) ";
   else if (k.restir && !k.defer)
     o << "__attribute__((amdgpu_waves_per_eu(4))) ";
+  if (k.wf) {
+    // wavefront SDF rounds (rt0_integrator.h wf_shade_body): no pass kernel
+    o << "void rt0_jit_wf_shade(const LaunchParams P) {\n"
+         "  rt0::wf_shade_body<rt0::JitScene, rt0::JitCfg, "
+      << vol << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    o << "extern \"C\" __global__ __launch_bounds__(256) ";
+    if (const char *e = getenv("RT0_JIT_MARCH_WAVES_PER_EU")) o << "__attribute__((amdgpu_waves_per_eu(" << atoi(e) << "))) ";
+    o << "void rt0_jit_wf_march(const LaunchParams P) {\n"
+         "  rt0::wf_march_body<rt0::JitScene, rt0::JitCfg>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    return o.str();
+  }
   o << "void rt0_jit_pass(const LaunchParams P) {\n"
        "  rt0::pass_body<rt0::JitScene, rt0::JitCfg, "
     << rt << ", " << vol << ", " << sdf << ", " << spc << ", false>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
@@ -329,8 +341,20 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
   if (rc != RT0_OK) return rc;
   CacheEntry e;
   hipFunction_t f[4] = {};
-  bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess &&
-            hipModuleGetFunction(&f[0], e.mod, "rt0_jit_pass") == hipSuccess;
+  bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
+  if (ok && k.wf) {
+    hipFunction_t s = nullptr, m = nullptr;
+    int per_cu = 0, cus = 0;
+    ok = hipModuleGetFunction(&s, e.mod, "rt0_jit_wf_shade") == hipSuccess &&
+         hipModuleGetFunction(&m, e.mod, "rt0_jit_wf_march") == hipSuccess &&
+         hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m, 256, 0) == hipSuccess &&
+         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess;
+    e.fns.wf_shade = (void *)s;
+    e.fns.wf_march = (void *)m;
+    e.fns.wf_march_blocks = std::max(1, per_cu) * std::max(1, cus);
+  } else if (ok) {
+    ok = hipModuleGetFunction(&f[0], e.mod, "rt0_jit_pass") == hipSuccess;
+  }
   if (ok && k.defer)
     ok = hipModuleGetFunction(&f[1], e.mod, "rt0_jit_nee") == hipSuccess &&
          hipModuleGetFunction(&f[2], e.mod, "rt0_jit_resolve") == hipSuccess;
@@ -340,7 +364,7 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
     err = "hipModuleLoadData/GetFunction failed for the JIT module";
     return RT0_E_HIP;
   }
-  e.fns.pass = (void *)f[0];
+  e.fns.pass = (void *)f[0];  // (null for a wavefront key)
   e.fns.nee = (void *)f[1];
   e.fns.resolve = (void *)f[2];
   e.fns.walk = (void *)f[3];
@@ -471,6 +495,13 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     key.walk = key.defer && nm > 0 && ns == 0 && !s.any_tex && !(key.flags & F_ANIM) && (!wk || atoi(wk) != 0) ? 1 : 0;
     // (the tree's depth and size are unknown here: RT0_BVH_STACK16=1 and
     // RT0_JIT_STACK=<entries> select what rt0_render would for such a tree)
+    // the wavefront rounds rt0_render uses for such a scene (rt0_host.cpp wf_eligible)
+    const char *wfe = getenv("RT0_WAVEFRONT");
+    bool wf = (!wfe || atoi(wfe) != 0) && !key.restir && ns > 0 && nm == 0 && s.n_lights <= 32 && key.max_bounces >= 1 &&
+              key.max_bounces <= 127;
+    for (int i = ne; i < ne + ns; i++) wf = wf && s.mat[i].type != 0;
+    for (int i = 0; i < s.n_lights; i++) wf = wf && s.light_index[i] < ne;
+    key.wf = wf ? 1 : 0;
     const char *w16 = getenv("RT0_BVH_STACK16"), *st = getenv("RT0_JIT_STACK");
     key.stack16 = w16 && atoi(w16) != 0 ? 1 : 0;
     if (st && nm > 0) key.bvh_stack = atoi(st);

@@ -29,8 +29,8 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_render_async", "rt0_sync", "rt0_read_accum", "rt0_write_accum", "rt0_clear", "rt0_resize",
            "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_accum_buffer_compact", "rt0_set_restir_buffers", "rt0_device_restir",
-           "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_set_executor_compat", "rt0_set_defer_light_sampling", "rt0_jit_compile", "rt0_set_counting",
-           "rt0_read_counters", "rt0_read_counters_n", "rt0_last_kernel_ms", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
+           "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_set_executor_compat", "rt0_set_defer_light_sampling", "rt0_set_wavefront", "rt0_jit_compile", "rt0_set_counting",
+           "rt0_read_counters", "rt0_read_counters_n", "rt0_last_kernel_ms", "rt0_last_render_path", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
            "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read",
            "rt0_set_temporal_frames", "rt0_set_viewport", "rt0_scratch_bytes"]
 
@@ -128,12 +128,14 @@ def lib():
         "rt0_set_jit": (c_int, [c_void_p, c_int]),
         "rt0_set_executor_compat": (c_int, [c_void_p, c_int]),
         "rt0_set_defer_light_sampling": (c_int, [c_void_p, c_int]),
+        "rt0_set_wavefront": (c_int, [c_void_p, c_int]),
         "rt0_jit_compile": (c_int, [ctypes.c_char_p, P(ctypes.c_char_p), c_int, P(Config), P(ctypes.c_size_t),
                                     ctypes.c_char_p, ctypes.c_size_t]),
         "rt0_set_counting": (c_int, [c_void_p, c_int]),
         "rt0_read_counters": (c_int, [c_void_p, P(ctypes.c_uint64)]),
         "rt0_read_counters_n": (c_int, [c_void_p, P(ctypes.c_uint64), c_int]),
         "rt0_last_kernel_ms": (c_int, [c_void_p, P(c_float), P(c_int)]),
+        "rt0_last_render_path": (c_int, [c_void_p]),
         "rt0_scratch_bytes": (c_int, [c_void_p, P(ctypes.c_size_t)]),
         "rt0_version": (ctypes.c_char_p, []),
         "rt0_tonemap_ex": (c_int, [c_void_p, c_float, c_int, P(ctypes.c_uint8)]),
@@ -535,6 +537,10 @@ class Renderer:
         default on."""
         self._chk(lib().rt0_set_defer_light_sampling(self.h, int(bool(on))))
 
+    def set_wavefront(self, on):
+        """Wavefront rounds for SDF scenes (rt0_set_wavefront); default on."""
+        self._chk(lib().rt0_set_wavefront(self.h, int(bool(on))))
+
     def set_counting(self, on):
         self._chk(lib().rt0_set_counting(self.h, int(bool(on))))
 
@@ -553,6 +559,13 @@ class Renderer:
         n = ctypes.c_size_t()
         self._chk(lib().rt0_scratch_bytes(self.h, ctypes.byref(n)))
         return n.value
+
+    PATHS = {1: "aot", 2: "pass", 3: "deferred", 4: "wavefront"}
+
+    def last_render_path(self):
+        """Kernels of the last render (rt0_last_render_path): 'aot', 'pass',
+        'deferred' or 'wavefront' (None before any render)."""
+        return self.PATHS.get(lib().rt0_last_render_path(self.h))
 
     def last_kernel_ms(self):
         ms, n = ctypes.c_float(), ctypes.c_int()
