@@ -37,7 +37,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement) with
 `roofline` (VALU FP32: algorithmic FLOP/sample from SURVEY 8d x counted events,
 over the kernel's HIP-event time; HBM traffic from the committed PMC passes)
 and, at N=1, `cpu_baseline` (the JS CPU integrator
-oracle/js/rt0_cpu.js on node worker_threads, bounded sample of the same
+raytracer-0_amd/js/rt0_cpu.js on node worker_threads, bounded sample of the same
 workload) with the C restatement oracle/rt0_oracle.c (OpenMP) beside it as
 `cpu_baseline_c`.  Only those two baseline legs touch oracle/.
 """
@@ -133,7 +133,7 @@ def host_threads():
 
 # ------------------------------------------------------------ CPU baselines
 def cpu_baseline_js(wl, budget_s=10.0):
-    """SURVEY 8d's CPU baseline: the JS CPU integrator (oracle/js/rt0_cpu.js,
+    """SURVEY 8d's CPU baseline: the JS CPU integrator (raytracer-0_amd/js/rt0_cpu.js,
     fp32 restatement of the same integrator, parity-checked in
     tests/test_cpu_js.py) on node worker_threads, timed on a bounded sample of
     the same workload: a 64-row band through the image centre, successive
@@ -179,7 +179,7 @@ def cpu_baseline_js(wl, budget_s=10.0):
         return {"error": r.stderr[-300:]}
     d = json.loads(r.stdout)
     return {"value": d["msamples_s"], "unit": "Msamples/s", "cores": d["threads"], "kind": "port",
-            "sample": "oracle/js/rt0_cpu.js (JS CPU integrator, node %s worker_threads x%d, %s): rows %d..%d of "
+            "sample": "raytracer-0_amd/js/rt0_cpu.js (JS CPU integrator, node %s worker_threads x%d, %s): rows %d..%d of "
                       "the %dx%d bench image%s, successive passes, %d samples in %.1f s"
                       % (d["node"], d["threads"], d["cpu"], r0, r0 + rows - 1, W, H, what, d["samples"], d["seconds"])}
 

@@ -1,6 +1,7 @@
 'use strict';
-// cpu_bench.js -- the JS CPU integrator (rt0_cpu.js) on worker_threads.
-// BASELINE / TEST INFRASTRUCTURE ONLY (see rt0_cpu.js).
+// cpu_bench.js -- the JS CPU integrator (raytracer-0_amd/js/rt0_cpu.js, the
+// product's CPU backend) on worker_threads, for bench.py's cpu_baseline and
+// the tests.  BASELINE / TEST INFRASTRUCTURE ONLY.
 //
 // node cpu_bench.js <configs.json> <config> <W> <H> <threads> <mode> ...
 //   mode "image" <frame0> <n> <out.f32>  : passes frame0..frame0+n-1 of the whole
@@ -26,7 +27,7 @@ const os = require('os');
 const fs = require('fs');
 const path = require('path');
 const { Worker, isMainThread, parentPort, workerData } = require('worker_threads');
-const { CpuRenderer } = require('./rt0_cpu.js');
+const { CpuRenderer } = require(path.join(__dirname, '..', '..', 'raytracer-0_amd', 'js', 'rt0_cpu.js'));
 
 function makeRenderer(d) {
   const cfgs = JSON.parse(fs.readFileSync(d.configs, 'utf8'));

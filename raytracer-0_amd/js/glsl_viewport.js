@@ -9,11 +9,43 @@
  * pipeline is replaced by the rt0 C ABI (include/rt0.h) through the N-API
  * addon rt0.node: a change of defines/constants/scene is picked up at the next
  * render() (the reference needs recompile(), index.html:1167-1196).
- * There is no CPU fallback: without a HIP device the constructor throws.
+ * Backends: opts.backend = 'hip' (default) renders through librt0 on an
+ * MI355X -- without a HIP device the constructor throws, there is no silent
+ * fallback; opts.backend = 'cpu' renders with the JS integrator on the host
+ * (cpu_backend.js; BASELINE configs[0], the reference's "JS CPU fallback").
  */
 const path = require('path');
 
-const addon = require(path.join(__dirname, 'rt0.node'));
+let _addon = null;
+function addonModule() {  // loaded on first use: the CPU backend needs no librt0
+  if (!_addon) _addon = require(path.join(__dirname, 'rt0.node'));
+  return _addon;
+}
+
+// The HIP backend: the N-API addon's calls on one librt0 context
+class AddonBackend {
+  constructor(width, height, device) {
+    this.kind = 'hip';
+    this.a = addonModule();
+    this.h = this.a.create(width, height, device);
+  }
+  setExecutorCompat(on) { this.a.setExecutorCompat(this.h, on); }
+  setCubemap(size, faces) { this.a.setCubemap(this.h, size, faces); }
+  setTexture(unit, w, h, data) { this.a.setTexture(this.h, unit, w, h, data); }
+  setConfig(defines, constants) { this.a.setConfig(this.h, defines, constants); }
+  setScene(scene, sdf) { this.a.setScene(this.h, scene, sdf); }
+  setCamera(pos, look, params) { this.a.setCamera(this.h, pos, look, params); }
+  setViewport(x, y, w, h) { this.a.setViewport(this.h, x, y, w, h); }
+  setTemporalFrames(n) { this.a.setTemporalFrames(this.h, n); }
+  render(first, n, t) { this.a.render(this.h, first, n, t); }
+  clear() { this.a.clear(this.h); }
+  resize(w, h) { this.a.resize(this.h, w, h); }
+  readAccum() { return this.a.readAccum(this.h); }
+  tonemap(cont) { return this.a.tonemap(this.h, cont); }
+  lastKernelMs() { return this.a.lastKernelMs(this.h); }
+}
+
+function readImage(p) { return addonModule().readImage(p); }
 
 // vector.js:2-95, the part the camera uses
 class Vector3 {
@@ -122,10 +154,19 @@ class GlslViewport {
     this.tile_size = [32, 32];
     this.total_tiles = [Math.ceil(this.canvas.width / 32) - 1, Math.ceil(this.canvas.height / 32) - 1];
     this.viewport = this.tile_rendering ? [0, 0, 32, 32] : [0, 0, this.canvas.width, this.canvas.height];
-    this._h = addon.create(this.canvas.width, this.canvas.height, this.device);
+    const backend = opts.backend || 'hip';
+    if (backend === 'cpu') {
+      const { CpuBackend } = require(path.join(__dirname, 'cpu_backend.js'));
+      this._b = new CpuBackend(this.canvas.width, this.canvas.height);
+    } else if (backend === 'hip') {
+      this._b = new AddonBackend(this.canvas.width, this.canvas.height, this.device);
+    } else {
+      throw new Error("opts.backend must be 'hip' or 'cpu'");
+    }
+    this.backend = this._b.kind;
     // opts.executorCompat: ReSTIR reservoirs as the reference's GLES executor
     // stores them (rt0_set_executor_compat); default GLSL semantics
-    if (opts.executorCompat) addon.setExecutorCompat(this._h, true);
+    if (opts.executorCompat) this._b.setExecutorCompat(true);
     this._compiled = null;
     this.images = {};
     // index.js:256-296: the RGBA noise image (u_rnd_tex) and opts.textures[0..3]
@@ -141,11 +182,11 @@ class GlslViewport {
 
   loadCubemap(faces) {
     if (!faces) {
-      addon.setCubemap(this._h, 0, null);
+      this._b.setCubemap(0, null);
       return;
     }
     const rgb = faces.map((f) => {
-      const img = typeof f === 'string' ? addon.readImage(f) : f;
+      const img = typeof f === 'string' ? readImage(f) : f;
       const n = img.width * img.height;
       if (img.data.length === n * 3) return { img, data: img.data };
       const d = new Uint8Array(n * 3);
@@ -157,7 +198,7 @@ class GlslViewport {
     const size = rgb[0].img.width;
     if (rgb.length !== 6 || rgb.some((f) => f.img.width !== size || f.img.height !== size))
       throw new Error('cubemap: six square faces of one size expected');
-    addon.setCubemap(this._h, size, rgb.map((f) => f.data));
+    this._b.setCubemap(size, rgb.map((f) => f.data));
     rgb.forEach((f, i) => { this.images['cubemap_img' + i] = f.img; });
   }
 
@@ -166,12 +207,12 @@ class GlslViewport {
     const name = (opts && opts.name) || 'tex0';
     const unit = name === 'rnd_tex' ? 4 : Number(name.replace('tex', ''));
     if (!(unit >= 0 && unit <= 4)) throw new Error('unknown texture unit ' + name);
-    if (typeof img === 'string') img = addon.readImage(img);
+    if (typeof img === 'string') img = readImage(img);
     if (img === null) {
-      addon.setTexture(this._h, unit, 0, 0, null);
+      this._b.setTexture(unit, 0, 0, null);
       return;
     }
-    addon.setTexture(this._h, unit, img.width, img.height, img.data);
+    this._b.setTexture(unit, img.width, img.height, img.data);
     this.images[name === 'rnd_tex' ? 'rnd_img' : 'img' + unit] = img;
   }
 
@@ -179,12 +220,12 @@ class GlslViewport {
   updateFrontTarget() {
     const key = JSON.stringify([this.defines, this.constants, this.scene, this.sdf_meshes]);
     if (key !== this._compiled) {
-      addon.setConfig(this._h, this.defines, this.constants);
-      addon.setScene(this._h, this.scene, this.sdf_meshes);
+      this._b.setConfig(this.defines, this.constants);
+      this._b.setScene(this.scene, this.sdf_meshes);
       this._compiled = key;
     }
     const c = this.camera;
-    addon.setCamera(this._h, [c.origin.x, c.origin.y, c.origin.z], [c.lookat.x, c.lookat.y, c.lookat.z],
+    this._b.setCamera([c.origin.x, c.origin.y, c.origin.z], [c.lookat.x, c.lookat.y, c.lookat.z],
       [c.fov, c.aperture, c.focalLength]);
   }
 
@@ -197,27 +238,27 @@ class GlslViewport {
     this.updateFrontTarget();
     const t = timeMs === undefined ? Date.now() - this.loadTime : timeMs;
     const vp = this.tile_rendering ? this.viewport : [0, 0, this.canvas.width, this.canvas.height];
-    addon.setViewport(this._h, vp[0], vp[1], vp[2], vp[3]);
+    this._b.setViewport(vp[0], vp[1], vp[2], vp[3]);
     if (!this.animatedScene) {
-      addon.render(this._h, this.passes + 1, n, t);
+      this._b.render(this.passes + 1, n, t);
       this.passes += n;
       return;
     }
-    addon.setTemporalFrames(this._h, this.temporalFrames);
+    this._b.setTemporalFrames(this.temporalFrames);
     for (let k = 0; k < n; k++) {
       if (this.passes > this.temporalFrames * 2) this.passes = this.temporalFrames;
-      addon.render(this._h, ++this.passes, 1, t);
+      this._b.render(++this.passes, 1, t);
     }
   }
 
   // index.js:822-880
-  clear() { addon.clear(this._h); }
+  clear() { this._b.clear(); }
 
   // index.js:471-493
   resize(v) {
     const size = { 0: 256, 1: 512, 2: 1024, 3: 2048, 4: 4096, 5: 8192 }[v] || v;
     this.canvas.width = this.canvas.height = size;
-    addon.resize(this._h, size, size);
+    this._b.resize(size, size);
     this.passes = 0;
     this.total_tiles = [Math.ceil(size / this.tile_size[0]) - 1, Math.ceil(size / this.tile_size[1]) - 1];
   }
@@ -268,13 +309,13 @@ class GlslViewport {
     this.clear();
   }
 
-  accumulator() { return addon.readAccum(this._h); }
+  accumulator() { return this._b.readAccum(); }
 
   // display pass (tonemapper.glsl:28-33) with u_cont = 1/passes, 1 when animated (index.js:1080-1090)
-  image() { return addon.tonemap(this._h, this.animatedScene ? 1.0 : 1.0 / Math.max(1, this.passes)); }
+  image() { return this._b.tonemap(this.animatedScene ? 1.0 : 1.0 / Math.max(1, this.passes)); }
 
-  lastKernelMs() { return addon.lastKernelMs(this._h); }
+  lastKernelMs() { return this._b.lastKernelMs(); }
 }
 
 module.exports = { GlslViewport, Vector3, sceneFromLines, sdfStatement, STATIC_CONSTANTS, ANIMATED_CONSTANTS,
-  CORNELL_LINES, addon };
+  CORNELL_LINES, get addon() { return addonModule(); } };

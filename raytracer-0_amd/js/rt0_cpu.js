@@ -1,18 +1,19 @@
 'use strict';
-// rt0_cpu.js -- the raytracer-0 integrator restated in JavaScript for the CPU.
-//
-// TEST / BASELINE INFRASTRUCTURE ONLY (SURVEY 8d: "the JS CPU integrator ...
-// timed on the GPU box's host in the same run").  The product (librt0.so) never
-// calls this; bench.py times it as `cpu_baseline`, tests/test_cpu_js.py checks
-// it against the C oracle (oracle/rt0_oracle.c), which is pinned to the
-// reference's golden fixtures.
+// rt0_cpu.js -- the raytracer-0 integrator in JavaScript for the CPU: the
+// product's CPU backend of GlslViewport (glsl_viewport.js, opts.backend =
+// 'cpu'; BASELINE configs[0], "JS CPU integrator path (no GPU)") and the
+// integrator bench.py times as `cpu_baseline` (SURVEY 8d).  It is chosen
+// explicitly, never as a silent fallback: without a HIP device the GPU
+// backend throws.  Checked against the reference's golden fixtures and the C
+// restatement (oracle/rt0_oracle.c, the checker) by tests/test_cpu_js.py; it
+// imports nothing from oracle/.
 //
 // It follows shaders/pathtracing/raytracer.glsl (line numbers cited per
 // function) in fp32: every operation is rounded with Math.fround, and the RNG
 // reproduces the reference executor's uint->float conversion, so frame k of a
-// pixel draws the same random numbers as the reference.  Scope: the C1/C2/C4
-// configs -- planes, spheres, boxes, SDFs (every #sdf_meshes kind, sphere-traced
-// with calcNormal), every untextured material, sky, plain NEE, MIS, SDF lights,
+// pixel draws the same random numbers as the reference.  Scope: planes,
+// spheres, boxes, SDFs (every #sdf_meshes kind, sphere-traced with
+// calcNormal), every untextured material, sky, plain NEE, MIS, SDF lights,
 // homogeneous volumetrics (free-flight sampling, in-scatter NEE, HG phase, fog
 // transmittance), ReSTIR in RENDER_MODE 0 (sampleLightsReSTIR with its
 // candidates, two-level temporal history, spatial taps, finalize, MRT packing:
@@ -23,7 +24,7 @@
 // commented-out Moller-Trumbore iTriangle of 864-892 over every triangle, as
 // the C restatement runs it -- the reference has no triangle path at all),
 // under GLSL semantics.  Animated-mode, cubemap and texture configs are
-// rejected (the C oracle covers them).
+// rejected ("outside the JS CPU integrator"; the HIP backend renders them).
 const f = Math.fround;
 
 // ------------------------------------------------------------------ RNG
@@ -227,8 +228,8 @@ function parseScene(lines) {
   lines.forEach((line, i) => {
     const parts = line.split(',');
     const mat = parts[0].trim(), type = parts[1].trim();
-    if (!(mat in MATS)) throw new Error('unsupported material for the JS baseline: ' + mat);
-    if (!(type in TYPES)) throw new Error('unsupported mesh type for the JS baseline: ' + type);
+    if (!(mat in MATS)) throw new Error('unsupported material for the JS CPU integrator: ' + mat);
+    if (!(type in TYPES)) throw new Error('unsupported mesh type for the JS CPU integrator: ' + type);
     if (mat.indexOf('MAT_LIGHT') >= 0) lights.push(i);
     const rest = parts.slice(2).join(',');
     const p = parseVec(rest, 3), j = parseVec(p.rest, 4);
@@ -287,7 +288,7 @@ class CpuRenderer {
   // cfg: a tests/golden/configs.json entry; cornell: cfgs.cornell_lines; camera default
   constructor(cfg, cornellLines, defaultCamera, width, height) {
     const defs = Object.assign({ USE_PROCEDURAL_SKY: true, USE_BIASED_SAMPLING: true }, cfg.defines || {});
-    if (defs.USE_CUBEMAP) throw new Error('USE_CUBEMAP is outside the JS baseline');
+    if (defs.USE_CUBEMAP) throw new Error('USE_CUBEMAP is outside the JS CPU integrator');
     this.spectral = !!defs.USE_SPECTRAL;
     this.hero = f(550);
     const c = Object.assign({
@@ -295,7 +296,7 @@ class CpuRenderer {
       sample_lights: true, use_mis: false, use_restir: false, MARCHING_STEPS: 128, FUDGE_FACTOR: 0.9,
       RESTIR_SAMPLES: 16, RENDER_MODE: 0,
     }, cfg.constants || {});
-    if (c.RENDER_MODE !== 0) throw new Error('RENDER_MODE 1 is outside the JS baseline');
+    if (c.RENDER_MODE !== 0) throw new Error('RENDER_MODE 1 is outside the JS CPU integrator');
     this.restir = !!c.use_restir;
     this.restirDef = !!defs.USE_RESTIR;
     this.restirSamples = c.RESTIR_SAMPLES;

@@ -20,7 +20,10 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
-GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve")
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_march")
+# a wavefront SDF launch (rt0_integrator.h wf_shade_body): MAX_BOUNCES + 2
+# shade and MAX_BOUNCES + 1 march dispatches, then one rt0_sum_kernel
+WF = ("rt0_jit_wf_shade", "rt0_jit_wf_march")
 
 
 def main():
@@ -33,7 +36,16 @@ def main():
            for k in GROUP}
     pas = dur[KERNEL]
     per_kernel = {}
-    if dur["rt0_jit_nee"]:  # deferred passes: pass + nee (+ walk) + resolve, one of each per pass
+    sums = [float(r["End_Timestamp"]) - float(r["Start_Timestamp"]) for r in rows
+            if r["Kernel_Name"].strip().startswith("rt0_sum_kernel")]
+    if dur["rt0_jit_wf_march"] and sums:  # wavefront launches: every dispatch of the launch + its sum, per launch
+        nl = len(sums)
+        per = {k: len(dur[k]) // nl for k in WF}
+        pas = [sum(sum(dur[k][i * per[k]:(i + 1) * per[k]]) for k in WF) + sums[i] for i in range(nl)]
+        per_kernel = {k: statistics.median([sum(dur[k][i * per[k]:(i + 1) * per[k]]) for i in range(skip, nl)]) / 1e6
+                      for k in WF if nl > skip}
+        per_kernel["dispatches_per_launch"] = per
+    elif dur["rt0_jit_nee"]:  # deferred passes: pass + nee (+ walk) + resolve, one of each per pass
         ks = [k for k in GROUP if dur[k]]
         n = min(len(dur[k]) for k in ks)
         pas = [sum(dur[k][i] for k in ks) for i in range(n)]
@@ -43,7 +55,7 @@ def main():
     for r in rows:
         if r["Kernel_Name"].strip() not in GROUP:
             other[r["Kernel_Name"][:80]].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
-    res = {"kernel": KERNEL, "dispatches": len(pas), "skipped": skip, "kept": len(kept),
+    res = {"kernel": "+".join(k for k in WF if dur[k]) if dur["rt0_jit_wf_march"] else KERNEL, "dispatches": len(pas), "skipped": skip, "kept": len(kept),
            "median_ms": statistics.median(kept) / 1e6 if kept else None,
            "mean_ms": statistics.mean(kept) / 1e6 if kept else None,
            "min_ms": min(kept) / 1e6 if kept else None, "max_ms": max(kept) / 1e6 if kept else None,

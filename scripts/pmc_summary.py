@@ -31,7 +31,21 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
-GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve")
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_march")
+# wavefront SDF launches (rt0_integrator.h wf_shade_body): MAX_BOUNCES + 2
+# shade and MAX_BOUNCES + 1 march dispatches per launch, closed by one
+# rt0_sum_kernel -- their counters are summed per launch
+WF = ("rt0_jit_wf_shade", "rt0_jit_wf_march")
+
+
+def launches_in(d):
+    """rt0_sum_kernel dispatches of a pass directory: one per wavefront launch."""
+    ids = set()
+    for fn in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(fn)):
+            if r["Kernel_Name"].strip().startswith("rt0_sum_kernel"):
+                ids.add(int(r["Dispatch_Id"]))
+    return len(ids)
 
 
 def dispatches(d, kernel):
@@ -59,20 +73,25 @@ def main():
     by_kernel = {}  # kernel -> {counter: mean per dispatch}
     for d in sys.argv[6:]:
         in_dir = {}  # this pass directory's counters, the group's kernels summed
+        nl = launches_in(d)
         for kernel in GROUP:
             vals, dur = dispatches(d, kernel)
-            ids = sorted(vals)[skip:]
+            every = sorted(vals)
+            per_launch = 1
+            if kernel in WF and nl > skip:
+                per_launch = max(1, len(every) // nl)
+            ids = every[skip * per_launch:]
             if not ids:
                 continue
             if kernel not in kernels:
                 kernels.append(kernel)
             names = set().union(*(vals[i].keys() for i in ids))
-            for c in names:  # per pass: the group's kernels summed
-                m = sum(vals[i].get(c, 0.0) for i in ids) / len(ids)
+            for c in names:  # per pass: the group's kernels summed (a wavefront launch's dispatches summed)
+                m = sum(vals[i].get(c, 0.0) for i in ids) / len(ids) * per_launch
                 in_dir[c] = in_dir.get(c, 0.0) + m
                 by_kernel.setdefault(kernel, {})[c] = m
                 n_kept[c] = len(ids)
-            if "GRBM_GUI_ACTIVE" in names and kernel == KERNEL:
+            if "GRBM_GUI_ACTIVE" in names and kernel in (KERNEL, "rt0_jit_wf_march"):
                 for i in ids:
                     if dur.get(i):
                         clock.append(vals[i]["GRBM_GUI_ACTIVE"] / 8.0 / dur[i])  # cycles per ns = GHz

@@ -1,5 +1,6 @@
-"""The JS CPU integrator (oracle/js/rt0_cpu.js) -- the reported CPU baseline
-of bench.py, SURVEY 8d -- renders what the reference renders: checked against
+"""The JS CPU integrator (raytracer-0_amd/js/rt0_cpu.js) -- GlslViewport's CPU
+backend (opts.backend = 'cpu', BASELINE configs[0]) and the reported CPU
+baseline of bench.py, SURVEY 8d -- renders what the reference renders: checked against
 the golden fixtures (the reference shader under SwiftShader) and the C oracle
 on the configs it covers (quadrics, SDFs, volumetrics, ReSTIR).  CPU only."""
 import json
@@ -75,7 +76,7 @@ def test_js_integrator_rejects_features_outside_its_scope(tmp_path):
     for name in ("anim_restir_demo",):  # RENDER_MODE 1
         r = subprocess.run([NODE, BENCH, CONFIGS, name, "16", "16", "1", "image", "1", "1",
                             str(tmp_path / "x.f32")], capture_output=True, text=True, timeout=120)
-        assert r.returncode != 0 and "outside the JS baseline" in r.stderr, name
+        assert r.returncode != 0 and "outside the JS CPU integrator" in r.stderr, name
 
 
 def js_restir_chain(name, w, h, n, tmp_path, constants=None, threads=4, extra=()):
@@ -172,3 +173,99 @@ def test_js_triangle_models_match_c_oracle(cfgs, tmp_path):
     # the model is in the picture: some pixels see it (hit index = the TRIANGLE entry)
     assert S[..., :3].mean() > 0 and abs(J[:, 0, ..., :3].mean() - S[..., :3].mean()) <= 2e-3 * S[..., :3].mean()
 
+
+
+VIEWPORT_JS = os.path.join(REPO, "raytracer-0_amd", "js", "glsl_viewport.js")
+
+
+def run_viewport_cpu(src, tmp_path):
+    script = tmp_path / "page.js"
+    script.write_text(src)
+    r = subprocess.run([NODE, str(script)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+def test_viewport_cpu_backend_renders_c1_like_the_page(cfgs, tmp_path):
+    """BASELINE configs[0] through the product surface: GlslViewport with
+    opts.backend = 'cpu' (the JS integrator, no GPU) driven the way the
+    reference's page drives it -- the C1 constants set on `sandbox`, then
+    RenderLoop's one render() per frame until max_passes (index.html:1218-1242
+    -> index.js:986-1105) -- against the reference's own C1 fixture (the
+    accumulated passes) and the C restatement."""
+    gold = np.load(os.path.join(REPO, "tests", "golden", "c1_cornell_cos.npz"))["samples"]
+    F, H, W = gold.shape[:3]
+    out = tmp_path / "acc.f32"
+    src = """
+const fs = require('fs');
+const v = require(%r);
+const sandbox = new v.GlslViewport(null, {width: %d, height: %d, backend: 'cpu', max_passes: %d});
+if (sandbox.backend !== 'cpu') throw new Error('backend ' + sandbox.backend);
+sandbox.constants[0] = 'const lowp int MAX_BOUNCES = 4;';
+sandbox.constants[7] = 'const bool sample_lights = false;';
+sandbox.constants[8] = 'const bool use_mis = false;';
+while (sandbox.passes < sandbox.max_passes) sandbox.render();   // RenderLoop
+fs.writeFileSync(%r, Buffer.from(sandbox.accumulator().buffer));
+const img = sandbox.image();
+console.log(JSON.stringify({passes: sandbox.passes, px: img.length, ms: sandbox.lastKernelMs()}));
+""" % (VIEWPORT_JS, W, H, F, str(out))
+    info = json.loads(run_viewport_cpu(src, tmp_path).strip().splitlines()[-1])
+    assert info["passes"] == F and info["px"] == W * H * 4
+    got = np.fromfile(str(out), np.float32).reshape(H, W, 4)
+    ref = np.zeros_like(gold[0])
+    for k in range(F):
+        ref[..., :3] = ref[..., :3] + gold[k][..., :3]
+    assert match(got, ref) >= 0.99
+    cfg = [c for c in cfgs["configs"] if c["name"] == "c1_cornell_cos"][0]
+    o = O.Oracle(cfg, cfgs, width=W, height=H)
+    oref = sum(o.frame(k)[0] for k in range(1, F + 1))
+    assert match(got, oref) >= 0.999
+
+
+def test_viewport_cpu_backend_scene_text_and_restir(cfgs, tmp_path):
+    """The CPU backend parses the reference's GLSL-side state back (scene
+    text from sceneFromLines, #sdf_meshes statements, define/constant lines):
+    an SDF scene and a ReSTIR scene (index.js's swap chain) render what the
+    JS integrator renders from the same config directly."""
+    import rt0
+    for name, n in (("sdf_cone", 2), ("c3_outdoor_restir", 3)):
+        cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+        scene, sdf = rt0.scene_strings(cfg, cfgs)
+        defines, consts = rt0.config_strings(cfg)
+        cam = cfg.get("camera") or cfgs["default_camera"]
+        out = tmp_path / ("%s.f32" % name)
+        src = """
+const fs = require('fs');
+const v = require(%r);
+const vp = new v.GlslViewport(null, {width: 32, height: 24, backend: 'cpu'});
+vp.defines = %s; vp.constants = %s; vp.scene = %s; vp.sdf_meshes = %s;
+const c = %s;
+vp.camera.origin = new v.Vector3(...c.origin); vp.camera.lookat = new v.Vector3(...c.lookat);
+vp.camera.fov = c.fov; vp.camera.aperture = c.aperture; vp.camera.focalLength = c.focalLength;
+for (let k = 0; k < %d; k++) vp.render();
+fs.writeFileSync(%r, Buffer.from(vp.accumulator().buffer));
+""" % (VIEWPORT_JS, json.dumps(defines), json.dumps(consts), json.dumps(scene), json.dumps(sdf), json.dumps(cam),
+       n, str(out))
+        run_viewport_cpu(src, tmp_path)
+        got = np.fromfile(str(out), np.float32).reshape(24, 32, 4)
+        if name == "c3_outdoor_restir":
+            ref = js_restir_chain(name, 32, 24, n, tmp_path)[:, 0].sum(0)
+        else:
+            ref = js_image(name, 32, 24, 1, n, tmp_path)
+        assert np.array_equal(got[..., :3], ref[..., :3]), name
+
+
+def test_viewport_backend_is_explicit(tmp_path):
+    """No silent fallback: an unknown backend is refused, and the CPU backend
+    refuses what only the HIP backend renders (textures, cubemap)."""
+    src = """
+const v = require(%r);
+let msg = [];
+try { new v.GlslViewport(null, {width: 8, height: 8, backend: 'webgl'}); } catch (e) { msg.push(e.message); }
+const vp = new v.GlslViewport(null, {width: 8, height: 8, backend: 'cpu'});
+try { vp.loadTexture({name: 'tex0'}, {width: 1, height: 1, data: new Uint8Array(4)}); } catch (e) { msg.push(e.message); }
+try { vp.loadCubemap([1,2,3,4,5,6].map(() => ({width: 1, height: 1, data: new Uint8Array(3)}))); } catch (e) { msg.push(e.message); }
+console.log(JSON.stringify(msg));
+""" % VIEWPORT_JS
+    msg = json.loads(run_viewport_cpu(src, tmp_path).strip().splitlines()[-1])
+    assert len(msg) == 3 and "backend" in msg[0] and "outside the JS CPU integrator" in msg[1] + msg[2]
