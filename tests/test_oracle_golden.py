@@ -287,6 +287,70 @@ def test_deep_volume_executor_paths(cfgs):
     assert S[..., :3][dep].mean() > gold[dep].mean()
 
 
+def _path_digits(v, base, n):
+    """The n digits (oldest first) of a path-record field (make_golden.py
+    instrument_paths: depth history in base 16, exit events in base 8)."""
+    v, d = int(v), []
+    for _ in range(n):
+        d.append(v % base)
+        v //= base
+    return d[::-1]
+
+
+def test_deep_volume_departures_accounted(cfgs):
+    """Every lane of c4_mandelbulb_deep whose executor record departs from
+    GLSL semantics, classified from the fixture's own records
+    (exec_paths/exec_exits) against the restatement's (RT0_DEBUG_PATHS):
+      (a) retired after a first-iteration scatter `continue` (record: one
+          iteration, one event = 1): every such lane meets rule 10's
+          condition (mask_kat.py QUAD CONTINUE: GLSL takes the continue in
+          iteration 1 and the lane is not its quad's first lane) -- but the
+          condition is not sufficient here, most candidates run as GLSL says;
+      (b) the first iteration's depth increment lost (depth 0 repeated; its
+          exit event missing or recorded) -- only in quads where no lane
+          scatters in iteration 1: another mechanism;
+      (c) anything else: bounded at 0.5% of the valid lanes.
+    Quads are the 2x2 scissor tiles of one glrun call each (tiles [2, 2])."""
+    name = "c4_mandelbulb_deep"
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    valid, conf = G["valid"], G["conformant"]
+    ep, ex = G["exec_paths"], G["exec_exits"]
+    o = O.Oracle(cfg, cfgs, width=16, height=16, overrides={"SWIFTSHADER_GHOST": 1, "RT0_DEBUG_PATHS": 1})
+    P, X = [], []
+    for k in G["frames"]:
+        _, p, x = o.frame(int(k))
+        P.append(p), X.append(x)
+    P, X = np.stack(P), np.stack(X)
+    F, H, W = valid.shape
+
+    def first_event(f, y, x):
+        return _path_digits(X[f, y, x, 0], 8, int(P[f, y, x, 0]))[0]
+
+    cand = set()  # rule 10's condition under GLSL semantics
+    for f, y, x in zip(*np.nonzero(valid)):
+        if int(P[f, y, x, 0]) > 1 and first_event(f, y, x) == 1 and not (x % 2 == 0 and y % 2 == 0):
+            cand.add((f, y, x))
+    kinds = {"a": [], "b": [], "c": []}
+    for f, y, x in zip(*np.nonzero(valid & ~conf)):
+        n = int(ep[f, y, x, 0])
+        hist, ev = _path_digits(ep[f, y, x, 1], 16, n), _path_digits(ex[f, y, x, 0], 8, n)
+        if n == 1 and ev == [1]:
+            kinds["a"].append((f, y, x))
+        elif n >= 2 and hist[0] == 0 and hist[1] == 0:
+            kinds["b"].append((f, y, x))
+        else:
+            kinds["c"].append((f, y, x))
+    assert all(p in cand for p in kinds["a"]), "a retirement outside rule 10's condition"
+    assert len(kinds["a"]) < len(cand)  # (41 of 351 in the committed fixture)
+    for f, y, x in kinds["b"]:
+        fy, fx = y & ~1, x & ~1
+        quad = [(fy, fx), (fy, fx + 1), (fy + 1, fx), (fy + 1, fx + 1)]
+        assert all(first_event(f, a, b) != 1 for a, b in quad if valid[f, a, b])
+    assert len(kinds["a"]) + len(kinds["b"]) + len(kinds["c"]) == int((valid & ~conf).sum())
+    assert len(kinds["c"]) <= 0.005 * valid.sum(), len(kinds["c"])
+
+
 def test_mask_kat_quad_continue():
     """Rule 10 (mask_kat.py QUAD CONTINUE): in the reference's bounce-loop
     shape, a lane that takes the scatter `continue` in the loop's first
