@@ -119,6 +119,9 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_WAVEFRONT
 #define RT0_WAVEFRONT 0
 #endif
+#ifndef RT0_WF_REFILL  // free lanes that trigger a march-kernel refill (wf_march_body)
+#define RT0_WF_REFILL 1
+#endif
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
   return x - floorf(x);
@@ -3086,8 +3089,14 @@ DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
   const float4 part = P.nee_partial[pix];
   const int n = P.nee_n[pix];
   v3 col = mk(part.x, part.y, part.z);
-  for (int k = 0; k < n; ++k) {
-    float4 o = P.nee_out[(size_t)k * plane + pix];
+  // every call's result is loaded before the first is added: the loads are
+  // independent, so a pixel waits one round trip for its calls instead of n
+  // (the kernel waited on memory 93% of its cycles, loading them one by one)
+  constexpr int K = Cfg::max_bounces() < 16 ? Cfg::max_bounces() : 16;
+  float4 res[K > 0 ? K : 1];
+#pragma unroll
+  for (int k = 0; k < K; ++k) res[k] = k < n ? P.nee_out[(size_t)k * plane + pix] : make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [&](int k, float4 o) {
 #if RT0_NEE_WALK
     if (const uint32_t tag = (uint32_t)__float_as_int(o.w)) {
       // a call rt0_jit_nee left to the walks: its result counts if both rays
@@ -3100,7 +3109,11 @@ DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
     }
 #endif
     col = col + mk(o.x, o.y, o.z);
-  }
+  };
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (k < n) add(k, res[k]);  // (constant indices: the results stay in registers)
+  for (int k = K; k < n; ++k) add(k, P.nee_out[(size_t)k * plane + pix]);
   if constexpr (SPECTRAL) {
     if (cfg.flags() & F_SPECTRAL) col = col * wavelength_to_rgb(part.w);
   }
@@ -3363,6 +3376,9 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   };
   while (true) {
     uint64_t fr = __ballot(!busy);
+    // refill once RT0_WF_REFILL lanes are free (or all are): each refill's
+    // job loads are a round trip the wave waits for
+    if (__popcll(fr) < RT0_WF_REFILL && __ballot(busy) != 0ull) fr = 0ull;
     while (fr != 0ull && reg < NR) {
       if (q >= nall) {
         if (++reg >= reg_end) grab();
