@@ -122,6 +122,9 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_WF_REFILL  // free lanes that trigger a march-kernel refill (wf_march_body)
 #define RT0_WF_REFILL 1
 #endif
+#ifndef RT0_WF_PREFETCH  // march lanes hold their next job in registers (wf_march_body)
+#define RT0_WF_PREFETCH 0
+#endif
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
   return x - floorf(x);
@@ -3374,6 +3377,71 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     }
     busy = false;
   };
+  // a job of the queue: entry j of region reg (march entries, then shadow entries)
+  auto load_job = [&](uint32_t j, float4 &a, float4 &b, float4 &e, uint32_t &ix, bool &sh) {
+    if (j < nc) {
+      const size_t k = (size_t)reg * R + j;
+      a = P.wf_out[2 * k];
+      b = P.wf_out[2 * k + 1];
+      ix = (uint32_t)k;
+      sh = false;
+    } else {
+      const size_t k = 3 * ((size_t)reg * RL + (j - nc));
+      a = P.wf_sh[k];
+      b = P.wf_sh[k + 1];
+      e = P.wf_sh[k + 2];
+      ix = __float_as_uint(b.w);
+      sh = true;
+    }
+  };
+  auto start_job = [&](const float4 &a, const float4 &b, const float4 &e, uint32_t ix, bool sh) {
+    o = mk(a.x, a.y, a.z);
+    tmin = a.w;
+    d = mk(b.x, b.y, b.z);
+    idx = ix;
+    shadow = sh;
+    c = mk(e.x, e.y, e.z);
+    dirl = sh && e.w != 0.0f;
+    busy = sh || tmin >= 0.0f;  // (a march entry without a march: only its light sampling goes on)
+    t = EPSILON * 4.0f;
+    id = 0.0f;
+    i = 0;
+    ph = 4;
+    if (busy && cap <= 0) stopped();  // (MARCHING_STEPS 0: no step at all)
+  };
+#if RT0_WF_PREFETCH
+  // Each lane holds its NEXT job in registers, loaded when it took the one
+  // before: a refill starts the prefetched jobs at once and issues the loads
+  // of their successors, which are not read before the following refill.
+  bool nf = false, nsh = false;
+  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
+  uint32_t nix = 0;
+  while (true) {
+    uint64_t fr = __ballot(!busy);
+    if (__popcll(fr) >= RT0_WF_REFILL || __ballot(busy) == 0ull) {
+      if (!busy && nf) {
+        start_job(n0, n1, n2, nix, nsh);
+        nf = false;
+      }
+      uint64_t fq = __ballot(!nf);
+      while (fq != 0ull && reg < NR) {
+        if (q >= nall) {
+          if (++reg >= reg_end) grab();
+          open();
+          continue;
+        }
+        const uint32_t take = min((uint32_t)__popcll(fq), nall - q);
+        const uint32_t rank = (uint32_t)__popcll(fq & lt);
+        if (!nf && rank < take) {
+          load_job(q + rank, n0, n1, n2, nix, nsh);
+          nf = true;
+        }
+        q += take;
+        fq = __ballot(!nf);
+      }
+    }
+    if (__ballot(busy || nf) == 0ull) break;  // the queue is dry and every lane answered
+#else
   while (true) {
     uint64_t fr = __ballot(!busy);
     // refill once RT0_WF_REFILL lanes are free (or all are): each refill's
@@ -3388,38 +3456,17 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       const uint32_t take = min((uint32_t)__popcll(fr), nall - q);
       const uint32_t rank = (uint32_t)__popcll(fr & lt);
       if (!busy && rank < take) {
-        const uint32_t j = q + rank;
-        if (j < nc) {
-          const size_t b = (size_t)reg * R + j;
-          const float4 j0 = P.wf_out[2 * b], j1 = P.wf_out[2 * b + 1];
-          o = mk(j0.x, j0.y, j0.z);
-          tmin = j0.w;
-          d = mk(j1.x, j1.y, j1.z);
-          idx = (uint32_t)b;
-          shadow = false;
-          busy = tmin >= 0.0f;  // (an entry without a march: only its light sampling goes on)
-        } else {
-          const size_t b = 3 * ((size_t)reg * RL + (j - nc));
-          const float4 e0 = P.wf_sh[b], e1 = P.wf_sh[b + 1], e2 = P.wf_sh[b + 2];
-          o = mk(e0.x, e0.y, e0.z);
-          tmin = e0.w;
-          d = mk(e1.x, e1.y, e1.z);
-          idx = __float_as_uint(e1.w);
-          c = mk(e2.x, e2.y, e2.z);
-          dirl = e2.w != 0.0f;
-          shadow = true;
-          busy = true;
-        }
-        t = EPSILON * 4.0f;
-        id = 0.0f;
-        i = 0;
-        ph = 4;
-        if (busy && cap <= 0) stopped();  // (MARCHING_STEPS 0: no step at all)
+        float4 a, b, e = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t ix;
+        bool sh;
+        load_job(q + rank, a, b, e, ix, sh);
+        start_job(a, b, e, ix, sh);
       }
       q += take;
       fr = __ballot(!busy);
     }
     if (__ballot(busy) == 0ull) break;  // the queue is dry and every lane answered
+#endif
     if (busy) {
       const v3 hp = ray_at(o, d, t);
       // calcNormal's probe ph: pos + (s.x, s.y, s.z) * EPSILON, times the same signs
