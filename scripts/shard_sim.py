@@ -1,19 +1,58 @@
-"""Per-GPU kernel time of one shard (rank 0 of N) on one device: the strong-
-scaling ceiling of the band sharding without any collective."""
-import json, os, sys, time
+"""Load balance of the progressive workloads' 16-row round-robin band sharding
+(bench.py ProgressiveJob, rt0_set_shard) on one device: every rank's share of
+one bench step rendered alone (the other ranks' bands skipped), for N = 2, 4,
+8.  Prints per-rank kernel times (HIP events, best of 3), max/mean, the
+strong-scaling ceiling T1 / (N * slowest rank) and the sum of the ranks'
+times over T1 (how much per-rank overhead sharding adds) -- the gather and
+RCCL are excluded.
+
+    python3 scripts/shard_sim.py c4 [c2 ...] > profiles/rNN/shard_sim/shard_sim.txt
+"""
+import json
+import os
+import sys
+
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(HERE, "..", "raytracer-0_amd")); sys.path.insert(0, os.path.join(HERE, "..", "oracle"))
-import rt0, oracle as O
-cfgs = O.load_configs()
-cfg = [c for c in cfgs["configs"] if c["name"] == "c2_cornell_mis_8"][0]
-res = {}
-for n in (1, 2, 4, 8):
-    r = rt0.Renderer(1024, 1024)
-    rt0.configure(r, cfg, cfgs)
-    r.set_shard(0, n, 16)
-    r.render(1, 64)
-    ts = []
-    for _ in range(5):
-        r.clear(); r.render(1, 64); ts.append(r.last_kernel_ms()[0])
-    res[n] = min(ts)
-    print(n, "shard kernel ms", res[n], "ideal", res[1] / n, "efficiency %.3f" % (res[1] / n / res[n]), flush=True)
+sys.path.insert(0, os.path.join(HERE, "..", "raytracer-0_amd"))
+import rt0  # noqa: E402
+from rt0 import workloads  # noqa: E402
+
+BAND = 16
+
+
+def main():
+    out = {}
+    for key in sys.argv[1:] or ["c4"]:
+        wl = workloads.get(key)
+        W, H, spp = wl["width"], wl["height"], wl["spp"]
+
+        def timed(rank, n):
+            r = rt0.Renderer(W, H)
+            workloads.configure(r, wl)
+            if n > 1:
+                r.set_shard(rank, n, BAND)
+            r.render(1, spp)  # warm-up (JIT compile, buffers)
+            ts = []
+            for k in range(3):
+                r.clear()
+                r.render(1 + spp * (k + 1), spp)
+                ts.append(r.last_kernel_ms()[0])
+            path = r.last_render_path()
+            r.close()
+            return min(ts), path
+
+        t1, path = timed(0, 1)
+        res = {"whole_ms": round(t1, 3), "render_path": path, "band_rows": BAND, "spp": spp}
+        print(key, "whole", res, flush=True)
+        for n in (2, 4, 8):
+            per = [timed(rank, n)[0] for rank in range(n)]
+            mean = sum(per) / n
+            res[str(n)] = {"rank_ms": [round(t, 3) for t in per], "max_over_mean": round(max(per) / mean, 3),
+                           "ceiling": round(t1 / (n * max(per)), 3), "sum_over_whole": round(sum(per) / t1, 3)}
+            print(key, n, res[str(n)], flush=True)
+        out[key] = res
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
