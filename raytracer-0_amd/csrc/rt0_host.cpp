@@ -730,7 +730,8 @@ static bool wf_eligible(const rt0_ctx *c) {
 // rounds of the shade and march kernels; the samples land in p.samples and
 // rt0_sum_kernel adds them in frame order (the caller launches it).
 static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
-  constexpr uint32_t kR = 512;  // slots per region (one shade wave)
+  // slots per region (one shade wave; the march kernel's unit of work)
+  const uint32_t kR = getenv("RT0_WF_REGION") ? (uint32_t)std::max(64, atoi(getenv("RT0_WF_REGION"))) / 64 * 64 : 512u;
   const uint32_t L = (uint32_t)std::max(1, c->host_scene.n_lights);
   const bool extra = (p.flags & F_MIS) || ((p.flags & F_SPECTRAL) && (c->cfg.defines & RT0_USE_SPECTRAL));
   // bytes per slot: state, two march-list entries, the answer + id, L shadow entries + answers
@@ -772,7 +773,8 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   p.wf_nregions = (int32_t)NR;
   p.wf_apad = (uint32_t)apad;
   p.wf_gx = grid.x;
-  const unsigned march_blocks = (unsigned)std::min<size_t>((size_t)c->jit.wf_march_blocks, (NR + 15) / 16);
+  // persistent march waves: what the device holds at once, at most one per region
+  const unsigned march_blocks = (unsigned)std::min<size_t>((size_t)c->jit.wf_march_blocks, (NR + 3) / 4);
   const int rounds = p.max_bounces + 2;
   for (int f0 = 0; f0 < p.nframes; f0 += fc) {
     p.wf_f0 = f0;

@@ -122,6 +122,9 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_WF_REFILL  // free lanes that trigger a march-kernel refill (wf_march_body)
 #define RT0_WF_REFILL 1
 #endif
+#ifndef RT0_WF_GROUP  // regions a march wave takes per device-counter grab (wf_march_body)
+#define RT0_WF_GROUP 4
+#endif
 #ifndef RT0_WF_PREFETCH  // march lanes hold their next job in registers (wf_march_body)
 #define RT0_WF_PREFETCH 0
 #endif
@@ -3331,7 +3334,7 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 template <class Scene, class Cfg>
 DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   using G = Geometry<Scene>;
-  constexpr uint32_t kRegionGroup = 4;
+  constexpr uint32_t kRegionGroup = RT0_WF_GROUP;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lt = (1ull << lane) - 1ull;
   const uint32_t R = (uint32_t)P.wf_R, NR = (uint32_t)P.wf_nregions, RL = R * (uint32_t)P.wf_L;
