@@ -242,7 +242,8 @@ struct LaunchParams {
   // index), and writes region w of this round's march list (wf_out,
   // wf_out_cnt) and shadow list (wf_sh: 3 float4 per entry, capacity wf_R *
   // wf_L per region, wf_sh_cnt); the march kernel takes regions off
-  // *wf_ctr and answers them (wf_res; wf_shres[light * wf_slots + slot]).
+  // wf_ctr[16 * k] (one counter per eighth of the regions) and answers them
+  // (wf_res; wf_shres[light * wf_slots + slot]).
   // Path state between rounds: wf_state[k * wf_slots + slot].
   int32_t wf_round, wf_R, wf_L, wf_nregions, wf_f0;
   uint32_t wf_apad, wf_slots, wf_gx;

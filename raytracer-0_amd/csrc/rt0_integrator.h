@@ -123,7 +123,7 @@ DEV float flog(float x) { return __logf(x); }
 #define RT0_WF_REFILL 1
 #endif
 #ifndef RT0_WF_GROUP  // regions a march wave takes per device-counter grab (wf_march_body)
-#define RT0_WF_GROUP 4
+#define RT0_WF_GROUP 1
 #endif
 #ifndef RT0_WF_PREFETCH  // march lanes hold their next job in registers (wf_march_body)
 #define RT0_WF_PREFETCH 0
@@ -3203,7 +3203,7 @@ DEV constexpr bool wf_extra_state() {
 template <class Scene, class Cfg, bool VOL, bool SPECTRAL>
 DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const SceneTables tabs = scene_tables(sc);  // (one barrier, before any wave leaves)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *P.wf_ctr = 0u;  // the march kernel's region counter
+  if (blockIdx.x == 0 && threadIdx.x < 8) P.wf_ctr[16 * threadIdx.x] = 0u;  // the march kernel's range counters
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
   if (w >= (uint32_t)P.wf_nregions) return;
@@ -3342,12 +3342,35 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const float fud = cfg.fudge();
   // the wave's queue (wave-uniform): region reg of [reg, reg_end), entry q of its nall
   uint32_t reg = 0, reg_end = 0, q = 0, nc = 0, nall = 0;
+  // The regions are split into kParts ranges with a counter each (64 B
+  // apart): a wave grabs from the range of its XCD (the dispatcher deals
+  // workgroups round-robin over the 8 XCDs), then from the others once its
+  // own is taken.  One device-wide counter serialised every grab of the chip
+  // (~5 ns each: 128-slot regions cost C4 549 vs 788 Msamples/s).
+  constexpr uint32_t kParts = 8;
+  uint32_t part = blockIdx.x % kParts, tried = 0;
+  auto part_lo = [&](uint32_t k) { return (uint32_t)(((uint64_t)NR * k) / kParts); };
   auto grab = [&]() {
-    uint32_t g = 0;
-    if (lane == 0) g = atomicAdd(P.wf_ctr, 1u);
-    g = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)g, 0));
-    reg = g * kRegionGroup;
-    reg_end = min(reg + kRegionGroup, NR);
+    while (tried < kParts) {
+      const uint32_t lo = part_lo(part), hi = part_lo(part + 1);
+      uint32_t g = 0;
+      if (lane == 0) {
+        uint32_t *ctr = P.wf_ctr + 16 * part;
+        // (a plain look first: a taken range costs no read-modify-write)
+        g = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lo + g * kRegionGroup < hi) g = atomicAdd(ctr, 1u);
+      }
+      g = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)g, 0));
+      const uint32_t r0 = lo + g * kRegionGroup;
+      if (r0 < hi) {
+        reg = r0;
+        reg_end = min(r0 + kRegionGroup, hi);
+        return;
+      }
+      part = (part + 1) % kParts;
+      ++tried;
+    }
+    reg = reg_end = NR;  // every region is taken
   };
   auto open = [&]() {
     q = 0;
