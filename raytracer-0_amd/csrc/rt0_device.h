@@ -248,6 +248,7 @@ struct LaunchParams {
   int32_t wf_round, wf_R, wf_L, wf_nregions, wf_f0;
   uint32_t wf_apad, wf_slots, wf_gx;
   uint32_t *wf_ctr;
+  uint32_t *wf_plan, *wf_plan_n;  // the round's non-empty regions (wf_plan_body) and their number
   float4 *wf_state;
   float4 *wf_in, *wf_out;
   uint32_t *wf_in_cnt, *wf_out_cnt, *wf_sh_cnt;

@@ -730,14 +730,23 @@ static bool wf_eligible(const rt0_ctx *c) {
 // rounds of the shade and march kernels; the samples land in p.samples and
 // rt0_sum_kernel adds them in frame order (the caller launches it).
 static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
-  // slots per region (one shade wave; the march kernel's unit of work)
-  const uint32_t kR = getenv("RT0_WF_REGION") ? (uint32_t)std::max(64, atoi(getenv("RT0_WF_REGION"))) / 64 * 64 : 512u;
+  // slots per region (one shade wave; the march kernel's unit of work): 512,
+  // halved down to 128 while the launch has fewer than 4 regions per march
+  // wave the device holds (an 8-way shard of C4: 8 192 regions of 512 slots
+  // for ~8 000 waves left each wave one region and its tail)
   const uint32_t L = (uint32_t)std::max(1, c->host_scene.n_lights);
   const bool extra = (p.flags & F_MIS) || ((p.flags & F_SPECTRAL) && (c->cfg.defines & RT0_USE_SPECTRAL));
   // bytes per slot: state, two march-list entries, the answer + id, L shadow entries + answers
   const size_t per_slot = (extra ? 48 : 32) + 2 * 32 + 16 + 4 + (size_t)L * (48 + 16);
   const size_t budget = getenv("RT0_WF_BYTES") ? (size_t)atoll(getenv("RT0_WF_BYTES")) : (size_t)8 << 30;
   const size_t apad = (size_t)grid.x * grid.y * 256;
+  uint32_t kR = 512;
+  if (const char *e = getenv("RT0_WF_REGION")) {
+    kR = (uint32_t)std::max(64, atoi(e)) / 64 * 64;
+  } else {
+    const size_t waves = (size_t)std::max(1, c->jit.wf_march_blocks) * 4;
+    while (kR > 128 && apad * (size_t)p.nframes / kR < 4 * waves) kR /= 2;
+  }
   const int fc = (int)std::max<size_t>(1, std::min<size_t>((size_t)p.nframes, budget / (apad * per_slot)));
   const size_t S = apad * (size_t)fc;
   if (S * L >= (1ull << 32)) return fail(c, RT0_E_UNSUPPORTED, "wavefront render: too many path slots");
@@ -745,7 +754,7 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_state = al(cap * (extra ? 3 : 2) * 16), b_list = al(cap * 32), b_res = al(cap * 16),
                b_id = al(cap * 4), b_sh = al(cap * L * 48), b_shres = al(cap * L * 16), b_cnt = al(NR * 4);
-  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 3 * b_cnt + 512;
+  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 4 * b_cnt + 512 + 256;
   if (need > c->wf_bytes) {
     if (c->d_wf) HIPCHK(c, hipFree(c->d_wf));
     c->d_wf = nullptr;
@@ -768,6 +777,8 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   uint32_t *cnts[2] = {(uint32_t *)take(b_cnt), (uint32_t *)take(b_cnt)};
   p.wf_sh_cnt = (uint32_t *)take(b_cnt);
   p.wf_ctr = (uint32_t *)take(512);  // 8 range counters, 64 B apart
+  p.wf_plan = (uint32_t *)take(b_cnt);
+  p.wf_plan_n = (uint32_t *)take(256);
   p.wf_R = (int32_t)kR;
   p.wf_L = (int32_t)L;
   p.wf_nregions = (int32_t)NR;
@@ -789,10 +800,13 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
       HIPCHK(c, rt0h::jit_launch(c->jit.wf_shade, &p, (unsigned)((p.wf_nregions + 3) / 4), 1, 1, c->stream) == RT0_OK
                     ? hipSuccess
                     : hipErrorLaunchFailure);
-      if (r + 1 < rounds)  // (the last round only finishes samples: nothing to march)
+      if (r + 1 < rounds) {  // (the last round only finishes samples: nothing to march)
+        HIPCHK(c, rt0h::jit_launch(c->jit.wf_plan, &p, 1, 1, 1, c->stream, 1024) == RT0_OK ? hipSuccess
+                                                                                        : hipErrorLaunchFailure);
         HIPCHK(c, rt0h::jit_launch(c->jit.wf_march, &p, std::max(1u, march_blocks), 1, 1, c->stream) == RT0_OK
                       ? hipSuccess
                       : hipErrorLaunchFailure);
+      }
     }
   }
   return RT0_OK;

@@ -3324,6 +3324,42 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   }
 }
 
+// The round's plan (rt0_jit_wf_plan, one workgroup of 1024 threads): the
+// regions whose march or shadow list is not empty, in region order, and their
+// number -- so the march kernel's grabs skip the empty regions of the late
+// rounds (most paths have ended) without a device-wide read-modify-write each.
+// Two passes over the region counts, each wave scanning 64 regions per step
+// (ballot + prefix count); the waves' totals are scanned in LDS.
+DEV void wf_plan_body(const LaunchParams &P) {
+  __shared__ uint32_t tot[16], base[16];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t NR = (uint32_t)P.wf_nregions;
+  const uint32_t span = ((NR + nw - 1) / nw + 63u) / 64u * 64u;
+  const uint32_t lo = min(w * span, NR), hi = min(lo + span, NR);
+  auto nonempty = [&](uint32_t r) { return r < hi && (P.wf_out_cnt[r] | P.wf_sh_cnt[r]) != 0u; };
+  uint32_t n = 0;
+  for (uint32_t b = lo; b < hi; b += 64u) n += (uint32_t)__popcll(__ballot(nonempty(b + lane)));
+  if (lane == 0) tot[w] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < nw; ++k) {
+      base[k] = s;
+      s += tot[k];
+    }
+    *P.wf_plan_n = s;
+  }
+  __syncthreads();
+  uint32_t at = base[w];
+  for (uint32_t b = lo; b < hi; b += 64u) {
+    const bool ne = nonempty(b + lane);
+    const uint64_t m = __ballot(ne);
+    if (ne) P.wf_plan[at + (uint32_t)__popcll(m & lt)] = b + lane;
+    at += (uint32_t)__popcll(m);
+  }
+}
+
 // The march kernel: persistent waves over the round's march and shadow lists.
 // A lane holds one entry: a closest-hit march (then, on a hit, calcNormal's
 // four probes) or a shadow march.  Each loop trip every busy lane evaluates
@@ -3341,15 +3377,18 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   const int cap = cfg.marching_steps();
   const float fud = cfg.fudge();
   // the wave's queue (wave-uniform): region reg of [reg, reg_end), entry q of its nall
-  uint32_t reg = 0, reg_end = 0, q = 0, nc = 0, nall = 0;
-  // The regions are split into kParts ranges with a counter each (64 B
-  // apart): a wave grabs from the range of its XCD (the dispatcher deals
-  // workgroups round-robin over the 8 XCDs), then from the others once its
-  // own is taken.  One device-wide counter serialised every grab of the chip
-  // (~5 ns each: 128-slot regions cost C4 549 vs 788 Msamples/s).
+  // The queue walks the round's plan (wf_plan_body: the regions with any
+  // entry, in order), split into kParts ranges with a counter each (64 B
+  // apart): a wave grabs kRegionGroup plan entries from the range of its XCD
+  // (the dispatcher deals workgroups round-robin over the 8 XCDs), then from
+  // the others once its own is taken.  A device-scope atomic on one address
+  // serialises at ~0.1 us: one counter over every region made the late rounds
+  // (a few paths left in a few regions) cost ~0.5-1 ms each in grabs alone.
   constexpr uint32_t kParts = 8;
+  const uint32_t NP = *P.wf_plan_n;
+  uint32_t reg = NR, pos = 0, pos_end = 0, q = 0, nc = 0, nall = 0;
   uint32_t part = blockIdx.x % kParts, tried = 0;
-  auto part_lo = [&](uint32_t k) { return (uint32_t)(((uint64_t)NR * k) / kParts); };
+  auto part_lo = [&](uint32_t k) { return (uint32_t)(((uint64_t)NP * k) / kParts); };
   auto grab = [&]() {
     while (tried < kParts) {
       const uint32_t lo = part_lo(part), hi = part_lo(part + 1);
@@ -3361,20 +3400,21 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
         if (lo + g * kRegionGroup < hi) g = atomicAdd(ctr, 1u);
       }
       g = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)g, 0));
-      const uint32_t r0 = lo + g * kRegionGroup;
-      if (r0 < hi) {
-        reg = r0;
-        reg_end = min(r0 + kRegionGroup, hi);
+      const uint32_t p0 = lo + g * kRegionGroup;
+      if (p0 < hi) {
+        pos = p0;
+        pos_end = min(p0 + kRegionGroup, hi);
         return;
       }
       part = (part + 1) % kParts;
       ++tried;
     }
-    reg = reg_end = NR;  // every region is taken
+    pos = pos_end = NP;  // the whole plan is taken
   };
   auto open = [&]() {
     q = 0;
     nc = nall = 0;
+    reg = pos < NP ? P.wf_plan[pos] : NR;
     if (reg < NR) {
       nc = P.wf_out_cnt[reg];
       nall = nc + P.wf_sh_cnt[reg];
@@ -3452,7 +3492,7 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       uint64_t fq = __ballot(!nf);
       while (fq != 0ull && reg < NR) {
         if (q >= nall) {
-          if (++reg >= reg_end) grab();
+          if (++pos >= pos_end) grab();
           open();
           continue;
         }
@@ -3475,7 +3515,7 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     if (__popcll(fr) < RT0_WF_REFILL && __ballot(busy) != 0ull) fr = 0ull;
     while (fr != 0ull && reg < NR) {
       if (q >= nall) {
-        if (++reg >= reg_end) grab();
+        if (++pos >= pos_end) grab();
         open();
         continue;
       }

@@ -176,6 +176,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "void rt0_jit_wf_shade(const LaunchParams P) {\n"
          "  rt0::wf_shade_body<rt0::JitScene, rt0::JitCfg, "
       << vol << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    o << "extern \"C\" __global__ __launch_bounds__(1024) void rt0_jit_wf_plan(const LaunchParams P) { "
+         "rt0::wf_plan_body(P); }\n";
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
     if (const char *e = getenv("RT0_JIT_MARCH_WAVES_PER_EU")) o << "__attribute__((amdgpu_waves_per_eu(" << atoi(e) << "))) ";
     o << "void rt0_jit_wf_march(const LaunchParams P) {\n"
@@ -343,14 +345,16 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
   hipFunction_t f[4] = {};
   bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
   if (ok && k.wf) {
-    hipFunction_t s = nullptr, m = nullptr;
+    hipFunction_t s = nullptr, m = nullptr, pl = nullptr;
     int per_cu = 0, cus = 0;
     ok = hipModuleGetFunction(&s, e.mod, "rt0_jit_wf_shade") == hipSuccess &&
          hipModuleGetFunction(&m, e.mod, "rt0_jit_wf_march") == hipSuccess &&
+         hipModuleGetFunction(&pl, e.mod, "rt0_jit_wf_plan") == hipSuccess &&
          hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m, 256, 0) == hipSuccess &&
          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess;
     e.fns.wf_shade = (void *)s;
     e.fns.wf_march = (void *)m;
+    e.fns.wf_plan = (void *)pl;
     e.fns.wf_march_blocks = std::max(1, per_cu) * std::max(1, cus);
   } else if (ok) {
     ok = hipModuleGetFunction(&f[0], e.mod, "rt0_jit_pass") == hipSuccess;
@@ -373,9 +377,9 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
   return RT0_OK;
 }
 
-int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, unsigned gz, void *stream) {
+int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, unsigned gz, void *stream, unsigned block) {
   void *args[] = {(void *)p};
-  hipError_t e = hipModuleLaunchKernel((hipFunction_t)fn, gx, gy, gz, 256, 1, 1, 0, (hipStream_t)stream, args, nullptr);
+  hipError_t e = hipModuleLaunchKernel((hipFunction_t)fn, gx, gy, gz, block, 1, 1, 0, (hipStream_t)stream, args, nullptr);
   return e == hipSuccess ? RT0_OK : RT0_E_HIP;
 }
 

@@ -31,7 +31,7 @@ struct JitKey {
 struct JitFns {
   void *pass = nullptr, *nee = nullptr, *resolve = nullptr;
   void *walk = nullptr;  // RT0_NEE_WALK keys
-  void *wf_shade = nullptr, *wf_march = nullptr;  // RT0_WAVEFRONT keys (no pass kernel then)
+  void *wf_shade = nullptr, *wf_march = nullptr, *wf_plan = nullptr;  // RT0_WAVEFRONT keys (no pass kernel then)
   int wf_march_blocks = 0;  // workgroups of the march kernel the device holds at once
 };
 
@@ -46,6 +46,7 @@ SceneDev make_scene_dev(const rt0_mesh *m, int ne, int ns, int nm, const int32_t
 // Compile (or fetch from the process cache) the kernel for this scene/config on
 // `device`.
 int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::string &err);
-int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, unsigned gz, void *stream);
+int jit_launch(void *fn, const LaunchParams *p, unsigned gx, unsigned gy, unsigned gz, void *stream,
+               unsigned block = 256);
 
 }  // namespace rt0h

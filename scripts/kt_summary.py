@@ -20,10 +20,10 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
-GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_march")
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_march")
 # a wavefront SDF launch (rt0_integrator.h wf_shade_body): MAX_BOUNCES + 2
 # shade and MAX_BOUNCES + 1 march dispatches, then one rt0_sum_kernel
-WF = ("rt0_jit_wf_shade", "rt0_jit_wf_march")
+WF = ("rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_march")
 
 
 def main():

@@ -31,11 +31,11 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
-GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_march")
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_march")
 # wavefront SDF launches (rt0_integrator.h wf_shade_body): MAX_BOUNCES + 2
 # shade and MAX_BOUNCES + 1 march dispatches per launch, closed by one
 # rt0_sum_kernel -- their counters are summed per launch
-WF = ("rt0_jit_wf_shade", "rt0_jit_wf_march")
+WF = ("rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_march")
 
 
 def launches_in(d):
