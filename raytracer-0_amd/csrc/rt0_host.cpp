@@ -753,8 +753,8 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   const size_t NR = (S + kR - 1) / kR, cap = NR * kR;
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_state = al(cap * (extra ? 3 : 2) * 16), b_list = al(cap * 32), b_res = al(cap * 16),
-               b_id = al(cap * 4), b_sh = al(cap * L * 48), b_shres = al(cap * L * 16), b_cnt = al(NR * 4);
-  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 4 * b_cnt + 512 + 256;
+               b_id = al(cap * 4), b_sh = al(cap * L * 48), b_shres = al(cap * L * 16), b_cnt = al((NR + 4) * 4);
+  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 7 * b_cnt + 512 + 256;
   if (need > c->wf_bytes) {
     if (c->d_wf) HIPCHK(c, hipFree(c->d_wf));
     c->d_wf = nullptr;
@@ -777,7 +777,7 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   uint32_t *cnts[2] = {(uint32_t *)take(b_cnt), (uint32_t *)take(b_cnt)};
   p.wf_sh_cnt = (uint32_t *)take(b_cnt);
   p.wf_ctr = (uint32_t *)take(512);  // 8 range counters, 64 B apart
-  p.wf_plan = (uint32_t *)take(b_cnt);
+  p.wf_plan = (uint32_t *)take(4 * b_cnt);  // uint4 per region
   p.wf_plan_n = (uint32_t *)take(256);
   p.wf_R = (int32_t)kR;
   p.wf_L = (int32_t)L;

@@ -122,8 +122,8 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_WF_REFILL  // free lanes that trigger a march-kernel refill (wf_march_body)
 #define RT0_WF_REFILL 1
 #endif
-#ifndef RT0_WF_GROUP  // regions a march wave takes per device-counter grab (wf_march_body)
-#define RT0_WF_GROUP 1
+#ifndef RT0_WF_UNIT  // entries a march wave takes per device-counter grab, about (wf_march_body)
+#define RT0_WF_UNIT 512
 #endif
 #ifndef RT0_WF_PREFETCH  // march lanes hold their next job in registers (wf_march_body)
 #define RT0_WF_PREFETCH 0
@@ -3325,38 +3325,53 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 }
 
 // The round's plan (rt0_jit_wf_plan, one workgroup of 1024 threads): the
-// regions whose march or shadow list is not empty, in region order, and their
-// number -- so the march kernel's grabs skip the empty regions of the late
-// rounds (most paths have ended) without a device-wide read-modify-write each.
-// Two passes over the region counts, each wave scanning 64 regions per step
-// (ballot + prefix count); the waves' totals are scanned in LDS.
+// regions whose march or shadow list is not empty, in region order, as
+// (region, march entries, all entries), their number and the round's total
+// of entries -- so the march kernel's grabs skip the empty regions of the
+// late rounds and take several of their sparse regions at once (see
+// kUnitJobs), each region opened with one load.  Each thread counts a
+// contiguous run of regions (16-B loads, all issued before the first is
+// counted), the threads' counts are scanned in LDS, the runs written again.
 DEV void wf_plan_body(const LaunchParams &P) {
-  __shared__ uint32_t tot[16], base[16];
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint64_t lt = (1ull << lane) - 1ull;
+  __shared__ uint32_t scan[1024], jobs[1024];
+  const uint32_t t = threadIdx.x, T = blockDim.x;
   const uint32_t NR = (uint32_t)P.wf_nregions;
-  const uint32_t span = ((NR + nw - 1) / nw + 63u) / 64u * 64u;
-  const uint32_t lo = min(w * span, NR), hi = min(lo + span, NR);
-  auto nonempty = [&](uint32_t r) { return r < hi && (P.wf_out_cnt[r] | P.wf_sh_cnt[r]) != 0u; };
-  uint32_t n = 0;
-  for (uint32_t b = lo; b < hi; b += 64u) n += (uint32_t)__popcll(__ballot(nonempty(b + lane)));
-  if (lane == 0) tot[w] = n;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t s = 0;
-    for (uint32_t k = 0; k < nw; ++k) {
-      base[k] = s;
-      s += tot[k];
-    }
-    *P.wf_plan_n = s;
+  const uint32_t per = ((NR + T - 1) / T + 3u) & ~3u;
+  const uint32_t lo = min(t * per, NR), hi = min(lo + per, NR);
+  const uint4 *oc = reinterpret_cast<const uint4 *>(P.wf_out_cnt), *sc = reinterpret_cast<const uint4 *>(P.wf_sh_cnt);
+  uint32_t n = 0, nj = 0;
+  for (uint32_t r = lo; r < hi; r += 4u) {
+    const uint4 a = oc[r >> 2], b = sc[r >> 2];  // (lo and per are multiples of 4; the arrays are padded)
+    const uint32_t ca[4] = {a.x, a.y, a.z, a.w}, cb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r + k < hi) {
+        n += (ca[k] | cb[k]) != 0u;
+        nj += ca[k] + cb[k];
+      }
   }
+  scan[t] = n;
+  jobs[t] = nj;
   __syncthreads();
-  uint32_t at = base[w];
-  for (uint32_t b = lo; b < hi; b += 64u) {
-    const bool ne = nonempty(b + lane);
-    const uint64_t m = __ballot(ne);
-    if (ne) P.wf_plan[at + (uint32_t)__popcll(m & lt)] = b + lane;
-    at += (uint32_t)__popcll(m);
+  for (uint32_t d = 1; d < T; d <<= 1) {  // inclusive scan of the threads' counts and entries
+    const uint32_t x = t >= d ? scan[t - d] : 0u, y = t >= d ? jobs[t - d] : 0u;
+    __syncthreads();
+    scan[t] += x;
+    jobs[t] += y;
+    __syncthreads();
+  }
+  if (t == T - 1) {
+    P.wf_plan_n[0] = scan[t];
+    P.wf_plan_n[1] = jobs[t];
+  }
+  uint32_t at = scan[t] - n;
+  uint4 *plan = reinterpret_cast<uint4 *>(P.wf_plan);
+  for (uint32_t r = lo; r < hi; r += 4u) {
+    const uint4 a = oc[r >> 2], b = sc[r >> 2];
+    const uint32_t ca[4] = {a.x, a.y, a.z, a.w}, cb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r + k < hi && (ca[k] | cb[k]) != 0u) plan[at++] = make_uint4(r + k, ca[k], ca[k] + cb[k], 0u);
   }
 }
 
@@ -3370,7 +3385,6 @@ DEV void wf_plan_body(const LaunchParams &P) {
 template <class Scene, class Cfg>
 DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   using G = Geometry<Scene>;
-  constexpr uint32_t kRegionGroup = RT0_WF_GROUP;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t lt = (1ull << lane) - 1ull;
   const uint32_t R = (uint32_t)P.wf_R, NR = (uint32_t)P.wf_nregions, RL = R * (uint32_t)P.wf_L;
@@ -3385,7 +3399,10 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   // serialises at ~0.1 us: one counter over every region made the late rounds
   // (a few paths left in a few regions) cost ~0.5-1 ms each in grabs alone.
   constexpr uint32_t kParts = 8;
-  const uint32_t NP = *P.wf_plan_n;
+  const uint32_t NP = P.wf_plan_n[0], TJ = P.wf_plan_n[1];
+  // regions per grab: enough for ~RT0_WF_UNIT entries at this round's mean
+  // entries per region (1 in the first rounds, tens once most paths ended)
+  const uint32_t kRegionGroup = max(1u, (uint32_t)(((uint64_t)RT0_WF_UNIT * NP + TJ - 1) / max(TJ, 1u)));
   uint32_t reg = NR, pos = 0, pos_end = 0, q = 0, nc = 0, nall = 0;
   uint32_t part = blockIdx.x % kParts, tried = 0;
   auto part_lo = [&](uint32_t k) { return (uint32_t)(((uint64_t)NP * k) / kParts); };
@@ -3414,10 +3431,12 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   auto open = [&]() {
     q = 0;
     nc = nall = 0;
-    reg = pos < NP ? P.wf_plan[pos] : NR;
-    if (reg < NR) {
-      nc = P.wf_out_cnt[reg];
-      nall = nc + P.wf_sh_cnt[reg];
+    reg = NR;
+    if (pos < NP) {
+      const uint4 e = reinterpret_cast<const uint4 *>(P.wf_plan)[pos];
+      reg = e.x;
+      nc = e.y;
+      nall = e.z;
     }
   };
   grab();
