@@ -248,7 +248,10 @@ struct LaunchParams {
   int32_t wf_round, wf_R, wf_L, wf_nregions, wf_f0;
   uint32_t wf_apad, wf_slots, wf_gx;
   uint32_t *wf_ctr;
-  uint32_t *wf_plan, *wf_plan_n;  // the round's non-empty regions (wf_plan_body) and their number
+  // the round's non-empty regions (wf_plan_body): plan block b's at
+  // wf_plan[4 * (b * wf_plan_span ...)], their number and entries per block
+  uint32_t *wf_plan, *wf_plan_bn, *wf_plan_bj;
+  int32_t wf_plan_blocks, wf_plan_span;
   float4 *wf_state;
   float4 *wf_in, *wf_out;
   uint32_t *wf_in_cnt, *wf_out_cnt, *wf_sh_cnt;

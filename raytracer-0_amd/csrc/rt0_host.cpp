@@ -754,7 +754,7 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_state = al(cap * (extra ? 3 : 2) * 16), b_list = al(cap * 32), b_res = al(cap * 16),
                b_id = al(cap * 4), b_sh = al(cap * L * 48), b_shres = al(cap * L * 16), b_cnt = al((NR + 4) * 4);
-  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 7 * b_cnt + 512 + 256;
+  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 7 * b_cnt + 512 + 2048;
   if (need > c->wf_bytes) {
     if (c->d_wf) HIPCHK(c, hipFree(c->d_wf));
     c->d_wf = nullptr;
@@ -778,7 +778,8 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   p.wf_sh_cnt = (uint32_t *)take(b_cnt);
   p.wf_ctr = (uint32_t *)take(512);  // 8 range counters, 64 B apart
   p.wf_plan = (uint32_t *)take(4 * b_cnt);  // uint4 per region
-  p.wf_plan_n = (uint32_t *)take(256);
+  p.wf_plan_bn = (uint32_t *)take(1024);      // per plan block (<= 256)
+  p.wf_plan_bj = (uint32_t *)take(1024);
   p.wf_R = (int32_t)kR;
   p.wf_L = (int32_t)L;
   p.wf_nregions = (int32_t)NR;
@@ -791,6 +792,9 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
     p.wf_f0 = f0;
     p.wf_slots = (uint32_t)(apad * (size_t)std::min(fc, p.nframes - f0));
     p.wf_nregions = (int32_t)((p.wf_slots + kR - 1) / kR);
+    // plan blocks of >= 256 regions, at most 256 of them (wf_plan_prefix)
+    p.wf_plan_span = std::max(256, (p.wf_nregions + 255) / 256);
+    p.wf_plan_blocks = (p.wf_nregions + p.wf_plan_span - 1) / p.wf_plan_span;
     for (int r = 0; r < rounds; r++) {
       p.wf_round = r;
       p.wf_in = lists[r & 1];
@@ -801,8 +805,9 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
                     ? hipSuccess
                     : hipErrorLaunchFailure);
       if (r + 1 < rounds) {  // (the last round only finishes samples: nothing to march)
-        HIPCHK(c, rt0h::jit_launch(c->jit.wf_plan, &p, 1, 1, 1, c->stream, 1024) == RT0_OK ? hipSuccess
-                                                                                        : hipErrorLaunchFailure);
+        HIPCHK(c, rt0h::jit_launch(c->jit.wf_plan, &p, (unsigned)p.wf_plan_blocks, 1, 1, c->stream) == RT0_OK
+                      ? hipSuccess
+                      : hipErrorLaunchFailure);
         HIPCHK(c, rt0h::jit_launch(c->jit.wf_march, &p, std::max(1u, march_blocks), 1, 1, c->stream) == RT0_OK
                       ? hipSuccess
                       : hipErrorLaunchFailure);

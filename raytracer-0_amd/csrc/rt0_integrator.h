@@ -3324,55 +3324,92 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   }
 }
 
-// The round's plan (rt0_jit_wf_plan, one workgroup of 1024 threads): the
-// regions whose march or shadow list is not empty, in region order, as
-// (region, march entries, all entries), their number and the round's total
-// of entries -- so the march kernel's grabs skip the empty regions of the
-// late rounds and take several of their sparse regions at once (see
-// kUnitJobs), each region opened with one load.  Each thread counts a
-// contiguous run of regions (16-B loads, all issued before the first is
-// counted), the threads' counts are scanned in LDS, the runs written again.
+// The round's plan (rt0_jit_wf_plan): the regions whose march or shadow list
+// is not empty, as (region, march entries, all entries), so that the march
+// kernel's grabs skip the empty regions of the late rounds and take several
+// sparse regions at once (kRegionGroup), each region opened with one load.
+// Plan block b (wf_plan_blocks workgroups of 256 threads) lists the non-empty
+// regions of [b * span, (b + 1) * span) at plan[b * span ...] and their count
+// and entries in wf_plan_bn[b] / wf_plan_bj[b]; each march workgroup scans
+// those totals once (wf_plan_prefix) -- no device-wide prefix pass.
 DEV void wf_plan_body(const LaunchParams &P) {
-  __shared__ uint32_t scan[1024], jobs[1024];
-  const uint32_t t = threadIdx.x, T = blockDim.x;
-  const uint32_t NR = (uint32_t)P.wf_nregions;
-  const uint32_t per = ((NR + T - 1) / T + 3u) & ~3u;
-  const uint32_t lo = min(t * per, NR), hi = min(lo + per, NR);
-  const uint4 *oc = reinterpret_cast<const uint4 *>(P.wf_out_cnt), *sc = reinterpret_cast<const uint4 *>(P.wf_sh_cnt);
-  uint32_t n = 0, nj = 0;
-  for (uint32_t r = lo; r < hi; r += 4u) {
-    const uint4 a = oc[r >> 2], b = sc[r >> 2];  // (lo and per are multiples of 4; the arrays are padded)
-    const uint32_t ca[4] = {a.x, a.y, a.z, a.w}, cb[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (r + k < hi) {
-        n += (ca[k] | cb[k]) != 0u;
-        nj += ca[k] + cb[k];
-      }
+  __shared__ uint32_t wn[4], wj[4];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t NR = (uint32_t)P.wf_nregions, span = (uint32_t)P.wf_plan_span, b = blockIdx.x;
+  const uint32_t lo = min(b * span, NR), hi = min(lo + span, NR);
+  uint32_t at = 0, nj = 0;  // (block-uniform)
+  uint4 *plan = reinterpret_cast<uint4 *>(P.wf_plan) + (size_t)b * span;
+  for (uint32_t r0 = lo; r0 < hi; r0 += 256u) {
+    const uint32_t r = r0 + threadIdx.x;
+    uint32_t ca = 0, cb = 0;
+    if (r < hi) {
+      ca = P.wf_out_cnt[r];
+      cb = P.wf_sh_cnt[r];
+    }
+    const bool ne = (ca | cb) != 0u;
+    const uint64_t m = __ballot(ne);
+    uint32_t j = ca + cb;  // this wave's entries: a butterfly sum
+    for (int o = 32; o > 0; o >>= 1) j += (uint32_t)__shfl_xor((int)j, o);
+    if (lane == 0) {
+      wn[w] = (uint32_t)__popcll(m);
+      wj[w] = j;
+    }
+    __syncthreads();
+    uint32_t before = 0, total = 0, jt = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+      before += k < w ? wn[k] : 0u;
+      total += wn[k];
+      jt += wj[k];
+    }
+    if (ne) plan[at + before + (uint32_t)__popcll(m & lt)] = make_uint4(r, ca, ca + cb, 0u);
+    at += total;
+    nj += jt;
+    __syncthreads();
   }
-  scan[t] = n;
-  jobs[t] = nj;
+  if (threadIdx.x == 0) {
+    P.wf_plan_bn[b] = at;
+    P.wf_plan_bj[b] = nj;
+  }
+}
+
+// A march workgroup's view of the plan: the exclusive prefix of the plan
+// blocks' counts in LDS (wf_plan_blocks <= 256), the plan's length and the
+// round's entries
+struct WfPlan {
+  const uint32_t *pre;
+  uint32_t np, tj;
+};
+DEV WfPlan wf_plan_prefix(const LaunchParams &P) {
+  __shared__ uint32_t pre[257], tot[2];
+  const uint32_t B = (uint32_t)P.wf_plan_blocks, t = threadIdx.x;
+  if (t < 64) {  // one wave: 4 blocks per lane, a shuffle scan of the lanes' sums
+    uint32_t n[4], j = 0, s = 0;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t bb = 4 * t + k;
+      n[k] = bb < B ? P.wf_plan_bn[bb] : 0u;
+      j += bb < B ? P.wf_plan_bj[bb] : 0u;
+      s += n[k];
+    }
+    uint32_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t x = (uint32_t)__shfl_up((int)inc, o);
+      if ((int)t >= o) inc += x;
+    }
+    uint32_t e = inc - s;
+    for (int k = 0; k < 4; ++k) {
+      pre[4 * t + k] = e;
+      e += n[k];
+    }
+    for (int o = 32; o > 0; o >>= 1) j += (uint32_t)__shfl_xor((int)j, o);
+    if (t == 63) {
+      pre[256] = inc;
+      tot[0] = inc;
+      tot[1] = j;
+    }
+  }
   __syncthreads();
-  for (uint32_t d = 1; d < T; d <<= 1) {  // inclusive scan of the threads' counts and entries
-    const uint32_t x = t >= d ? scan[t - d] : 0u, y = t >= d ? jobs[t - d] : 0u;
-    __syncthreads();
-    scan[t] += x;
-    jobs[t] += y;
-    __syncthreads();
-  }
-  if (t == T - 1) {
-    P.wf_plan_n[0] = scan[t];
-    P.wf_plan_n[1] = jobs[t];
-  }
-  uint32_t at = scan[t] - n;
-  uint4 *plan = reinterpret_cast<uint4 *>(P.wf_plan);
-  for (uint32_t r = lo; r < hi; r += 4u) {
-    const uint4 a = oc[r >> 2], b = sc[r >> 2];
-    const uint32_t ca[4] = {a.x, a.y, a.z, a.w}, cb[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (r + k < hi && (ca[k] | cb[k]) != 0u) plan[at++] = make_uint4(r + k, ca[k], ca[k] + cb[k], 0u);
-  }
+  return WfPlan{pre, tot[0], tot[1]};
 }
 
 // The march kernel: persistent waves over the round's march and shadow lists.
@@ -3399,7 +3436,8 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   // serialises at ~0.1 us: one counter over every region made the late rounds
   // (a few paths left in a few regions) cost ~0.5-1 ms each in grabs alone.
   constexpr uint32_t kParts = 8;
-  const uint32_t NP = P.wf_plan_n[0], TJ = P.wf_plan_n[1];
+  const WfPlan pl = wf_plan_prefix(P);  // (one barrier, before any wave leaves)
+  const uint32_t NP = pl.np, TJ = pl.tj, PB = (uint32_t)P.wf_plan_blocks, PS = (uint32_t)P.wf_plan_span;
   // regions per grab: enough for ~RT0_WF_UNIT entries at this round's mean
   // entries per region (1 in the first rounds, tens once most paths ended)
   const uint32_t kRegionGroup = max(1u, (uint32_t)(((uint64_t)RT0_WF_UNIT * NP + TJ - 1) / max(TJ, 1u)));
@@ -3433,7 +3471,13 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     nc = nall = 0;
     reg = NR;
     if (pos < NP) {
-      const uint4 e = reinterpret_cast<const uint4 *>(P.wf_plan)[pos];
+      uint32_t lo = 0, hi = PB;  // the plan block holding entry pos: pre[lo] <= pos < pre[lo + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pl.pre[mid] <= pos) lo = mid;
+        else hi = mid;
+      }
+      const uint4 e = reinterpret_cast<const uint4 *>(P.wf_plan)[(size_t)lo * PS + (pos - pl.pre[lo])];
       reg = e.x;
       nc = e.y;
       nall = e.z;

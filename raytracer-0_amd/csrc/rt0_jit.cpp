@@ -176,7 +176,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "void rt0_jit_wf_shade(const LaunchParams P) {\n"
          "  rt0::wf_shade_body<rt0::JitScene, rt0::JitCfg, "
       << vol << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
-    o << "extern \"C\" __global__ __launch_bounds__(1024) void rt0_jit_wf_plan(const LaunchParams P) { "
+    o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_wf_plan(const LaunchParams P) { "
          "rt0::wf_plan_body(P); }\n";
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
     if (const char *e = getenv("RT0_JIT_MARCH_WAVES_PER_EU")) o << "__attribute__((amdgpu_waves_per_eu(" << atoi(e) << "))) ";
