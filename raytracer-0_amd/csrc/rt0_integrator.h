@@ -123,7 +123,7 @@ DEV float flog(float x) { return __logf(x); }
 #define RT0_WF_REFILL 1
 #endif
 #ifndef RT0_WF_UNIT  // entries a march wave takes per device-counter grab, about (wf_march_body)
-#define RT0_WF_UNIT 512
+#define RT0_WF_UNIT 256
 #endif
 #ifndef RT0_WF_PREFETCH  // march lanes hold their next job in registers (wf_march_body)
 #define RT0_WF_PREFETCH 0
@@ -3441,6 +3441,10 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   // regions per grab: enough for ~RT0_WF_UNIT entries at this round's mean
   // entries per region (1 in the first rounds, tens once most paths ended)
   const uint32_t kRegionGroup = max(1u, (uint32_t)(((uint64_t)RT0_WF_UNIT * NP + TJ - 1) / max(TJ, 1u)));
+  // a wave beyond this round's number of grabs leaves at once: in the late
+  // rounds (a few hundred grabs) the whole grid probing every range cost
+  // ~0.5 ms per round in serialised read-modify-writes
+  if (blockIdx.x * 4u + (threadIdx.x >> 6) >= (NP + kRegionGroup - 1) / kRegionGroup) return;
   uint32_t reg = NR, pos = 0, pos_end = 0, q = 0, nc = 0, nall = 0;
   uint32_t part = blockIdx.x % kParts, tried = 0;
   auto part_lo = [&](uint32_t k) { return (uint32_t)(((uint64_t)NP * k) / kParts); };
