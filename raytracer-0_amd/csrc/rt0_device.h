@@ -247,6 +247,7 @@ struct LaunchParams {
   // Path state between rounds: wf_state[k * wf_slots + slot].
   int32_t wf_round, wf_R, wf_L, wf_nregions, wf_f0;
   uint32_t wf_apad, wf_slots, wf_gx;
+  uint32_t wf_slot0;  // the launch's first slot of this part (a wavefront half on its own stream)
   uint32_t *wf_ctr;
   // the round's non-empty regions (wf_plan_body): plan block b's at
   // wf_plan[4 * (b * wf_plan_span ...)], their number and entries per block

@@ -135,6 +135,8 @@ struct rt0_ctx {
   void *d_wf = nullptr;
   size_t wf_bytes = 0;
   bool wavefront = true;  // rt0_set_wavefront (RT0_WAVEFRONT=0 at rt0_create: off)
+  hipStream_t wf_streams[3] = {};  // the wavefront halves' extra streams (wf_render)
+  hipEvent_t wf_fork = nullptr, wf_join[3] = {};
   std::string jit_err;
   std::string err;
 };
@@ -293,6 +295,11 @@ void rt0_destroy(rt0_ctx *c) {
   if (c->d_cube) (void)hipFree(c->d_cube);
   if (c->d_bvh) (void)hipFree(c->d_bvh);
   if (c->d_tris) (void)hipFree(c->d_tris);
+  for (auto &s : c->wf_streams)
+    if (s) (void)hipStreamDestroy(s);
+  if (c->wf_fork) (void)hipEventDestroy(c->wf_fork);
+  for (auto &e : c->wf_join)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -730,89 +737,123 @@ static bool wf_eligible(const rt0_ctx *c) {
 // rounds of the shade and march kernels; the samples land in p.samples and
 // rt0_sum_kernel adds them in frame order (the caller launches it).
 static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
-  // slots per region (one shade wave; the march kernel's unit of work): 512,
-  // halved down to 128 while the launch has fewer than 4 regions per march
-  // wave the device holds (an 8-way shard of C4: 8 192 regions of 512 slots
-  // for ~8 000 waves left each wave one region and its tail)
   const uint32_t L = (uint32_t)std::max(1, c->host_scene.n_lights);
   const bool extra = (p.flags & F_MIS) || ((p.flags & F_SPECTRAL) && (c->cfg.defines & RT0_USE_SPECTRAL));
   // bytes per slot: state, two march-list entries, the answer + id, L shadow entries + answers
   const size_t per_slot = (extra ? 48 : 32) + 2 * 32 + 16 + 4 + (size_t)L * (48 + 16);
   const size_t budget = getenv("RT0_WF_BYTES") ? (size_t)atoll(getenv("RT0_WF_BYTES")) : (size_t)8 << 30;
   const size_t apad = (size_t)grid.x * grid.y * 256;
+  // The slots of a frame chunk run as K independent halves on K HIP streams
+  // (RT0_WF_STREAMS, default 2): every round ends when its slowest march does
+  // (a long march's ~0.2 ms at the end of a nearly empty round), and the other
+  // half's kernels fill that tail.
+  const int K = std::max(1, std::min(4, getenv("RT0_WF_STREAMS") ? atoi(getenv("RT0_WF_STREAMS")) : 2));
+  // slots per region (one shade wave; the march kernel's unit of work): 512,
+  // halved down to 128 while a half has fewer than 4 regions per march wave
+  // the device holds (an 8-way shard of C4: 8 192 regions of 512 slots for
+  // ~8 000 waves left each wave one region and its tail)
   uint32_t kR = 512;
   if (const char *e = getenv("RT0_WF_REGION")) {
     kR = (uint32_t)std::max(64, atoi(e)) / 64 * 64;
   } else {
     const size_t waves = (size_t)std::max(1, c->jit.wf_march_blocks) * 4;
-    while (kR > 128 && apad * (size_t)p.nframes / kR < 4 * waves) kR /= 2;
+    while (kR > 128 && apad * (size_t)p.nframes / K / kR < 4 * waves) kR /= 2;
   }
   const int fc = (int)std::max<size_t>(1, std::min<size_t>((size_t)p.nframes, budget / (apad * per_slot)));
-  const size_t S = apad * (size_t)fc;
-  if (S * L >= (1ull << 32)) return fail(c, RT0_E_UNSUPPORTED, "wavefront render: too many path slots");
-  const size_t NR = (S + kR - 1) / kR, cap = NR * kR;
+  const size_t S = apad * (size_t)fc;                     // slots of a frame chunk
+  const size_t Sk = ((S + K - 1) / K + kR - 1) / kR * kR;  // slots of one half (whole regions)
+  if (Sk * L >= (1ull << 32)) return fail(c, RT0_E_UNSUPPORTED, "wavefront render: too many path slots");
+  const size_t NR = Sk / kR, cap = NR * kR;
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_state = al(cap * (extra ? 3 : 2) * 16), b_list = al(cap * 32), b_res = al(cap * 16),
                b_id = al(cap * 4), b_sh = al(cap * L * 48), b_shres = al(cap * L * 16), b_cnt = al((NR + 4) * 4);
-  const size_t need = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 7 * b_cnt + 512 + 2048;
-  if (need > c->wf_bytes) {
+  const size_t one = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 7 * b_cnt + 512 + 2048;
+  if ((size_t)K * one > c->wf_bytes) {
     if (c->d_wf) HIPCHK(c, hipFree(c->d_wf));
     c->d_wf = nullptr;
     c->wf_bytes = 0;
-    HIPCHK(c, hipMalloc(&c->d_wf, need));
-    c->wf_bytes = need;
+    HIPCHK(c, hipMalloc(&c->d_wf, (size_t)K * one));
+    c->wf_bytes = (size_t)K * one;
   }
-  char *m = (char *)c->d_wf;
-  auto take = [&](size_t b) {
-    char *q = m;
-    m += b;
-    return q;
-  };
-  p.wf_state = (float4 *)take(b_state);
-  float4 *lists[2] = {(float4 *)take(b_list), (float4 *)take(b_list)};
-  p.wf_res = (float4 *)take(b_res);
-  p.wf_res_id = (float *)take(b_id);
-  p.wf_sh = (float4 *)take(b_sh);
-  p.wf_shres = (float4 *)take(b_shres);
-  uint32_t *cnts[2] = {(uint32_t *)take(b_cnt), (uint32_t *)take(b_cnt)};
-  p.wf_sh_cnt = (uint32_t *)take(b_cnt);
-  p.wf_ctr = (uint32_t *)take(512);  // 8 range counters, 64 B apart
-  p.wf_plan = (uint32_t *)take(4 * b_cnt);  // uint4 per region
-  p.wf_plan_bn = (uint32_t *)take(1024);      // per plan block (<= 256)
-  p.wf_plan_bj = (uint32_t *)take(1024);
-  p.wf_R = (int32_t)kR;
-  p.wf_L = (int32_t)L;
-  p.wf_nregions = (int32_t)NR;
-  p.wf_apad = (uint32_t)apad;
-  p.wf_gx = grid.x;
+  for (int k = 0; k < K - 1; k++)
+    if (!c->wf_streams[k]) HIPCHK(c, hipStreamCreateWithFlags(&c->wf_streams[k], hipStreamNonBlocking));
+  if (!c->wf_fork) HIPCHK(c, hipEventCreateWithFlags(&c->wf_fork, hipEventDisableTiming));
+  for (int k = 0; k < 3; k++)
+    if (!c->wf_join[k]) HIPCHK(c, hipEventCreateWithFlags(&c->wf_join[k], hipEventDisableTiming));
+  hipStream_t st[4] = {c->stream, c->wf_streams[0], c->wf_streams[1], c->wf_streams[2]};
+  LaunchParams q[4];
+  float4 *lists[4][2];
+  uint32_t *cnts[4][2];
+  for (int k = 0; k < K; k++) {
+    LaunchParams &u = q[k];
+    u = p;
+    char *m = (char *)c->d_wf + (size_t)k * one;
+    auto take = [&](size_t b) {
+      char *r = m;
+      m += b;
+      return r;
+    };
+    u.wf_state = (float4 *)take(b_state);
+    lists[k][0] = (float4 *)take(b_list);
+    lists[k][1] = (float4 *)take(b_list);
+    u.wf_res = (float4 *)take(b_res);
+    u.wf_res_id = (float *)take(b_id);
+    u.wf_sh = (float4 *)take(b_sh);
+    u.wf_shres = (float4 *)take(b_shres);
+    cnts[k][0] = (uint32_t *)take(b_cnt);
+    cnts[k][1] = (uint32_t *)take(b_cnt);
+    u.wf_sh_cnt = (uint32_t *)take(b_cnt);
+    u.wf_ctr = (uint32_t *)take(512);          // 8 range counters, 64 B apart
+    u.wf_plan = (uint32_t *)take(4 * b_cnt);   // uint4 per region
+    u.wf_plan_bn = (uint32_t *)take(1024);     // per plan block (<= 256)
+    u.wf_plan_bj = (uint32_t *)take(1024);
+    u.wf_R = (int32_t)kR;
+    u.wf_L = (int32_t)L;
+    u.wf_apad = (uint32_t)apad;
+    u.wf_gx = grid.x;
+  }
   // persistent march waves: what the device holds at once, at most one per region
   const unsigned march_blocks = (unsigned)std::min<size_t>((size_t)c->jit.wf_march_blocks, (NR + 3) / 4);
   const int rounds = p.max_bounces + 2;
+  auto launch = [&](void *fn, const LaunchParams &u, unsigned blocks, hipStream_t s) {
+    return rt0h::jit_launch(fn, &u, blocks, 1, 1, s) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
+  };
+  HIPCHK(c, hipEventRecord(c->wf_fork, c->stream));
+  for (int k = 1; k < K; k++) HIPCHK(c, hipStreamWaitEvent(st[k], c->wf_fork, 0));
   for (int f0 = 0; f0 < p.nframes; f0 += fc) {
-    p.wf_f0 = f0;
-    p.wf_slots = (uint32_t)(apad * (size_t)std::min(fc, p.nframes - f0));
-    p.wf_nregions = (int32_t)((p.wf_slots + kR - 1) / kR);
-    // plan blocks of >= 256 regions, at most 256 of them (wf_plan_prefix)
-    p.wf_plan_span = std::max(256, (p.wf_nregions + 255) / 256);
-    p.wf_plan_blocks = (p.wf_nregions + p.wf_plan_span - 1) / p.wf_plan_span;
+    const size_t Sc = apad * (size_t)std::min(fc, p.nframes - f0);  // this chunk's slots
+    int live = 0;
+    for (int k = 0; k < K; k++) {
+      LaunchParams &u = q[k];
+      u.wf_f0 = f0;
+      u.wf_slot0 = (uint32_t)std::min(Sc, (size_t)k * Sk);
+      u.wf_slots = (uint32_t)(std::min(Sc, (size_t)(k + 1) * Sk) - u.wf_slot0);
+      u.wf_nregions = (int32_t)((u.wf_slots + kR - 1) / kR);
+      // plan blocks of >= 256 regions, at most 256 of them (wf_plan_prefix)
+      u.wf_plan_span = std::max(256, (u.wf_nregions + 255) / 256);
+      u.wf_plan_blocks = std::max(1, (u.wf_nregions + u.wf_plan_span - 1) / u.wf_plan_span);
+      if (u.wf_slots > 0) live = k + 1;
+    }
     for (int r = 0; r < rounds; r++) {
-      p.wf_round = r;
-      p.wf_in = lists[r & 1];
-      p.wf_in_cnt = cnts[r & 1];
-      p.wf_out = lists[(r + 1) & 1];
-      p.wf_out_cnt = cnts[(r + 1) & 1];
-      HIPCHK(c, rt0h::jit_launch(c->jit.wf_shade, &p, (unsigned)((p.wf_nregions + 3) / 4), 1, 1, c->stream) == RT0_OK
-                    ? hipSuccess
-                    : hipErrorLaunchFailure);
-      if (r + 1 < rounds) {  // (the last round only finishes samples: nothing to march)
-        HIPCHK(c, rt0h::jit_launch(c->jit.wf_plan, &p, (unsigned)p.wf_plan_blocks, 1, 1, c->stream) == RT0_OK
-                      ? hipSuccess
-                      : hipErrorLaunchFailure);
-        HIPCHK(c, rt0h::jit_launch(c->jit.wf_march, &p, std::max(1u, march_blocks), 1, 1, c->stream) == RT0_OK
-                      ? hipSuccess
-                      : hipErrorLaunchFailure);
+      for (int k = 0; k < live; k++) {
+        LaunchParams &u = q[k];
+        u.wf_round = r;
+        u.wf_in = lists[k][r & 1];
+        u.wf_in_cnt = cnts[k][r & 1];
+        u.wf_out = lists[k][(r + 1) & 1];
+        u.wf_out_cnt = cnts[k][(r + 1) & 1];
+        HIPCHK(c, launch(c->jit.wf_shade, u, (unsigned)((u.wf_nregions + 3) / 4), st[k]));
+      }
+      if (r + 1 == rounds) break;  // (the last round only finishes samples: nothing to march)
+      for (int k = 0; k < live; k++) {
+        HIPCHK(c, launch(c->jit.wf_plan, q[k], (unsigned)q[k].wf_plan_blocks, st[k]));
+        HIPCHK(c, launch(c->jit.wf_march, q[k], std::max(1u, march_blocks), st[k]));
       }
     }
+  }
+  for (int k = 1; k < K; k++) {
+    HIPCHK(c, hipEventRecord(c->wf_join[k - 1], st[k]));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->wf_join[k - 1], 0));
   }
   return RT0_OK;
 }

@@ -3231,7 +3231,7 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       marched = j0.w >= 0.0f;
     }
     // the slot's frame and pixel (pass_body's tile order within a frame)
-    const uint32_t f = slot / P.wf_apad, loc = slot - f * P.wf_apad;
+    const uint32_t gs = P.wf_slot0 + slot, f = gs / P.wf_apad, loc = gs - f * P.wf_apad;
     const uint32_t tile = loc >> 8, tx = tile % P.wf_gx, ty = tile / P.wf_gx, wv = (loc >> 6) & 3u, ln = loc & 63u;
     const int px = P.vp_x0 + (int)(tx * 16u + (ln & 7u) + ((wv & 1u) << 3));
     const int r = P.vp_y0 + (int)(ty * 16u + (ln >> 3) + ((wv >> 1) << 3));
