@@ -18,7 +18,11 @@ runs under it; WORLD_SIZE must equal --gpus.  One process per GPU:
     dealt round-robin over ranks (rt0_set_shard); each rank renders its bands
     straight into a band-packed torch buffer (rt0_set_accum_buffer_compact:
     the RCCL send buffer as it stands), and rank 0 gathers the bands over RCCL
-    into one preallocated buffer and reorders them with one index_copy_;
+    into one preallocated buffer and reorders them with one index_copy_.  By
+    default a step at N GPUs renders N x spp passes ("weak" scaling: every
+    rank renders its 1/N of the rows for all of them, the per-GPU work of N =
+    1; C4 at N = 8 is then the 64-spp render BASELINE.md quotes);
+    `--scaling strong` splits the N = 1 step N ways instead;
   * ReSTIR workloads (C3, C5): two round-robin row bands per rank
     (shard.interleaved_band), a halo exchange of the newest reservoir planes
     at every band boundary after every pass (RCCL point-to-point,
@@ -28,7 +32,7 @@ accumulator zeroing, the exchanges, the gather) with events, so steps run back
 to back with no host synchronisation between them (one device-wide
 synchronize ends the timed region; the last step's kernel time is read
 after it).  Both gathers are inside the timed
-region ("strong" scaling: total work fixed); rank 0's gather time is reported
+region; rank 0's gather time is reported
 separately.  `--dist-backend gloo` stages every transfer through host memory:
 the one-GPU rehearsal of the N>1 path (all ranks on one device with
 RT0_BENCH_DEVICE=0, tests/test_bench_dist.py).
@@ -302,14 +306,14 @@ class ClockSampler:
 class Progressive:
     """C1/C2/C4: 16-row bands round-robin, band-packed accumulators, one gather."""
 
-    def __init__(self, rt0, torch, wl, rank, world, local, staged=False):
+    def __init__(self, rt0, torch, wl, rank, world, local, staged=False, spp=None):
         import rt0.shard as shard
         from rt0 import workloads
         self.torch, self.world = torch, world
         W, H = wl["width"], wl["height"]
         self.r = rt0.Renderer(W, H, device=local)
         workloads.configure(self.r, wl)
-        self.spp = wl["spp"]
+        self.spp = spp or wl["spp"]
         self.gather = None
         if world > 1:
             self.r.set_shard(rank, world, BAND)
@@ -536,6 +540,12 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N>1: nccl = RCCL over xGMI; gloo = every transfer staged through host memory")
     ap.add_argument("--save-image", default=None, help="rank 0: np.save the last step's HDR image (H x W x 4)")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="progressive workloads (C1, C2, C4) at N GPUs: weak = a step renders N x spp passes, each "
+                         "rank its 1/N of the rows for all of them (per-GPU work fixed; C4 at N = 8 is the 64-spp "
+                         "job BASELINE.md quotes); strong = spp passes split N ways.  ReSTIR workloads are always "
+                         "strong (each pass reads the previous pass's reservoirs).")
+    ap.add_argument("--spp", type=int, default=None, help="passes per step at N = 1 (default: the workload's)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -561,6 +571,10 @@ def main():
         dist.init_process_group(args.dist_backend)  # "nccl" = RCCL on ROCm
     W, H = wl["width"], wl["height"]
 
+    base_spp = args.spp or wl["spp"]
+    weak = not workloads.restir(wl) and args.scaling == "weak"
+    step_spp = base_spp * world if weak else base_spp  # passes per step over the whole image
+    wl = dict(wl, spp=step_spp)
     job = (Restir if workloads.restir(wl) else Progressive)(rt0, torch, wl, rank, world, local, staged=staged)
     job.r.set_jit(bool(args.jit))
     job.r.set_executor_compat(args.executor_compat)
@@ -667,7 +681,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (the reference's own scene grammar and materials; no external data)",

@@ -1,7 +1,8 @@
 """Load balance of the progressive workloads' 16-row round-robin band sharding
-(bench.py ProgressiveJob, rt0_set_shard) on one device: every rank's share of
+(bench.py Progressive, rt0_set_shard) on one device: every rank's share of
 one bench step rendered alone (the other ranks' bands skipped), for N = 2, 4,
-8.  Prints per-rank kernel times (HIP events, best of 3), max/mean, the
+8, under strong scaling (spp passes split N ways) and under bench.py's
+default weak scaling (N x spp passes, each rank its rows for all of them).  Prints per-rank kernel times (HIP events, best of 3), max/mean, the
 strong-scaling ceiling T1 / (N * slowest rank) and the sum of the ranks'
 times over T1 (how much per-rank overhead sharding adds) -- the gather and
 RCCL are excluded.
@@ -26,16 +27,17 @@ def main():
         wl = workloads.get(key)
         W, H, spp = wl["width"], wl["height"], wl["spp"]
 
-        def timed(rank, n):
+        def timed(rank, n, frames=None):
+            frames = frames or spp
             r = rt0.Renderer(W, H)
             workloads.configure(r, wl)
             if n > 1:
                 r.set_shard(rank, n, BAND)
-            r.render(1, spp)  # warm-up (JIT compile, buffers)
+            r.render(1, frames)  # warm-up (JIT compile, buffers)
             ts = []
             for k in range(3):
                 r.clear()
-                r.render(1 + spp * (k + 1), spp)
+                r.render(1 + frames * (k + 1), frames)
                 ts.append(r.last_kernel_ms()[0])
             path = r.last_render_path()
             r.close()
@@ -50,6 +52,14 @@ def main():
             res[str(n)] = {"rank_ms": [round(t, 3) for t in per], "max_over_mean": round(max(per) / mean, 3),
                            "ceiling": round(t1 / (n * max(per)), 3), "sum_over_whole": round(sum(per) / t1, 3)}
             print(key, n, res[str(n)], flush=True)
+            # bench.py's default N > 1 step (weak scaling): n x spp passes, each
+            # rank its 1/n of the rows for all of them -- the ceiling is the N = 1
+            # step time over the slowest rank's
+            perw = [timed(rank, n, spp * n)[0] for rank in range(n)]
+            res[str(n) + "_weak"] = {"rank_ms": [round(t, 3) for t in perw],
+                                     "max_over_mean": round(max(perw) * n / sum(perw), 3),
+                                     "ceiling": round(t1 / max(perw), 3)}
+            print(key, n, "weak", res[str(n) + "_weak"], flush=True)
         out[key] = res
     print(json.dumps(out))
 

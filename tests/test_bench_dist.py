@@ -41,9 +41,24 @@ def run_bench(tmp_path, config, gpus, extra=()):
 @pytest.mark.parametrize("config", ["c2", "c3", "c5"])
 def test_bench_two_ranks_match_one(tmp_path, gpu_required, config):
     one, a = run_bench(tmp_path, config, 1)
-    two, b = run_bench(tmp_path, config, 2, ["--dist-backend", "gloo"])
+    two, b = run_bench(tmp_path, config, 2, ["--dist-backend", "gloo", "--scaling", "strong"])
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["config"]["dist_backend"] == "gloo"
     assert a.shape == b.shape
+    assert np.isfinite(a).all() and a[..., :3].mean() > 0.0
+    assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_bench_weak_scaling_two_ranks(tmp_path, gpu_required, config):
+    """The default N>1 step of a progressive workload (weak scaling): N x spp
+    passes, each rank rendering its rows for all of them -- the gathered image
+    equals one rank rendering 2 x spp passes, bit for bit, and the line says
+    "weak" with the samples of the whole job."""
+    spp = 4
+    one, a = run_bench(tmp_path, config, 1, ["--spp", str(2 * spp)])
+    two, b = run_bench(tmp_path, config, 2, ["--dist-backend", "gloo", "--spp", str(spp)])
+    assert two["scaling"] == "weak" and two["config"]["spp"] == 2 * spp == one["config"]["spp"]
     assert np.isfinite(a).all() and a[..., :3].mean() > 0.0
     assert np.array_equal(a, b), np.abs(a - b).max()
