@@ -316,17 +316,21 @@ int rt0_set_executor_compat(rt0_ctx *ctx, int enable);
  * off) or 0 = inline calls.  Executor compatibility always runs them inline.
  * Replaces nothing in the reference: the GL pipeline has no such choice. */
 int rt0_set_defer_light_sampling(rt0_ctx *ctx, int enable);
-/* Wavefront rounds for SDF scenes (scene-specialised kernels, no ReSTIR, no
- * triangle models, no SDF light): a pass runs as MAX_BOUNCES + 2 rounds of a
- * shade kernel (each path's bounce up to its next SDF march) and a march
- * kernel (every pending sphere trace, normal and shadow march on lanes that
- * refill as they finish), the launch's passes side by side; samples are added
- * in pass order (rt0_integrator.h wf_shade_body).  The same map() steps as
- * the pass kernel; light-sampling sums are formed in call order one round
- * later, so FMA placement can differ at the last bit (tests/
- * test_gpu_wavefront.py).  1 (default; RT0_WAVEFRONT=0 in the environment
- * turns it off) or 0 = the pass kernel.  Replaces nothing in the reference. */
-int rt0_set_wavefront(rt0_ctx *ctx, int enable);
+/* Wavefront rounds.  mode 1 (default): SDF scenes (scene-specialised
+ * kernels, no ReSTIR, no triangle models, no SDF light): a pass runs as
+ * MAX_BOUNCES + 2 rounds of a shade kernel (each path's bounce up to its next
+ * SDF march) and a march kernel (every pending sphere trace, normal and shadow
+ * march on lanes that refill as they finish), the launch's passes side by
+ * side; samples are added in pass order (rt0_integrator.h wf_shade_body).
+ * The same map() steps as the pass kernel; light-sampling sums are formed in
+ * call order one round later, so FMA placement can differ at the last bit
+ * (tests/test_gpu_wavefront.py).  mode 2: also the deferred ReSTIR passes of
+ * scenes with triangle models -- shade rounds and a closest-hit walk kernel
+ * (wf_restir_shade_body, wf_walk_body); the same walks and hits, measured
+ * slower than the pass kernel on BASELINE config 5, hence not
+ * the default.  0 = the pass kernel.  RT0_WAVEFRONT=<mode> in the environment
+ * sets the default at rt0_create.  Replaces nothing in the reference. */
+int rt0_set_wavefront(rt0_ctx *ctx, int mode);
 /* Compile the scene-specialised kernel for (scene, config) without a device
  * (hipRTC only): checks the generated code builds; *code_size receives the
  * code-object size.  err (may be NULL) receives the compiler log. */
@@ -358,7 +362,7 @@ int rt0_last_kernel_ms(const rt0_ctx *ctx, float *ms, int *launches);
 #define RT0_PATH_AOT 1        /* the ahead-of-time pass kernels (rt0_set_jit(0), counting) */
 #define RT0_PATH_PASS 2       /* the scene-specialised pass kernel */
 #define RT0_PATH_DEFERRED 3   /* ReSTIR: pass + light sampling (+ walk) + resolve */
-#define RT0_PATH_WAVEFRONT 4  /* SDF scenes: wavefront shade + march rounds (rt0_set_wavefront) */
+#define RT0_PATH_WAVEFRONT 4  /* wavefront shade + march / walk rounds (rt0_set_wavefront) */
 int rt0_last_render_path(const rt0_ctx *ctx);
 /* Bytes of device scratch the context holds for frame-chunked launches
  * (per-frame sample planes over the launch rectangle; grows on demand). */

@@ -134,7 +134,7 @@ struct rt0_ctx {
   // answers, the shadow list and its answers, sized for wf_bytes
   void *d_wf = nullptr;
   size_t wf_bytes = 0;
-  bool wavefront = true;  // rt0_set_wavefront (RT0_WAVEFRONT=0 at rt0_create: off)
+  int wavefront = 1;  // rt0_set_wavefront mode (RT0_WAVEFRONT=<mode> at rt0_create)
   hipStream_t wf_streams[3] = {};  // the wavefront halves' extra streams (wf_render)
   hipEvent_t wf_fork = nullptr, wf_join[3] = {};
   std::string jit_err;
@@ -256,7 +256,7 @@ int rt0_create(int width, int height, int device, rt0_ctx **out) {
   c->device = device;
   if (const char *e = getenv("RT0_JIT")) c->use_jit = atoi(e) != 0;
   if (const char *e = getenv("RT0_DEFER_NEE")) c->defer_nee = atoi(e) != 0;
-  if (const char *e = getenv("RT0_WAVEFRONT")) c->wavefront = atoi(e) != 0;
+  if (const char *e = getenv("RT0_WAVEFRONT")) c->wavefront = std::max(0, std::min(2, atoi(e)));
   rt0h::default_config(c->cfg);
   int rc;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -719,12 +719,16 @@ static int choose_variant(const rt0_ctx *c) {
 // whose light-sampling shadow rays are decided by quadric lights: no SDF
 // entry is a light or is sampled as one (direct_light's WfShadow), at most 32
 // light slots (one bit each in the path state), 1..127 bounces (the state's
-// 7-bit counters).  rt0_set_wavefront(0) keeps the pass kernel.
-static bool wf_eligible(const rt0_ctx *c) {
+// 7-bit counters) -- and the deferred ReSTIR passes of scenes with triangle
+// models whose light sampling has the occlusion-walk kernel (`restir_walk`:
+// render_impl's want_walk; wf_restir_shade_body).  rt0_set_wavefront(0)
+// keeps the pass kernel.
+static bool wf_eligible(const rt0_ctx *c, bool restir_walk) {
   const SceneDev &s = c->host_scene;
   const rt0_config &g = c->cfg;
-  if (!c->wavefront || !c->use_jit || c->counting || (g.defines & RT0_USE_RESTIR)) return false;
-  if (s.n_sdfs <= 0 || s.n_models > 0 || s.n_lights > 32 || g.max_bounces < 1 || g.max_bounces > 127) return false;
+  if (!c->wavefront || !c->use_jit || c->counting || g.max_bounces < 1 || g.max_bounces > 127) return false;
+  if (g.defines & RT0_USE_RESTIR) return restir_walk && c->wavefront >= 2;
+  if (s.n_sdfs <= 0 || s.n_models > 0 || s.n_lights > 32) return false;
   for (int i = s.n_meshes; i < s.n_meshes + s.n_sdfs; i++)
     if (s.mat[i].type == 0 /* LIGHT */) return false;
   for (int i = 0; i < s.n_lights; i++)
@@ -736,8 +740,12 @@ static bool wf_eligible(const rt0_ctx *c) {
 // frame chunks of as many frames as wf_bytes holds, each MAX_BOUNCES + 2
 // rounds of the shade and march kernels; the samples land in p.samples and
 // rt0_sum_kernel adds them in frame order (the caller launches it).
+// ReSTIR (one pass, p.nframes = 1): MAX_BOUNCES + 1 rounds of the shade and
+// closest-hit walk kernels over 64-slot regions (one per pass wave); the
+// caller then launches the deferred-pass kernels (nee, walk, resolve).
 static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
-  const uint32_t L = (uint32_t)std::max(1, c->host_scene.n_lights);
+  const bool restir = (c->cfg.defines & RT0_USE_RESTIR) != 0;
+  const uint32_t L = restir ? 0u : (uint32_t)std::max(1, c->host_scene.n_lights);
   const bool extra = (p.flags & F_MIS) || ((p.flags & F_SPECTRAL) && (c->cfg.defines & RT0_USE_SPECTRAL));
   // bytes per slot: state, two march-list entries, the answer + id, L shadow entries + answers
   const size_t per_slot = (extra ? 48 : 32) + 2 * 32 + 16 + 4 + (size_t)L * (48 + 16);
@@ -753,7 +761,9 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   // the device holds (an 8-way shard of C4: 8 192 regions of 512 slots for
   // ~8 000 waves left each wave one region and its tail)
   uint32_t kR = 512;
-  if (const char *e = getenv("RT0_WF_REGION")) {
+  if (restir) {
+    kR = 64;  // the deferred calls' regions are the pass waves'
+  } else if (const char *e = getenv("RT0_WF_REGION")) {
     kR = (uint32_t)std::max(64, atoi(e)) / 64 * 64;
   } else {
     const size_t waves = (size_t)std::max(1, c->jit.wf_march_blocks) * 4;
@@ -762,7 +772,7 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   const int fc = (int)std::max<size_t>(1, std::min<size_t>((size_t)p.nframes, budget / (apad * per_slot)));
   const size_t S = apad * (size_t)fc;                     // slots of a frame chunk
   const size_t Sk = ((S + K - 1) / K + kR - 1) / kR * kR;  // slots of one half (whole regions)
-  if (Sk * L >= (1ull << 32)) return fail(c, RT0_E_UNSUPPORTED, "wavefront render: too many path slots");
+  if (Sk * std::max(1u, L) >= (1ull << 32)) return fail(c, RT0_E_UNSUPPORTED, "wavefront render: too many path slots");
   const size_t NR = Sk / kR, cap = NR * kR;
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_state = al(cap * (extra ? 3 : 2) * 16), b_list = al(cap * 32), b_res = al(cap * 16),
@@ -814,7 +824,7 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   }
   // persistent march waves: what the device holds at once, at most one per region
   const unsigned march_blocks = (unsigned)std::min<size_t>((size_t)c->jit.wf_march_blocks, (NR + 3) / 4);
-  const int rounds = p.max_bounces + 2;
+  const int rounds = p.max_bounces + (restir ? 1 : 2);
   auto launch = [&](void *fn, const LaunchParams &u, unsigned blocks, hipStream_t s) {
     return rt0h::jit_launch(fn, &u, blocks, 1, 1, s) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
   };
@@ -923,7 +933,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   const bool want_walk = defer && nee_walk_enabled() && c->host_scene.n_models > 0 && c->n_tris > 0 &&
                          c->host_scene.n_sdfs == 0 && !c->host_scene.any_tex && c->cfg.render_mode == 0 &&
                          (size_t)grid.x * grid.y * 4 * 64 * (size_t)p.max_bounces < (1u << 29) - 1u;
-  const bool want_wf = wf_eligible(c);
+  const bool want_wf = wf_eligible(c, want_walk);
   if (c->use_jit && !c->counting) {
     if (c->jit_dirty || !(c->jit.pass || c->jit.wf_shade) || (defer != (c->jit.nee != nullptr)) ||
         (defer && want_walk != (c->jit.walk != nullptr)) || want_wf != (c->jit.wf_shade != nullptr)) {
@@ -1030,7 +1040,12 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       if (defer) {
         // waves wholly outside the viewport write no count
         HIPCHK(c, hipMemsetAsync(c->d_nee_count, 0, pass_waves * sizeof(uint32_t), c->stream));
-        HIPCHK(c, launch(p, 1, grid));
+        if (wf_run) {  // the pass's paths as wavefront rounds (shade + closest-hit walk)
+          int rc = wf_render(c, p, grid);
+          if (rc != RT0_OK) return rc;
+        } else {
+          HIPCHK(c, launch(p, 1, grid));
+        }
         // one light-sampling wave per RT0_NEE_REGIONS pass waves' regions
         const unsigned nee_waves = (unsigned)((pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave());
         HIPCHK(c, rt0h::jit_launch(c->jit.nee, &p, (nee_waves + 3) / 4, 1, 1, c->stream) == RT0_OK
@@ -1271,7 +1286,7 @@ int rt0_set_jit(rt0_ctx *c, int enable) {
 
 int rt0_set_wavefront(rt0_ctx *c, int enable) {
   if (!c) return RT0_E_ARG;
-  c->wavefront = enable != 0;  // the next render picks the matching JIT module
+  c->wavefront = std::max(0, std::min(2, enable));  // the next render picks the matching JIT module
   return RT0_OK;
 }
 

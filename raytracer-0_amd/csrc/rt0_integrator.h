@@ -122,11 +122,14 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_WF_REFILL  // free lanes that trigger a march-kernel refill (wf_march_body)
 #define RT0_WF_REFILL 1
 #endif
+#ifndef RT0_WF_WALK_REFILL  // free lanes that trigger a walk-kernel refill (wf_walk_body)
+#define RT0_WF_WALK_REFILL 16
+#endif
+#ifndef RT0_WF_INLINE_NODES  // BVH nodes the ReSTIR shade kernel walks before parking a ray (intersect)
+#define RT0_WF_INLINE_NODES 1
+#endif
 #ifndef RT0_WF_UNIT  // entries a march wave takes per device-counter grab, about (wf_march_body)
 #define RT0_WF_UNIT 256
-#endif
-#ifndef RT0_WF_PREFETCH  // march lanes hold their next job in registers (wf_march_body)
-#define RT0_WF_PREFETCH 0
 #endif
 DEV float nc_fract(float x) {
 #pragma clang fp contract(off)
@@ -445,8 +448,11 @@ DEV uint32_t wave_append(uint32_t *ctr) {
 // Leaves hold one triangle and are tested in place, left before right; the
 // first leaf test of every lane runs in one block whichever side it is on
 // (8.36-8.39 vs 8.57-8.59 ms at 1024^2).
+// budget (the wavefront ReSTIR shade kernel): stop after that many nodes,
+// *complete = false if the walk had not finished.
 template <bool ANY = false>
-DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr) {
+DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr,
+                    int budget = 0x7fffffff, bool *complete = nullptr) {
   BvhStack stk;
   int sp = 0, node = 0, best = -1;
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
@@ -454,6 +460,10 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
   // a ray visits each of the n-1 nodes at most once: the cap only guarantees
   // that every wave exits even on a corrupt tree
   for (int guard = 2 * P.n_tris + 8; guard > 0; --guard) {
+    if (complete && budget-- <= 0) {
+      *complete = false;
+      break;
+    }
     const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
     const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
     float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
@@ -737,7 +747,32 @@ struct Geometry {
     });
     if constexpr (Scene::kMayHaveModels) {  // TRIANGLE models (after the quadrics, before the SDF march)
       if (sc.n_models() > 0 && P.n_tris > 0) {
-        const int ti = bvh_closest(P, o, d, m, tmin, nbvh);
+        int ti;
+        if (RT0_WAVEFRONT != 0 && !SDF && ms) {
+          // wavefront ReSTIR rounds: the closest-hit walk kernel (wf_walk_body)
+          // answers the ray -- the first call parks it with the quadrics' bound,
+          // the same call after the walk recomputes the quadrics (deterministic)
+          // and takes the walk's (t, triangle)
+          if (!ms->done) {
+            // the walk's first RT0_WF_INLINE_NODES nodes here: a ray that misses
+            // the model's root boxes (most of them) or ends that soon is
+            // answered in place; the others are walked again from the root
+            float tb = tmin;
+            bool complete = true;
+            ti = bvh_closest(P, o, d, m, tb, nbvh, RT0_WF_INLINE_NODES, &complete);
+            if (!complete) {
+              *ms = March{o, d, tmin, 0.f, 0.f, 0, true, false, mk(0.f, 0.f, 0.f)};
+              return -1.0f;
+            }
+            tmin = tb;
+          } else {
+            ms->done = false;
+            ti = __float_as_int(ms->id);
+            if (ti >= 0) tmin = ms->t;
+          }
+        } else {
+          ti = bvh_closest(P, o, d, m, tmin, nbvh);
+        }
         if (ti >= 0) {
           const TriDev T = P.tris[ti];
           const v3 e0 = mk(T.e0x, T.e0y, T.e0z), e1 = mk(T.e1x, T.e1y, T.e1z);
@@ -2202,6 +2237,10 @@ struct Integrator {
   // jobs (wf_nee_surface / wf_nee_volume)
   static constexpr bool WF = RT0_WAVEFRONT != 0 && SDF && !RESTIR && !COUNT;
   static constexpr bool SUSP = SDF && !RESTIR && !COUNT && !WF;
+  // WFB (RT0_WAVEFRONT modules of ReSTIR scenes with triangle models): the
+  // bounce step in the wavefront ReSTIR shade kernel -- a closest-hit query of
+  // the triangles parks the path for the walk kernel (wf_restir_shade_body)
+  static constexpr bool WFB = RT0_WAVEFRONT != 0 && RESTIR && !SDF && !COUNT && Scene::kMayHaveModels;
   struct NeeCtx {
     v3 x, n, acc;  // surface: hit point, nl, sum over lights; volume: scatter point, incoming rd
     float seed;    // surface: the light-sampling seed base; volume: the path seed
@@ -2218,6 +2257,7 @@ struct Integrator {
     NeeCtx nc;
   };
   DEV March *march_slot(Path &ps) {
+    if constexpr (WFB) return (sc.n_models() > 0 && P.n_tris > 0) ? &ps.ms : nullptr;
     if constexpr (!SUSP && !WF) return nullptr;
     // with triangle models the resumed call would walk the BVH again: no budget
     if constexpr (Scene::kMayHaveModels)
@@ -2353,7 +2393,7 @@ struct Integrator {
     if (COUNT) ++n_iter;
     Hit hit;
     float t = isect(ro, rd, hit, march_slot(ps));
-    if ((SUSP || WF) && t < 0.0f) return true;  // march pending: step() repeats this bounce once it is done
+    if ((SUSP || WF || WFB) && t < 0.0f) return true;  // march (or walk) pending: step() repeats this bounce once it is done
     if constexpr (VOL) {
       if (flag(F_VOL)) {
         float sd = -flog(fmaxf(hash(nc_addmul(seed + 4729.3f, (float)depth, 991.1f)), 1e-6f)) / VOL_SIGMA_T;
@@ -2758,8 +2798,9 @@ template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   // (a wavefront module parks pending marches for its march kernel: its SDF
   // paths cannot run here)
-  static_assert(!Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::WF,
-                "RT0_WAVEFRONT modules render SDF scenes through wf_shade_body / wf_march_body");
+  static_assert(!Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::WF &&
+                    !Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::WFB,
+                "RT0_WAVEFRONT modules render through wf_shade_body / wf_restir_shade_body");
   const SceneTables tabs = scene_tables(sc);  // (before any thread leaves: one barrier)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lx = (lane & 7) + ((wave & 1) << 3);
@@ -3324,6 +3365,147 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   }
 }
 
+// ============================================= wavefront ReSTIR model renders
+// ReSTIR scenes with triangle models (C5: a glass icosphere of 81 920
+// triangles under 10 lights) spent half their pass kernel in the inline
+// closest-hit walk at a third of the lanes busy: one lane's ray walks a deep
+// subtree while its neighbours' rays missed the model or finished.  Here the
+// pass kernel's paths run as rounds of
+//   rt0_jit_wf_shade (wf_restir_shade_body): per path slot, the bounce step of
+//     the pass kernel (Integrator::step, RESTIR, deferred sampleLightsReSTIR
+//     calls appended to the pass wave's NeeRec region as before) up to the
+//     next closest-hit query of the triangles, whose ray (bounded by the
+//     quadrics' closest t) is parked as an entry of the region's list;
+//   rt0_jit_wf_plan + rt0_jit_wf_walk (wf_walk_body): the entries walked
+//     through the BVH by persistent waves whose lanes refill as they finish.
+// One region = one pass wave (64 slots, pass_body's pixel order), so the
+// deferred-call regions, rt0_jit_nee, rt0_jit_walk and rt0_jit_resolve run
+// unchanged after the last round.  Every walk is bvh_closest's (same node
+// order, same tests, strict t < tmin) and the quadric part of intersection()
+// is recomputed on resume, so the samples are bit-identical to the pass
+// kernel's.  Path state, wf_state[k * wf_slots + slot]: k = 0 acc.xyz,
+// mask.x; 1: mask.yz, packed bounce counters (wf_shade_body's layout), the
+// deferred calls so far; 2 (MIS or spectral): previous normal, hero.
+template <class Scene, class Cfg, bool VOL, bool SPECTRAL>
+DEV void wf_restir_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  const SceneTables tabs = scene_tables(sc);  // (one barrier, before any wave leaves)
+  if (blockIdx.x == 0 && threadIdx.x < 8) P.wf_ctr[16 * threadIdx.x] = 0u;  // the walk kernel's range counters
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
+  if (w >= (uint32_t)P.wf_nregions) return;
+  using It = Integrator<Scene, Cfg, true, VOL, false, SPECTRAL, false>;
+  static_assert(It::WFB, "wavefront ReSTIR shading needs a module of triangle models (RT0_WAVEFRONT)");
+  constexpr bool kExtra = wf_extra_state<Cfg, SPECTRAL>();
+  const uint32_t S = P.wf_slots;
+  const uint32_t nw = (P.wf_slot0 >> 6) + w;  // the pass wave (wf_slot0: whole waves)
+  *(volatile uint32_t *)wf_wave_counter(0) = 0u;  // (every lane stores the same value)
+  *(volatile uint32_t *)nee_wave_counter() = P.wf_round == 0 ? 0u : P.nee_count[nw];
+  const uint32_t n = P.wf_round == 0 ? 64u : P.wf_in_cnt[w];
+  const size_t rbase = (size_t)w * 64u;
+  if (lane < n) do {
+    uint32_t slot;
+    v3 ro = mk(0.f, 0.f, 0.f), rd = ro;
+    bool walked = false;
+    if (P.wf_round == 0) {
+      slot = (uint32_t)rbase + lane;
+      if (slot >= S) break;
+    } else {
+      const float4 j0 = P.wf_in[2 * (rbase + lane)], j1 = P.wf_in[2 * (rbase + lane) + 1];
+      slot = __float_as_uint(j1.w);
+      ro = mk(j0.x, j0.y, j0.z);
+      rd = mk(j1.x, j1.y, j1.z);
+      walked = j0.w >= 0.0f;
+    }
+    const uint32_t loc = P.wf_slot0 + slot;  // pass_body's tile order (one frame)
+    const uint32_t tile = loc >> 8, tx = tile % P.wf_gx, ty = tile / P.wf_gx, wv = (loc >> 6) & 3u, ln = loc & 63u;
+    const int px = P.vp_x0 + (int)(tx * 16u + (ln & 7u) + ((wv & 1u) << 3));
+    const int r = P.vp_y0 + (int)(ty * 16u + (ln >> 3) + ((wv >> 1) << 3));
+    if (px >= P.vp_x1 || r >= P.vp_y1) break;
+    const int py = image_row(P, r);
+    if (py >= P.height) break;
+    const size_t pix = (size_t)py * P.width + px;
+    It it(P, sc, cfg);
+    it.use_tables(tabs);
+    it.set_pixel(px, py);
+    it.frame = P.frame0;
+    it.nee_pix = (int32_t)pix;
+    it.nee_wave = nw;
+    typename It::Path ps;
+    bool alive = true;
+    if (P.wf_round == 0) {
+      it.begin_sample(ps);
+      ps.ms.active = ps.ms.done = false;
+    } else {
+      const float4 s0 = P.wf_state[slot], s1 = P.wf_state[(size_t)S + slot];
+      const uint32_t pk = __float_as_uint(s1.z);
+      ps.ro = ro;
+      ps.rd = rd;
+      ps.acc = mk(s0.x, s0.y, s0.z);
+      ps.mask = mk(s0.w, s1.x, s1.y);
+      ps.prev_nl = mk(0.f, 1.f, 0.f);
+      if constexpr (kExtra) {
+        const float4 s2 = P.wf_state[2 * (size_t)S + slot];
+        ps.prev_nl = mk(s2.x, s2.y, s2.z);
+        it.hero = s2.w;
+      } else {
+        it.hero = 550.0f;
+      }
+      ps.seed = it.pixel_seed();
+      ps.depth = (int)(pk & 127u);
+      ps.spec = ((pk >> 7) & 1u) != 0u;
+      it.diff_b = (int)((pk >> 8) & 127u);
+      it.spec_b = (int)((pk >> 15) & 127u);
+      it.scat_ev = (int)((pk >> 22) & 127u);
+      it.nee_k = (int32_t)__float_as_uint(s1.w);
+      it.fin = empty_res();  // (only the deferred calls touch g_final_reservoir)
+      it.gr_have = false;
+      ps.ms.active = false;
+      ps.ms.done = walked;
+      if (walked) {
+        const float4 q = P.wf_res[rbase + lane];
+        ps.ms.t = q.x;
+        ps.ms.id = q.y;  // the triangle (int bits) or -1
+      }
+      alive = walked;
+    }
+    // the bounce this walk answers, then the next bounces up to the next walk
+    while (alive && !ps.ms.active) alive = it.step(ps);
+    if (alive) {
+      const uint32_t pk = (uint32_t)ps.depth | (ps.spec ? 1u << 7 : 0u) | ((uint32_t)it.diff_b << 8) |
+                          ((uint32_t)it.spec_b << 15) | ((uint32_t)it.scat_ev << 22);
+      P.wf_state[slot] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, ps.mask.x);
+      P.wf_state[(size_t)S + slot] = make_float4(ps.mask.y, ps.mask.z, __uint_as_float(pk), __uint_as_float((uint32_t)it.nee_k));
+      if constexpr (kExtra) P.wf_state[2 * (size_t)S + slot] = make_float4(ps.prev_nl.x, ps.prev_nl.y, ps.prev_nl.z, it.hero);
+      const uint32_t o = wave_append(wf_wave_counter(0));
+      const March &m = ps.ms;
+      P.wf_out[2 * (rbase + o)] = make_float4(m.o.x, m.o.y, m.o.z, m.tmin);
+      P.wf_out[2 * (rbase + o) + 1] = make_float4(m.d.x, m.d.y, m.d.z, __uint_as_float(slot));
+    } else {
+      // pass_body's deferred-pass ending: the path's own radiance and its
+      // number of deferred calls for rt0_jit_resolve; without deferred calls
+      // the reservoir MRTs here (rt0_jit_nee writes them otherwise)
+      P.nee_partial[pix] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, it.hero);
+      P.nee_n[pix] = it.nee_k;
+      if (it.nee_k == 0 && P.rout_main != nullptr && P.rout_aux != nullptr) {
+        if (it.flag(F_RESTIR_DEF)) {
+          const Res q = empty_res();
+          P.rout_main[pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
+          P.rout_aux[pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+        } else {
+          P.rout_main[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+          P.rout_aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  } while (false);
+  // (the wave has reconverged: every append is counted)
+  if (lane == 0) {
+    P.wf_out_cnt[w] = *(volatile uint32_t *)wf_wave_counter(0);
+    P.wf_sh_cnt[w] = 0u;
+    P.nee_count[nw] = *(volatile uint32_t *)nee_wave_counter();
+  }
+}
+
 // The round's plan (rt0_jit_wf_plan): the regions whose march or shadow list
 // is not empty, as (region, march entries, all entries), so that the march
 // kernel's grabs skip the empty regions of the late rounds and take several
@@ -3412,43 +3594,32 @@ DEV WfPlan wf_plan_prefix(const LaunchParams &P) {
   return WfPlan{pre, tot[0], tot[1]};
 }
 
-// The march kernel: persistent waves over the round's march and shadow lists.
-// A lane holds one entry: a closest-hit march (then, on a hit, calcNormal's
-// four probes) or a shadow march.  Each loop trip every busy lane evaluates
-// map() once; a lane that is done writes its answer and is refilled from the
-// wave's queue before the next trip.  The queue walks kRegionGroup regions
-// per device-counter grab; each region's march entries, then its shadow
-// entries.
-template <class Scene, class Cfg>
-DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
-  using G = Geometry<Scene>;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  const uint32_t R = (uint32_t)P.wf_R, NR = (uint32_t)P.wf_nregions, RL = R * (uint32_t)P.wf_L;
-  const int cap = cfg.marching_steps();
-  const float fud = cfg.fudge();
-  // the wave's queue (wave-uniform): region reg of [reg, reg_end), entry q of its nall
-  // The queue walks the round's plan (wf_plan_body: the regions with any
-  // entry, in order), split into kParts ranges with a counter each (64 B
-  // apart): a wave grabs kRegionGroup plan entries from the range of its XCD
-  // (the dispatcher deals workgroups round-robin over the 8 XCDs), then from
-  // the others once its own is taken.  A device-scope atomic on one address
-  // serialises at ~0.1 us: one counter over every region made the late rounds
-  // (a few paths left in a few regions) cost ~0.5-1 ms each in grabs alone.
-  constexpr uint32_t kParts = 8;
-  const WfPlan pl = wf_plan_prefix(P);  // (one barrier, before any wave leaves)
-  const uint32_t NP = pl.np, TJ = pl.tj, PB = (uint32_t)P.wf_plan_blocks, PS = (uint32_t)P.wf_plan_span;
-  // regions per grab: enough for ~RT0_WF_UNIT entries at this round's mean
-  // entries per region (1 in the first rounds, tens once most paths ended)
-  const uint32_t kRegionGroup = max(1u, (uint32_t)(((uint64_t)RT0_WF_UNIT * NP + TJ - 1) / max(TJ, 1u)));
+// A march / walk wave's queue over the round's plan (wf_plan_body: the
+// regions with any entry, in order), split into kParts ranges with a counter
+// each (64 B apart): a wave grabs G plan entries from the range of its XCD
+// (the dispatcher deals workgroups round-robin over the 8 XCDs), then from
+// the others once its own is taken; G covers ~RT0_WF_UNIT entries at the
+// round's mean entries per region (1 region in the first rounds, tens once
+// most paths ended).  A device-scope atomic on one address serialises at
+// ~0.1 us: one counter over every region made the late rounds (a few paths
+// left in a few regions) cost ~0.5-1 ms each in grabs alone.  Wave-uniform.
+struct WfQueue {
+  static constexpr uint32_t kParts = 8;
+  const LaunchParams &P;
+  WfPlan pl;
+  uint32_t lane, NR, NP, PB, PS, G;
+  uint32_t reg, pos, pos_end, q, nc, nall, part, tried;
+  DEV WfQueue(const LaunchParams &p, const WfPlan &plan)
+      : P(p), pl(plan), lane(threadIdx.x & 63u), NR((uint32_t)p.wf_nregions), NP(plan.np),
+        PB((uint32_t)p.wf_plan_blocks), PS((uint32_t)p.wf_plan_span),
+        G(max(1u, (uint32_t)(((uint64_t)RT0_WF_UNIT * plan.np + plan.tj - 1) / max(plan.tj, 1u)))), reg(NR), pos(0),
+        pos_end(0), q(0), nc(0), nall(0), part(blockIdx.x % kParts), tried(0) {}
   // a wave beyond this round's number of grabs leaves at once: in the late
   // rounds (a few hundred grabs) the whole grid probing every range cost
   // ~0.5 ms per round in serialised read-modify-writes
-  if (blockIdx.x * 4u + (threadIdx.x >> 6) >= (NP + kRegionGroup - 1) / kRegionGroup) return;
-  uint32_t reg = NR, pos = 0, pos_end = 0, q = 0, nc = 0, nall = 0;
-  uint32_t part = blockIdx.x % kParts, tried = 0;
-  auto part_lo = [&](uint32_t k) { return (uint32_t)(((uint64_t)NP * k) / kParts); };
-  auto grab = [&]() {
+  DEV bool surplus() const { return blockIdx.x * 4u + (threadIdx.x >> 6) >= (NP + G - 1) / G; }
+  DEV uint32_t part_lo(uint32_t k) const { return (uint32_t)(((uint64_t)NP * k) / kParts); }
+  DEV void grab() {
     while (tried < kParts) {
       const uint32_t lo = part_lo(part), hi = part_lo(part + 1);
       uint32_t g = 0;
@@ -3456,21 +3627,21 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
         uint32_t *ctr = P.wf_ctr + 16 * part;
         // (a plain look first: a taken range costs no read-modify-write)
         g = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lo + g * kRegionGroup < hi) g = atomicAdd(ctr, 1u);
+        if (lo + g * G < hi) g = atomicAdd(ctr, 1u);
       }
       g = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)g, 0));
-      const uint32_t p0 = lo + g * kRegionGroup;
+      const uint32_t p0 = lo + g * G;
       if (p0 < hi) {
         pos = p0;
-        pos_end = min(p0 + kRegionGroup, hi);
+        pos_end = min(p0 + G, hi);
         return;
       }
       part = (part + 1) % kParts;
       ++tried;
     }
     pos = pos_end = NP;  // the whole plan is taken
-  };
-  auto open = [&]() {
+  }
+  DEV void open() {
     q = 0;
     nc = nall = 0;
     reg = NR;
@@ -3486,9 +3657,53 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       nc = e.y;
       nall = e.z;
     }
-  };
-  grab();
-  open();
+  }
+  DEV void start() {
+    grab();
+    open();
+  }
+  DEV void next_region() {
+    if (++pos >= pos_end) grab();
+    open();
+  }
+  DEV bool dry() const { return reg >= NR; }
+  // hand up to popcount(fr) entries of the queue to the lanes of fr (ballot
+  // + prefix count; across regions): take(j) runs on each lane that gets
+  // entry j of region reg, and may leave the lane free again (an entry with
+  // nothing to do), which then takes the next one
+  template <class Busy, class Take>
+  DEV void refill(uint64_t fr, Busy busy, Take take) {
+    const uint64_t lt = (1ull << lane) - 1ull;
+    while (fr != 0ull && !dry()) {
+      if (q >= nall) {
+        next_region();
+        continue;
+      }
+      const uint32_t n = min((uint32_t)__popcll(fr), nall - q);
+      const uint32_t rank = (uint32_t)__popcll(fr & lt);
+      if (!busy() && rank < n) take(q + rank);
+      q += n;
+      fr = __ballot(!busy());
+    }
+  }
+};
+
+// The march kernel: persistent waves over the round's march and shadow lists.
+// A lane holds one entry: a closest-hit march (then, on a hit, calcNormal's
+// four probes) or a shadow march.  Each loop trip every busy lane evaluates
+// map() once; a lane that is done writes its answer and is refilled from the
+// wave's queue (WfQueue) before the next trip, once RT0_WF_REFILL lanes are
+// free.
+template <class Scene, class Cfg>
+DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  using G = Geometry<Scene>;
+  const uint32_t R = (uint32_t)P.wf_R, RL = R * (uint32_t)P.wf_L;
+  const int cap = cfg.marching_steps();
+  const float fud = cfg.fudge();
+  const WfPlan pl = wf_plan_prefix(P);  // (one barrier, before any wave leaves)
+  WfQueue Q(P, pl);
+  if (Q.surplus()) return;
+  Q.start();
   bool busy = false, shadow = false, dirl = false;
   v3 o = mk(0.f, 0.f, 0.f), d = o, c = o, na = o;
   float tmin = 0.f, t = 0.f, id = 0.f;
@@ -3510,96 +3725,41 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     }
     busy = false;
   };
-  // a job of the queue: entry j of region reg (march entries, then shadow entries)
-  auto load_job = [&](uint32_t j, float4 &a, float4 &b, float4 &e, uint32_t &ix, bool &sh) {
-    if (j < nc) {
-      const size_t k = (size_t)reg * R + j;
+  // entry j of region Q.reg: its march entries, then its shadow entries
+  auto take = [&](uint32_t j) {
+    float4 a, b, e = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < Q.nc) {
+      const size_t k = (size_t)Q.reg * R + j;
       a = P.wf_out[2 * k];
       b = P.wf_out[2 * k + 1];
-      ix = (uint32_t)k;
-      sh = false;
+      idx = (uint32_t)k;
+      shadow = false;
     } else {
-      const size_t k = 3 * ((size_t)reg * RL + (j - nc));
+      const size_t k = 3 * ((size_t)Q.reg * RL + (j - Q.nc));
       a = P.wf_sh[k];
       b = P.wf_sh[k + 1];
       e = P.wf_sh[k + 2];
-      ix = __float_as_uint(b.w);
-      sh = true;
+      idx = __float_as_uint(b.w);
+      shadow = true;
     }
-  };
-  auto start_job = [&](const float4 &a, const float4 &b, const float4 &e, uint32_t ix, bool sh) {
     o = mk(a.x, a.y, a.z);
     tmin = a.w;
     d = mk(b.x, b.y, b.z);
-    idx = ix;
-    shadow = sh;
     c = mk(e.x, e.y, e.z);
-    dirl = sh && e.w != 0.0f;
-    busy = sh || tmin >= 0.0f;  // (a march entry without a march: only its light sampling goes on)
+    dirl = shadow && e.w != 0.0f;
+    busy = shadow || tmin >= 0.0f;  // (a march entry without a march: only its light sampling goes on)
     t = EPSILON * 4.0f;
     id = 0.0f;
     i = 0;
     ph = 4;
     if (busy && cap <= 0) stopped();  // (MARCHING_STEPS 0: no step at all)
   };
-#if RT0_WF_PREFETCH
-  // Each lane holds its NEXT job in registers, loaded when it took the one
-  // before: a refill starts the prefetched jobs at once and issues the loads
-  // of their successors, which are not read before the following refill.
-  bool nf = false, nsh = false;
-  float4 n0 = make_float4(0.f, 0.f, 0.f, 0.f), n1 = n0, n2 = n0;
-  uint32_t nix = 0;
   while (true) {
-    uint64_t fr = __ballot(!busy);
-    if (__popcll(fr) >= RT0_WF_REFILL || __ballot(busy) == 0ull) {
-      if (!busy && nf) {
-        start_job(n0, n1, n2, nix, nsh);
-        nf = false;
-      }
-      uint64_t fq = __ballot(!nf);
-      while (fq != 0ull && reg < NR) {
-        if (q >= nall) {
-          if (++pos >= pos_end) grab();
-          open();
-          continue;
-        }
-        const uint32_t take = min((uint32_t)__popcll(fq), nall - q);
-        const uint32_t rank = (uint32_t)__popcll(fq & lt);
-        if (!nf && rank < take) {
-          load_job(q + rank, n0, n1, n2, nix, nsh);
-          nf = true;
-        }
-        q += take;
-        fq = __ballot(!nf);
-      }
-    }
-    if (__ballot(busy || nf) == 0ull) break;  // the queue is dry and every lane answered
-#else
-  while (true) {
-    uint64_t fr = __ballot(!busy);
+    const uint64_t fr = __ballot(!busy);
     // refill once RT0_WF_REFILL lanes are free (or all are): each refill's
-    // job loads are a round trip the wave waits for
-    if (__popcll(fr) < RT0_WF_REFILL && __ballot(busy) != 0ull) fr = 0ull;
-    while (fr != 0ull && reg < NR) {
-      if (q >= nall) {
-        if (++pos >= pos_end) grab();
-        open();
-        continue;
-      }
-      const uint32_t take = min((uint32_t)__popcll(fr), nall - q);
-      const uint32_t rank = (uint32_t)__popcll(fr & lt);
-      if (!busy && rank < take) {
-        float4 a, b, e = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t ix;
-        bool sh;
-        load_job(q + rank, a, b, e, ix, sh);
-        start_job(a, b, e, ix, sh);
-      }
-      q += take;
-      fr = __ballot(!busy);
-    }
+    // loads are a round trip the wave waits for
+    if (__popcll(fr) >= RT0_WF_REFILL || __ballot(busy) == 0ull) Q.refill(fr, [&]() { return busy; }, take);
     if (__ballot(busy) == 0ull) break;  // the queue is dry and every lane answered
-#endif
     if (busy) {
       const v3 hp = ray_at(o, d, t);
       // calcNormal's probe ph: pos + (s.x, s.y, s.z) * EPSILON, times the same signs
@@ -3631,5 +3791,101 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     }
   }
 }
+
+// The closest-hit walk kernel of wavefront ReSTIR passes over triangle models
+// (rt0_jit_wf_walk): each march-list entry is a camera or bounce ray whose
+// quadric part the shade kernel has done (the bound is the closest quadric's
+// t); a lane walks it through the BVH as bvh_closest does -- nearer child
+// first, the far one on the lane's LDS stack, leaves tested in place left
+// before right, strict t < tmin -- one node per loop trip, and on answering
+// (t, triangle) takes the queue's next entry, so the lanes keep walking
+// whatever the rays' lengths.
+#if RT0_BVH_STACK16 || defined(RT0_BVH_STACK)
+DEV void wf_walk_body(const LaunchParams &P) {
+  const uint32_t R = (uint32_t)P.wf_R;
+  const WfPlan pl = wf_plan_prefix(P);  // (one barrier, before any wave leaves)
+  WfQueue Q(P, pl);
+  if (Q.surplus()) return;
+  Q.start();
+  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
+  const TriDev *__restrict__ tris = P.tris;
+  BvhStack stk;
+  bool busy = false;
+  v3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
+  float tmin = 0.f;
+  int node = 0, sp = 0, guard = 0, best = -1;
+  uint32_t idx = 0;
+  auto take = [&](uint32_t j) {
+    const size_t k = (size_t)Q.reg * R + j;
+    const float4 a = P.wf_out[2 * k], b = P.wf_out[2 * k + 1];
+    o = mk(a.x, a.y, a.z);
+    tmin = a.w;
+    d = mk(b.x, b.y, b.z);
+    inv = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+    idx = (uint32_t)k;
+    busy = tmin >= 0.0f;  // (an entry without a walk: only its light sampling goes on)
+    node = 0;
+    sp = 0;
+    guard = 0;
+    best = -1;
+  };
+  while (true) {
+    const uint64_t fr = __ballot(!busy);
+    // (a walk trip is one node: refills wait for RT0_WF_WALK_REFILL free lanes)
+    if (__popcll(fr) >= RT0_WF_WALK_REFILL || __ballot(busy) == 0ull) Q.refill(fr, [&]() { return busy; }, take);
+    if (__ballot(busy) == 0ull) break;  // the queue is dry and every lane answered
+    if (busy) {
+      bool done = false;
+      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
+      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+      float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
+      float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
+      const int cl = lk.x, cr = lk.y;
+      int l0 = -1, l1 = -1;
+      if (tl != F_INF && cl < 0) {
+        l0 = ~cl;
+        tl = F_INF;
+      }
+      if (tr != F_INF && cr < 0) {
+        if (l0 < 0) l0 = ~cr;
+        else l1 = ~cr;
+        tr = F_INF;
+      }
+      if (l0 >= 0) {
+        float t;
+        if (tri_test(tris[l0], o, d, tmin, t)) {
+          tmin = t;
+          best = l0;
+        }
+        if (l1 >= 0 && tri_test(tris[l1], o, d, tmin, t)) {
+          tmin = t;
+          best = l1;
+        }
+      }
+      if (tl != F_INF && tr != F_INF) {
+        const bool lfirst = tl <= tr;
+        stk.put(sp, lfirst ? cr : cl);
+        sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
+        node = lfirst ? cl : cr;
+      } else if (tl != F_INF) {
+        node = cl;
+      } else if (tr != F_INF) {
+        node = cr;
+      } else if (sp == 0) {
+        done = true;
+      } else {
+        node = stk.get(--sp);
+      }
+      // a ray visits each node at most once: the cap only guarantees that
+      // every wave drains even on a corrupt tree
+      if (++guard > 2 * P.n_tris + 8) done = true;
+      if (done) {
+        P.wf_res[idx] = make_float4(tmin, __int_as_float(best), 0.f, 0.f);
+        busy = false;
+      }
+    }
+  }
+}
+#endif
 
 }  // namespace rt0

@@ -167,26 +167,34 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   const char *wn_env = getenv("RT0_JIT_NEE_WAVES_PER_EU");
   if (w_env)
     o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w_env) << "))) ";
+  else if (k.wf && k.restir)  // (the wavefront ReSTIR shade kernel walks no BVH: left to the compiler)
+    ;
   else if (s.n_models > 0)  // with 16-bit stack entries the LDS allows 8: C5 9.14 vs 9.38 ms per pass at 6
     o << "__attribute__((amdgpu_waves_per_eu(" << (k.stack16 && k.bvh_stack > 0 ? 8 : 6) << "))) ";
   else if (k.restir && !k.defer)
     o << "__attribute__((amdgpu_waves_per_eu(4))) ";
   if (k.wf) {
-    // wavefront SDF rounds (rt0_integrator.h wf_shade_body): no pass kernel
+    // wavefront rounds, no pass kernel: SDF scenes (rt0_integrator.h
+    // wf_shade_body + wf_march_body) or ReSTIR scenes with triangle models
+    // (wf_restir_shade_body + wf_walk_body, then the deferred-pass kernels below)
     o << "void rt0_jit_wf_shade(const LaunchParams P) {\n"
-         "  rt0::wf_shade_body<rt0::JitScene, rt0::JitCfg, "
+      << (k.restir ? "  rt0::wf_restir_shade_body<rt0::JitScene, rt0::JitCfg, " : "  rt0::wf_shade_body<rt0::JitScene, rt0::JitCfg, ")
       << vol << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
     o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_wf_plan(const LaunchParams P) { "
          "rt0::wf_plan_body(P); }\n";
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
     if (const char *e = getenv("RT0_JIT_MARCH_WAVES_PER_EU")) o << "__attribute__((amdgpu_waves_per_eu(" << atoi(e) << "))) ";
-    o << "void rt0_jit_wf_march(const LaunchParams P) {\n"
-         "  rt0::wf_march_body<rt0::JitScene, rt0::JitCfg>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
-    return o.str();
+    if (k.restir)
+      o << "void rt0_jit_wf_walk(const LaunchParams P) { rt0::wf_walk_body(P); }\n";
+    else
+      o << "void rt0_jit_wf_march(const LaunchParams P) {\n"
+           "  rt0::wf_march_body<rt0::JitScene, rt0::JitCfg>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    if (!k.restir) return o.str();
+  } else {
+    o << "void rt0_jit_pass(const LaunchParams P) {\n"
+         "  rt0::pass_body<rt0::JitScene, rt0::JitCfg, "
+      << rt << ", " << vol << ", " << sdf << ", " << spc << ", false>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
   }
-  o << "void rt0_jit_pass(const LaunchParams P) {\n"
-       "  rt0::pass_body<rt0::JitScene, rt0::JitCfg, "
-    << rt << ", " << vol << ", " << sdf << ", " << spc << ", false>(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
   if (k.defer) {
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
     if (wn_env)
@@ -347,8 +355,9 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
   if (ok && k.wf) {
     hipFunction_t s = nullptr, m = nullptr, pl = nullptr;
     int per_cu = 0, cus = 0;
+    // (the round's traversal kernel: the SDF march, or the ReSTIR scenes' closest-hit walk)
     ok = hipModuleGetFunction(&s, e.mod, "rt0_jit_wf_shade") == hipSuccess &&
-         hipModuleGetFunction(&m, e.mod, "rt0_jit_wf_march") == hipSuccess &&
+         hipModuleGetFunction(&m, e.mod, k.restir ? "rt0_jit_wf_walk" : "rt0_jit_wf_march") == hipSuccess &&
          hipModuleGetFunction(&pl, e.mod, "rt0_jit_wf_plan") == hipSuccess &&
          hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m, 256, 0) == hipSuccess &&
          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess;
@@ -501,10 +510,15 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     // RT0_JIT_STACK=<entries> select what rt0_render would for such a tree)
     // the wavefront rounds rt0_render uses for such a scene (rt0_host.cpp wf_eligible)
     const char *wfe = getenv("RT0_WAVEFRONT");
-    bool wf = (!wfe || atoi(wfe) != 0) && !key.restir && ns > 0 && nm == 0 && s.n_lights <= 32 && key.max_bounces >= 1 &&
-              key.max_bounces <= 127;
-    for (int i = ne; i < ne + ns; i++) wf = wf && s.mat[i].type != 0;
-    for (int i = 0; i < s.n_lights; i++) wf = wf && s.light_index[i] < ne;
+    const int wf_mode = wfe ? atoi(wfe) : 1;
+    bool wf = wf_mode > 0 && key.max_bounces >= 1 && key.max_bounces <= 127;
+    if (key.restir) {
+      wf = wf && wf_mode >= 2 && key.walk && cfg->render_mode == 0;
+    } else {
+      wf = wf && ns > 0 && nm == 0 && s.n_lights <= 32;
+      for (int i = ne; i < ne + ns; i++) wf = wf && s.mat[i].type != 0;
+      for (int i = 0; i < s.n_lights; i++) wf = wf && s.light_index[i] < ne;
+    }
     key.wf = wf ? 1 : 0;
     const char *w16 = getenv("RT0_BVH_STACK16"), *st = getenv("RT0_JIT_STACK");
     key.stack16 = w16 && atoi(w16) != 0 ? 1 : 0;

@@ -23,7 +23,7 @@ struct JitKey {
   int nee_regions = 2;  // RT0_NEE_REGIONS: pass-wave record regions per light-sampling wave
   int walk = 0;         // RT0_NEE_WALK: the light-sampling calls' triangle occlusion queries in rt0_jit_walk
   int stack16 = 0;      // RT0_BVH_STACK16: every BVH node index fits 16 + 64 / RT0_BVH_STACK bits
-  int wf = 0;           // RT0_WAVEFRONT: SDF passes as wavefront rounds (rt0_jit_wf_shade + rt0_jit_wf_march)
+  int wf = 0;           // RT0_WAVEFRONT: passes as wavefront rounds (rt0_jit_wf_shade + rt0_jit_wf_march / _walk)
 };
 
 // The kernels of one compiled module: the pass kernel and, for a deferred
@@ -31,7 +31,9 @@ struct JitKey {
 struct JitFns {
   void *pass = nullptr, *nee = nullptr, *resolve = nullptr;
   void *walk = nullptr;  // RT0_NEE_WALK keys
-  void *wf_shade = nullptr, *wf_march = nullptr, *wf_plan = nullptr;  // RT0_WAVEFRONT keys (no pass kernel then)
+  // RT0_WAVEFRONT keys (no pass kernel then); wf_march is the round's
+  // traversal kernel: the SDF march, or for ReSTIR keys the closest-hit walk
+  void *wf_shade = nullptr, *wf_march = nullptr, *wf_plan = nullptr;
   int wf_march_blocks = 0;  // workgroups of the march kernel the device holds at once
 };
 

@@ -537,9 +537,10 @@ class Renderer:
         default on."""
         self._chk(lib().rt0_set_defer_light_sampling(self.h, int(bool(on))))
 
-    def set_wavefront(self, on):
-        """Wavefront rounds for SDF scenes (rt0_set_wavefront); default on."""
-        self._chk(lib().rt0_set_wavefront(self.h, int(bool(on))))
+    def set_wavefront(self, mode):
+        """Wavefront rounds (rt0_set_wavefront): 0 off, 1 / True SDF scenes
+        (the default), 2 also ReSTIR scenes with triangle models."""
+        self._chk(lib().rt0_set_wavefront(self.h, int(mode)))
 
     def set_counting(self, on):
         self._chk(lib().rt0_set_counting(self.h, int(bool(on))))

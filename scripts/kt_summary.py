@@ -11,6 +11,9 @@ warm-up included).  A deferred ReSTIR pass is three dispatches (rt0_jit_pass,
 rt0_jit_nee, rt0_jit_resolve; rt0_integrator.h), four in scenes with models
 (+ rt0_jit_walk): their kept medians are reported per kernel and "median_ms"
 .. "max_ms" are then per pass, the kernels' durations summed pass by pass.
+Wavefront launches (rt0_jit_wf_*: shade, plan and march or walk per round)
+are summed launch by launch with what completes them: rt0_sum_kernel, or a
+ReSTIR pass's nee (+ walk) + resolve.
 """
 import csv
 import glob
@@ -20,10 +23,14 @@ import sys
 from collections import defaultdict
 
 KERNEL = "rt0_jit_pass"
-GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_march")
+GROUP = ("rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve", "rt0_jit_wf_shade", "rt0_jit_wf_plan",
+         "rt0_jit_wf_march", "rt0_jit_wf_walk")
 # a wavefront SDF launch (rt0_integrator.h wf_shade_body): MAX_BOUNCES + 2
-# shade and MAX_BOUNCES + 1 march dispatches, then one rt0_sum_kernel
-WF = ("rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_march")
+# shade and MAX_BOUNCES + 1 march dispatches, then one rt0_sum_kernel; a
+# wavefront ReSTIR pass: MAX_BOUNCES + 1 shade and MAX_BOUNCES walk
+# dispatches, then rt0_jit_nee (+ rt0_jit_walk) + rt0_jit_resolve
+WF = ("rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_march", "rt0_jit_wf_walk")
+TAIL = ("rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve")
 
 
 def main():
@@ -38,12 +45,16 @@ def main():
     per_kernel = {}
     sums = [float(r["End_Timestamp"]) - float(r["Start_Timestamp"]) for r in rows
             if r["Kernel_Name"].strip().startswith("rt0_sum_kernel")]
-    if dur["rt0_jit_wf_march"] and sums:  # wavefront launches: every dispatch of the launch + its sum, per launch
-        nl = len(sums)
-        per = {k: len(dur[k]) // nl for k in WF}
-        pas = [sum(sum(dur[k][i * per[k]:(i + 1) * per[k]]) for k in WF) + sums[i] for i in range(nl)]
+    wf = bool(dur["rt0_jit_wf_march"] or dur["rt0_jit_wf_walk"])
+    if wf and (sums or dur["rt0_jit_resolve"]):  # wavefront launches: every dispatch of the launch + its tail, per launch
+        tail = {k: dur[k] for k in TAIL if dur[k]} if dur["rt0_jit_resolve"] else {"rt0_sum_kernel": sums}
+        nl = min(len(v) for v in tail.values())
+        per = {k: len(dur[k]) // nl for k in WF if dur[k]}
+        pas = [sum(sum(dur[k][i * per[k]:(i + 1) * per[k]]) for k in per) + sum(v[i] for v in tail.values())
+               for i in range(nl)]
         per_kernel = {k: statistics.median([sum(dur[k][i * per[k]:(i + 1) * per[k]]) for i in range(skip, nl)]) / 1e6
-                      for k in WF if nl > skip}
+                      for k in per if nl > skip}
+        per_kernel.update({k: statistics.median(v[skip:nl]) / 1e6 for k, v in tail.items() if nl > skip})
         per_kernel["dispatches_per_launch"] = per
     elif dur["rt0_jit_nee"]:  # deferred passes: pass + nee (+ walk) + resolve, one of each per pass
         ks = [k for k in GROUP if dur[k]]
@@ -53,9 +64,9 @@ def main():
     kept = pas[skip:]
     other = defaultdict(list)
     for r in rows:
-        if r["Kernel_Name"].strip() not in GROUP:
+        if r["Kernel_Name"].strip() not in GROUP and not (wf and r["Kernel_Name"].startswith("rt0_sum_kernel")):
             other[r["Kernel_Name"][:80]].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
-    res = {"kernel": "+".join(k for k in WF if dur[k]) if dur["rt0_jit_wf_march"] else KERNEL, "dispatches": len(pas), "skipped": skip, "kept": len(kept),
+    res = {"kernel": "+".join(k for k in GROUP if dur[k]) if wf else KERNEL, "dispatches": len(pas), "skipped": skip, "kept": len(kept),
            "median_ms": statistics.median(kept) / 1e6 if kept else None,
            "mean_ms": statistics.mean(kept) / 1e6 if kept else None,
            "min_ms": min(kept) / 1e6 if kept else None, "max_ms": max(kept) / 1e6 if kept else None,

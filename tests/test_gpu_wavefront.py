@@ -1,6 +1,7 @@
-"""Wavefront SDF rounds (rt0_set_wavefront; rt0_integrator.h wf_shade_body /
-wf_march_body) against the pass kernel they replace, and their own exact
-properties.
+"""Wavefront rounds (rt0_set_wavefront; rt0_integrator.h wf_shade_body /
+wf_march_body for SDF scenes, wf_restir_shade_body / wf_walk_body for ReSTIR
+scenes with triangle models) against the pass kernel they replace, and their
+own exact properties.
 
 The march kernel runs every map() evaluation, bound test and calcNormal sum
 of the pass kernel's march (the same arithmetic at one program point); the
@@ -148,3 +149,68 @@ def test_wavefront_matches_reference_fixture(name, cfgs, gpu_required):
     ok, _ = pixel_match(np.stack(got), gold)
     bad = 1.0 - ok[valid].mean()
     assert bad <= BAD_FRAC.get(name, BAD_FRAC["default"]), (name, bad)
+
+
+def restir_chain(cfgs, wf, n=6, size=64, viewport=None, shard=None):
+    import test_models as T
+    cfg = T.cfg_by_name(cfgs, "c5_spectral_models")
+    r = T.make(cfg, cfgs, size, size)
+    r.set_wavefront(2 if wf else 0)  # (mode 2: ReSTIR scenes with models too)
+    if viewport:
+        r.set_viewport(*viewport)
+    if shard:
+        r.set_shard(*shard)
+        r.set_halo(4)
+    S, M, A = [], [], []
+    for k in range(1, n + 1):
+        r.render(k, 1)
+        S.append(r.read_accum())
+        m, a = r.read_restir(0)
+        M.append(m)
+        A.append(a)
+    return np.stack(S), np.stack(M), np.stack(A), r.last_render_path()
+
+
+def test_wavefront_restir_models_match_pass_kernel(cfgs, gpu_required):
+    """ReSTIR with triangle models (BASELINE config 5 at 64x64): the pass's
+    paths as shade rounds + closest-hit walk rounds against the deferred pass
+    kernel, over a 6-pass chain (each pass reads the reservoirs the previous
+    ones wrote).  Every walk is bvh_closest's and the quadric tests are
+    recomputed on resume: the same hits, the same deferred calls; only the
+    compiler's FMA contraction can differ between the two kernels -- held to
+    test_gpu_defer's bar (1e-5 / 1e-4 relative, >= 98% bit-identical)."""
+    from test_gpu_defer import close_and_mostly_identical
+    s1, m1, a1, p1 = restir_chain(cfgs, True)
+    s0, m0, a0, p0 = restir_chain(cfgs, False)
+    assert p1 == "wavefront" and p0 == "deferred", (p1, p0)
+    assert np.isfinite(s1).all()
+    print("bit-identical samples %.4f reservoirs %.4f" % ((s0[..., :3] == s1[..., :3]).all(-1).mean(),
+                                                          (m0 == m1).all(-1).mean()))
+    close_and_mostly_identical(m0, m1, "reservoir main")
+    close_and_mostly_identical(a0, a1, "reservoir aux")
+    close_and_mostly_identical(s0[..., :3], s1[..., :3], "samples")
+    assert s1[..., :3].mean() > 0.0
+
+
+def test_wavefront_restir_models_viewport_and_shards(cfgs, gpu_required):
+    """A tile and a contiguous row-block shard of the model scene through the
+    wavefront rounds: only their pixels are drawn, and they match the
+    deferred pass kernel's render of the same tile / shard (slots map to
+    pass waves whatever the launch covers)."""
+    from test_gpu_defer import close_and_mostly_identical
+    vp = (8, 16, 40, 24)
+    s1, m1, _, p1 = restir_chain(cfgs, True, n=3, viewport=vp)
+    s0, m0, _, _ = restir_chain(cfgs, False, n=3, viewport=vp)
+    assert p1 == "wavefront"
+    inside = np.zeros(s1.shape[1:3], bool)
+    inside[vp[1]:vp[1] + vp[3], vp[0]:vp[0] + vp[2]] = True
+    assert not s1[:, ~inside, :3].any()
+    close_and_mostly_identical(m0, m1, "reservoir main")
+    close_and_mostly_identical(s0[..., :3], s1[..., :3], "samples")
+    # one pass per call of a sharded ReSTIR render: shard 1 of 2 (rows 32..63)
+    s1, m1, _, p1 = restir_chain(cfgs, True, n=1, shard=(1, 2, 32))
+    s0, m0, _, _ = restir_chain(cfgs, False, n=1, shard=(1, 2, 32))
+    assert p1 == "wavefront"
+    assert not s1[0][:32, :, :3].any() and s1[0][32:, :, :3].any()
+    close_and_mostly_identical(m0, m1, "reservoir main")
+    close_and_mostly_identical(s0[..., :3], s1[..., :3], "samples")

@@ -188,12 +188,25 @@ def test_jit_walk_module_for_model_scenes(cfgs, tmp_path, monkeypatch):
     monkeypatch.setenv("RT0_JIT_STACK", "24")
     for i in range(64):  # grow the environment so its array is reallocated
         monkeypatch.setenv("RT0_TEST_PAD_%d" % i, "x" * 64)
-    rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))
-    co = sorted(glob.glob(str(tmp_path / "k_*.co")))[-1]
-    notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True,
-                           text=True).stdout
-    lds = {m.group(2): int(m.group(1)) for m in
-           re.finditer(r"\.group_segment_fixed_size:\s+(\d+)(?:.|\n)*?\.name:\s+(\S+)", notes)}
+
+    def compile_lds():
+        rt0.jit_compile(scene, sdf, rt0.parse_config(*rt0.config_strings(cfg)))
+        co = max(glob.glob(str(tmp_path / "k_*.co")), key=os.path.getmtime)
+        notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True,
+                               text=True).stdout
+        return co, {m.group(2): int(m.group(1)) for m in
+                    re.finditer(r"\.group_segment_fixed_size:\s+(\d+)(?:.|\n)*?\.name:\s+(\S+)", notes)}
+
+    # rt0_set_wavefront(2): wavefront rounds (rt0_jit_wf_shade, _wf_plan, the
+    # closest-hit walk rt0_jit_wf_walk), then the deferred-pass kernels
+    monkeypatch.setenv("RT0_WAVEFRONT", "2")
+    co, lds = compile_lds()
+    assert {"rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_walk", "rt0_jit_nee", "rt0_jit_walk",
+            "rt0_jit_resolve"} <= set(lds) and "rt0_jit_pass" not in lds, lds
+    assert 256 * 24 * 2 <= lds["rt0_jit_wf_walk"] <= 256 * 24 * 2 + 2048  # the stack + the plan prefix
+    # the default (mode 1: SDF scenes only): the pass kernel
+    monkeypatch.setenv("RT0_WAVEFRONT", "1")
+    co, lds = compile_lds()
     assert {"rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve"} <= set(lds), lds
     assert lds["rt0_jit_walk"] == 256 * 24 * 2 + 16  # the stack + the wave counters
     # the pass and light-sampling kernels also hold LDS copies of the scene
