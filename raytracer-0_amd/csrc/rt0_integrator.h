@@ -110,6 +110,12 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_NEE_WALK  // light-sampling calls' triangle occlusion queries in rt0_jit_walk (models scenes)
 #define RT0_NEE_WALK 0
 #endif
+#ifndef RT0_WALK_ROOT_TEST  // light-sampling kernel drops walk jobs that miss the root's child boxes
+#define RT0_WALK_ROOT_TEST 1
+#endif
+#ifndef RT0_WALK_SPEC  // rt0_jit_walk postpones leaf tests until half the busy lanes hold one
+#define RT0_WALK_SPEC 1
+#endif
 #ifndef RT0_BVH_STACK16  // BVH traversal stacks as 16-bit LDS entries + high bits in a register
 #define RT0_BVH_STACK16 0
 #endif
@@ -384,6 +390,15 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
   const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
   const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
   return (tn <= tf && tn < tmin) ? tn : F_INF;
+}
+// whether a ray (1/d = inv) enters neither child box of the BVH's root
+// before tmax: then every walk of it ends at its first node with no triangle
+// test (bvh_closest, walk_body), so it needs none
+DEV bool bvh_root_miss(const LaunchParams &P, v3 o, v3 inv, float tmax) {
+  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
+  const float4 a = nodes[0], b = nodes[1], c = nodes[2];
+  return box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmax) == F_INF &&
+         box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmax) == F_INF;
 }
 // The per-lane traversal stacks: ONE LDS array for every traversal of the
 // kernel (closest-hit and occlusion instances alike -- a __shared__ array
@@ -2988,8 +3003,17 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       } else {
         // the result as it is if both rays pass, tagged for rt0_jit_resolve; the
         // pixel's last call writes the reservoir MRTs with W as if visible
-        // (resolve zeroes W when the visibility ray is blocked)
-        const int tag = (int)(((uint32_t)slot + 1u) << 2) | (sp.has[0] ? 1 : 0) | (sp.has[1] ? 2 : 0);
+        // (resolve zeroes W when the visibility ray is blocked).  A ray that
+        // misses the model's root boxes is answered here (not occluded).
+        bool w0 = sp.has[0], w1 = sp.has[1];
+        if constexpr (RT0_WALK_ROOT_TEST) {
+          auto miss = [&](const WalkJob &j) {
+            return bvh_root_miss(P, mk(j.ox, j.oy, j.oz), mk(frcp(j.dx), frcp(j.dy), frcp(j.dz)), j.tmax);
+          };
+          w0 = w0 && !miss(sp.j[0]);
+          w1 = w1 && !miss(sp.j[1]);
+        }
+        const int tag = (w0 || w1) ? (int)(((uint32_t)slot + 1u) << 2) | (w0 ? 1 : 0) | (w1 ? 2 : 0) : 0;
         P.nee_out[(size_t)r.k() * plane + r.pix] =
             make_float4(sp.f.x * r.mr, sp.f.y * r.mg, sp.f.z * r.mb, __int_as_float(tag));
         if (r.k() == P.nee_n[r.pix] - 1 && P.rout_main != nullptr && P.rout_aux != nullptr) {
@@ -2997,8 +3021,8 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
           P.rout_main[r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, sp.W);
           P.rout_aux[r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
         }
-        has0 = sp.has[0];
-        has1 = sp.has[1];
+        has0 = w0;
+        has1 = w1;
         j0 = sp.j[0];
         j1 = sp.j[1];
         j0.slot2 = 2u * (uint32_t)slot;
@@ -3031,7 +3055,103 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 // lane whose ray is answered takes the wave's next job (an LDS counter), so
 // the wave walks on full lanes until its list runs dry instead of waiting for
 // its longest ray every 64 jobs.  One node (two child boxes) per iteration.
+// RT0_WALK_SPEC: walk_body with the leaf tests postponed (speculative
+// while-while traversal, Aila & Laine 2009): a lane whose node visit finds
+// leaf triangles keeps them pending and the wave tests pending leaves only
+// once half its busy lanes hold some (or every busy lane does), so the
+// triangle tests run on many lanes at once instead of splitting every
+// iteration into node lanes and leaf lanes.  An occlusion answer is a set
+// property (some triangle in (EPSILON, tmax)): the visiting order does not
+// change it.
+DEV void walk_body_spec(const LaunchParams &P) {
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
+  if (w >= (uint32_t)P.walk_waves) return;
+  const uint32_t n = P.walk_count[w];
+  const WalkJob *__restrict__ jobs = P.walk_jobs + (size_t)w * (2u * RT0_NEE_REGIONS * (uint32_t)P.nee_cap);
+  uint32_t *ctr = nee_wave_counter();
+  *(volatile uint32_t *)ctr = 64u;  // every lane stores the same value: jobs 0..63 go by lane index
+  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
+  const TriDev *__restrict__ tris = P.tris;
+  BvhStack stk;
+  uint32_t j = threadIdx.x & 63u;
+  bool have = false;
+  v3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
+  float tmax = 0.f;
+  uint32_t slot2 = 0;
+  int node = 0, sp = 0, guard = 0, pa = -1, pb = -1;  // node -1: traversal over; pa/pb: pending leaves
+  auto load = [&]() {
+    have = j < n;
+    if (have) {
+      const WalkJob jb = jobs[j];
+      o = mk(jb.ox, jb.oy, jb.oz);
+      d = mk(jb.dx, jb.dy, jb.dz);
+      inv = mk(frcp(d.x), frcp(d.y), frcp(d.z));
+      tmax = jb.tmax;
+      slot2 = jb.slot2;
+      node = 0;
+      sp = 0;
+      guard = 0;  // (stale stack entries are never read: sp restarts at 0)
+      pa = pb = -1;
+    }
+  };
+  load();
+  while (__ballot(have) != 0ull) {
+    // node phase: lanes without pending leaves visit their next node
+    if (have && pa < 0 && node >= 0) {
+      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
+      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+      float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmax);
+      float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmax);
+      const int cl = lk.x, cr = lk.y;
+      if (tl != F_INF && cl < 0) {
+        pa = ~cl;
+        tl = F_INF;
+      }
+      if (tr != F_INF && cr < 0) {
+        if (pa < 0) pa = ~cr;
+        else pb = ~cr;
+        tr = F_INF;
+      }
+      if (tl != F_INF && tr != F_INF) {
+        const bool lfirst = tl <= tr;
+        stk.put(sp, lfirst ? cr : cl);
+        sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
+        node = lfirst ? cl : cr;
+      } else if (tl != F_INF) {
+        node = cl;
+      } else if (tr != F_INF) {
+        node = cr;
+      } else if (sp == 0) {
+        node = -1;
+      } else {
+        node = stk.get(--sp);
+      }
+      // a ray visits each node at most once: the cap only guarantees that
+      // every wave drains even on a corrupt tree
+      if (++guard > 2 * P.n_tris + 8) node = -1;
+    }
+    // leaf phase: once half the busy lanes hold leaves, or no busy lane can
+    // visit a node without testing its leaves first
+    const uint64_t busy = __ballot(have), lf = __ballot(have && pa >= 0),
+                   stuck = __ballot(have && (pa >= 0 || node < 0));
+    bool occ = false;
+    if ((2 * __popcll(lf) >= __popcll(busy) || stuck == busy) && have && pa >= 0) {
+      float t;
+      occ = tri_test(tris[pa], o, d, tmax, t) || (pb >= 0 && tri_test(tris[pb], o, d, tmax, t));
+      pa = pb = -1;
+    }
+    if (have && (occ || (pa < 0 && node < 0))) {
+      P.walk_res[slot2] = occ ? 1u : 0u;
+      j = atomicAdd(ctr, 1u);
+      load();
+    }
+  }
+}
+
 DEV void walk_body(const LaunchParams &P) {
+#if RT0_WALK_SPEC
+  walk_body_spec(P);
+#else
   const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
   if (w >= (uint32_t)P.walk_waves) return;
   const uint32_t n = P.walk_count[w];
@@ -3114,6 +3234,7 @@ DEV void walk_body(const LaunchParams &P) {
       }
     }
   }
+#endif
 }
 
 #endif
