@@ -297,7 +297,11 @@ int rt0_set_jit(rt0_ctx *ctx, int enable);
  * (1757) -- a GLES execution artefact, pinned by oracle/gen/mask_kat.py.
  * 1 = reproduce it (the reservoir chain then matches the reference executor
  * pass after pass); 0 (default) = GLSL semantics.  Radiance of a pass is the
- * same either way; only the reservoirs the next passes read differ. */
+ * same either way; only the reservoirs the next passes read differ.
+ * 1 also fetches the RGBA8 asset textures (u_tex0..3, u_rnd_tex) through the
+ * executor's fixed-point bilinear filter (16-bit coordinate fraction, 16-bit
+ * tap weights; oracle/gen/tex_kat.py measures it, bit-exact on power-of-two
+ * sizes) instead of exact fp32 bilinear. */
 int rt0_set_executor_compat(rt0_ctx *ctx, int enable);
 /* Deferred ReSTIR light sampling (scene-specialised kernels): a pass runs its
  * paths with every sampleLightsReSTIR call (raytracer.glsl:1619-1801)

@@ -186,6 +186,7 @@ typedef struct {
   int ghost;
   int scatter0_exit; /* SWIFTSHADER_SCATTER0_EXIT: the executor's first-iteration `continue` (see radiance) */
   int scatter_exit;  /* SWIFTSHADER_SCATTER_EXIT: the executor retires the lane at every scatter `continue` */
+  int ss_tex;        /* SWIFTSHADER_TEX_FILTER: the executor's fixed-point RGBA8 bilinear filter (tex_fetch_ss) */
   int dbg_paths;     /* RT0_DEBUG_PATHS: non-ReSTIR reservoir outputs carry per-sample path statistics */
   /* camera uniforms (index.js:421-423) */
   v3 cam_pos, cam_look, cam_params;
@@ -421,10 +422,46 @@ static int iSDF(Frag *F, v3 o, v3 d, float tmin, float *t, v3 *n, int *index) {
 /* -------------------------------------------------------------- textures */
 /* GL texture() on an RGBA8 asset: GL_LINEAR, GL_REPEAT, level 0
  * (GlslViewport.loadTexture, index.js:703-708); unbound = (0,0,0,1). */
+/* SwiftShader 4.1's GL_LINEAR + GL_REPEAT fetch of an RGBA8 texture, as the
+ * known-answer shaders of oracle/gen/tex_kat.py measure it (tests/golden/
+ * tex_filter_kat.npz; bit-exact on power-of-two sizes, every asset of the
+ * reference is one): the coordinate becomes a 16-bit fixed-point fraction
+ * (trunc(u * 65536) & 0xFFFF -- REPEAT wraps there), the half-texel offset
+ * is taken off in that unit (floor(32768 / w)), and times w it is a 16.16
+ * texel position: texel x >> 16 and weight f = x & 0xFFFF.  Texels widen to
+ * 16 bits (v * 257); each of the four taps weighs ((wx * wy) >> 16) with
+ * wx = 65535 - f or f (likewise wy), contributes (t * w) >> 16, and the sum
+ * is read back as sum * (1 / 65535).  Against exact bilinear this loses 1-3 units
+ * of 1/65535 and quantises the sub-texel position to w / 65536 texels (64
+ * steps per texel at w = 1024). */
+static int ss_coord(float u, int w, int *i0, int *i1) {
+  float x = u * 65536.0f;
+  int q = (fabsf(x) < 2147483520.0f) ? (int)x : (int)0x80000000; /* cvttps2dq (out of range: 0x80000000) */
+  int s = ((q & 0xFFFF) - 32768 / w) * w, i = s >> 16; /* arithmetic shift: floor */
+  *i0 = ((i % w) + w) % w;
+  *i1 = (*i0 + 1) % w;
+  return s & 0xFFFF;
+}
+void tex_fetch_ss(const unsigned char *img, int w, int h, float u, float v, float out[4]) {
+  int x0, x1, y0, y1;
+  unsigned fu = (unsigned)ss_coord(u, w, &x0, &x1), fv = (unsigned)ss_coord(v, h, &y0, &y1);
+  unsigned w00 = ((65535u - fu) * (65535u - fv)) >> 16, w10 = (fu * (65535u - fv)) >> 16;
+  unsigned w01 = ((65535u - fu) * fv) >> 16, w11 = (fu * fv) >> 16;
+  for (int c = 0; c < 4; c++) {
+    unsigned t00 = img[((size_t)y0 * w + x0) * 4 + c] * 257u, t10 = img[((size_t)y0 * w + x1) * 4 + c] * 257u;
+    unsigned t01 = img[((size_t)y1 * w + x0) * 4 + c] * 257u, t11 = img[((size_t)y1 * w + x1) * 4 + c] * 257u;
+    unsigned n = ((t00 * w00) >> 16) + ((t10 * w10) >> 16) + ((t01 * w01) >> 16) + ((t11 * w11) >> 16);
+    out[c] = (float)n * (1.0f / 65535.0f); /* (the readback multiplies by the reciprocal) */
+  }
+}
 static void tex_fetch(const Oracle *o, int unit, float u, float v, float out[4]) {
   const unsigned char *img = o->tex_img[unit];
   if (!img) { out[0] = out[1] = out[2] = 0.0f; out[3] = 1.0f; return; }
   int w = o->tex_w[unit], h = o->tex_h[unit];
+  if (o->ss_tex) {
+    tex_fetch_ss(img, w, h, u, v, out);
+    return;
+  }
   float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
   float fx = floorf(x), fy = floorf(y);
   float a = x - fx, b = y - fy;
@@ -1651,6 +1688,7 @@ int or_set_constant(void *h, const char *name, double v) {
   else if (!strcmp(name, "SWIFTSHADER_GHOST")) o->ghost = iv;
   else if (!strcmp(name, "SWIFTSHADER_SCATTER0_EXIT")) o->scatter0_exit = iv;
   else if (!strcmp(name, "SWIFTSHADER_SCATTER_EXIT")) o->scatter_exit = iv;
+  else if (!strcmp(name, "SWIFTSHADER_TEX_FILTER")) o->ss_tex = iv;
   else if (!strcmp(name, "RT0_DEBUG_PATHS")) o->dbg_paths = iv;
   else if (!strcmp(name, "RENDER_MODE")) {
     o->render_mode = iv;

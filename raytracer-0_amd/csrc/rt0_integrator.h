@@ -985,10 +985,44 @@ DEV float smoothstep_(float e0, float e1, float x) {
 }
 // GL_LINEAR + GL_REPEAT fetch at level 0 of an RGBA8 asset texture
 // (GlslViewport.loadTexture, index.js:703-708); unbound unit = (0,0,0,1).
+// Executor compatibility (F_EXEC_GHOST): SwiftShader 4.1's fixed-point
+// GL_LINEAR + GL_REPEAT fetch, measured by the known-answer shaders of
+// oracle/gen/tex_kat.py (tests/golden/tex_filter_kat.npz; restated as
+// tex_fetch_ss in oracle/rt0_oracle.c): the coordinate as a 16-bit fraction
+// (trunc(u * 65536) & 0xFFFF), the half texel taken off in that unit
+// (32768 / w), times w a 16.16 texel position (texel s >> 16, weight
+// s & 0xFFFF); texels widened to v * 257, tap weights (wx * wy) >> 16, taps
+// (t * w) >> 16 summed, read back times 1 / 65535.
+DEV int ss_coord(float u, int w, int &i0, int &i1) {
+  const float x = u * 65536.0f;
+  const int q = fabsf(x) < 2147483520.0f ? (int)x : (int)0x80000000;  // (cvttps2dq: out of range -> INT_MIN)
+  const int s = ((q & 0xFFFF) - 32768 / w) * w;
+  int i = (s >> 16) % w;  // (arithmetic shift: floor)
+  i += i < 0 ? w : 0;
+  i0 = i;
+  i1 = i + 1 == w ? 0 : i + 1;
+  return s & 0xFFFF;
+}
+DEV T4 tex_rgba8_ss(const uint32_t *__restrict__ img, int w, int h, float u, float v) {
+  int x0, x1, y0, y1;
+  const uint32_t fu = (uint32_t)ss_coord(u, w, x0, x1), fv = (uint32_t)ss_coord(v, h, y0, y1);
+  const uint32_t w00 = ((65535u - fu) * (65535u - fv)) >> 16, w10 = (fu * (65535u - fv)) >> 16;
+  const uint32_t w01 = ((65535u - fu) * fv) >> 16, w11 = (fu * fv) >> 16;
+  const uint32_t q00 = img[y0 * w + x0], q10 = img[y0 * w + x1], q01 = img[y1 * w + x0], q11 = img[y1 * w + x1];
+  float r[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    auto t = [&](uint32_t q) { return ((q >> (8 * c)) & 255u) * 257u; };
+    const uint32_t n = ((t(q00) * w00) >> 16) + ((t(q10) * w10) >> 16) + ((t(q01) * w01) >> 16) + ((t(q11) * w11) >> 16);
+    r[c] = (float)n * (1.0f / 65535.0f);
+  }
+  return T4{r[0], r[1], r[2], r[3]};
+}
 DEV T4 tex_rgba8(const LaunchParams &P, int unit, float u, float v) {
   const uint32_t *__restrict__ img = P.tex_img[unit];
   if (img == nullptr) return T4{0.f, 0.f, 0.f, 1.f};
   const int w = P.tex_w[unit], h = P.tex_h[unit];
+  if (P.flags & F_EXEC_GHOST) return tex_rgba8_ss(img, w, h, u, v);
   const float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
   const float fx = floorf(x), fy = floorf(y);
   const float a = x - fx, b = y - fy;

@@ -188,6 +188,29 @@ def test_gpu_restir_chain_matches_reference(name, cfgs, gpu_required):
     assert good, (name, l2)
 
 
+@pytest.mark.parametrize("name", ["page_scene0_slabfirst", "page_scene1", "tex_check_assets", "tex_check_test"])
+def test_gpu_executor_texture_filter(name, cfgs, gpu_required):
+    """rt0_set_executor_compat also fetches the asset textures through the
+    executor's fixed-point bilinear filter (rt0_integrator.h tex_rgba8_ss,
+    pinned by tests/golden/tex_filter_kat.npz): against the reference's own
+    fixtures the product then holds the restatement's bounds
+    (test_oracle_golden.TEX_FILTER_BAD; GLSL semantics: BAD_FRAC above)."""
+    from test_oracle_golden import TEX_FILTER_BAD
+    if not have(name):
+        pytest.skip("fixture not generated")
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    gold = G["samples"]
+    frames = G["frames"] if "frames" in G else range(1, gold.shape[0] + 1)
+    r = make(cfgs, name, gold.shape[2], gold.shape[1])
+    r.set_executor_compat(True)
+    got = np.stack([single(r, int(k)) for k in frames])
+    valid = G["valid"] if "valid" in G else np.ones(gold.shape[:3], bool)
+    ok, _ = pixel_match(got[..., :3], gold[..., :3])
+    bad = 1.0 - ok[valid].mean()
+    print("%s: %.4f of pixels differ under executor compat" % (name, bad))
+    assert bad <= TEX_FILTER_BAD[name], (name, bad)
+
+
 def test_gpu_page_scene0(cfgs, gpu_required):
     """The reference page's default scene (index.html:752-790) end to end on
     its real assets.  GLSL semantics make the order of its two SDF statements
