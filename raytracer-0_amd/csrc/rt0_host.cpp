@@ -69,6 +69,8 @@ struct rt0_ctx {
   std::vector<Model> models;
   bool bvh_dirty = false;
   BvhNode *d_bvh = nullptr;
+  Bvh4Node *d_bvh4 = nullptr;  // the SAH tree collapsed to 4-wide nodes (null: LBVH build or < 2 triangles)
+  int bvh4_stack = 0;           // traversal stack entries a 4-wide walk can need
   TriDev *d_tris = nullptr;
   int n_tris = 0, bvh_depth = 0;
   SceneDev *d_scene = nullptr;
@@ -294,6 +296,7 @@ void rt0_destroy(rt0_ctx *c) {
     if (t) (void)hipFree(t);
   if (c->d_cube) (void)hipFree(c->d_cube);
   if (c->d_bvh) (void)hipFree(c->d_bvh);
+  if (c->d_bvh4) (void)hipFree(c->d_bvh4);
   if (c->d_tris) (void)hipFree(c->d_tris);
   for (auto &s : c->wf_streams)
     if (s) (void)hipStreamDestroy(s);
@@ -484,6 +487,14 @@ int rt0_set_model(rt0_ctx *c, int model, const float *positions, int n_vertices,
 // one BVH: the binned-SAH tree built on the host (rt0_bvh_sah.cpp, default) or
 // the device LBVH (rt0_bvh.hip; RT0_BVH_BUILD=lbvh).  Runs at the first render
 // after a scene/model change.
+// RT0_BVH4=1: the scene-specialised kernels walk the 4-wide tree.  Measured
+// slower on C5 (9.66 vs 8.32 ms per pass: the pass kernel 5.0 vs 3.9 ms,
+// spilling at 8 waves; profiles/r05/c5_bvh4), so the binary tree stays the
+// default.
+static bool bvh4_enabled() {
+  static const bool on = getenv("RT0_BVH4") && atoi(getenv("RT0_BVH4")) != 0;
+  return on;
+}
 static bool bvh_builder_sah() {
   static const bool sah = !(getenv("RT0_BVH_BUILD") && std::string(getenv("RT0_BVH_BUILD")) == "lbvh");
   return sah;
@@ -513,7 +524,10 @@ static int build_bvh(rt0_ctx *c) {
   }
   const int n = (int)owner.size();
   if (c->d_bvh) HIPCHK(c, hipFree(c->d_bvh));
+  if (c->d_bvh4) HIPCHK(c, hipFree(c->d_bvh4));
   if (c->d_tris) HIPCHK(c, hipFree(c->d_tris));
+  c->d_bvh4 = nullptr;
+  c->bvh4_stack = 0;
   c->d_bvh = nullptr;
   c->d_tris = nullptr;
   c->n_tris = 0;
@@ -527,6 +541,13 @@ static int build_bvh(rt0_ctx *c) {
     std::vector<TriDev> tris;
     depth = rt0h::bvh_build_sah(n, v.data(), owner.data(), nodes, tris);
     HIPCHK(c, hipMemcpy(c->d_bvh, nodes.data(), nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
+    std::vector<Bvh4Node> nodes4;
+    const int need = rt0h::bvh4_collapse(nodes, n, nodes4);
+    if (need >= 0 && need + 1 < RT0_BVH_STACK) {
+      HIPCHK(c, hipMalloc(&c->d_bvh4, nodes4.size() * sizeof(Bvh4Node)));
+      HIPCHK(c, hipMemcpy(c->d_bvh4, nodes4.data(), nodes4.size() * sizeof(Bvh4Node), hipMemcpyHostToDevice));
+      c->bvh4_stack = need + 1;
+    }
     HIPCHK(c, hipMemcpy(c->d_tris, tris.data(), tris.size() * sizeof(TriDev), hipMemcpyHostToDevice));
   } else {
     float *d_v = nullptr;
@@ -544,7 +565,8 @@ static int build_bvh(rt0_ctx *c) {
   if (depth >= RT0_BVH_STACK)
     return fail(c, RT0_E_UNSUPPORTED, "BVH depth " + std::to_string(depth) + " exceeds the traversal stack");
   if (getenv("RT0_BVH_DEBUG"))
-    fprintf(stderr, "rt0 bvh: %s build, %d triangles, depth %d\n", bvh_builder_sah() ? "sah" : "lbvh", n, depth);
+    fprintf(stderr, "rt0 bvh: %s build, %d triangles, depth %d, 4-wide stack %d\n", bvh_builder_sah() ? "sah" : "lbvh",
+            n, depth, c->bvh4_stack);
   c->n_tris = n;
   c->bvh_depth = depth;
   c->jit_dirty = true;  // the scene-specialised kernel's traversal stack follows the depth
@@ -677,6 +699,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.cube = c->d_cube;
   p.cube_size = c->cube_size;
   p.bvh = c->d_bvh;
+  p.bvh4 = c->d_bvh4;
   p.tris = c->d_tris;
   p.n_tris = c->n_tris;
   p.accum = c->acc();
@@ -941,6 +964,10 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       if (c->exec_compat) key.flags |= F_EXEC_GHOST;
       key.halo_check = c->n_shards > 1 ? 1 : 0;
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
+      // the 4-wide tree (RT0_BVH4=1 in the environment); the stack also
+      // serves the binary walks the wavefront rounds keep
+      key.bvh4 = key.bvh_stack > 0 && c->d_bvh4 != nullptr && bvh4_enabled() ? 1 : 0;
+      if (key.bvh4) key.bvh_stack = std::max(key.bvh_stack, c->bvh4_stack);
       key.defer = defer ? 1 : 0;
       {  // 16-bit traversal stack entries + high bits in a 64-bit register (rt0_integrator.h BvhStack)
         const int entries = key.bvh_stack > 0 ? rt0h::jit_stack_entries(key) : 0;

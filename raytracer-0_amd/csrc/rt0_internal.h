@@ -9,6 +9,7 @@
 
 struct BvhNode;
 struct TriDev;
+struct Bvh4Node;
 
 namespace rt0h {
 int lookup_material(const std::string &name, rt0_mesh &m);
@@ -22,6 +23,10 @@ void default_config(rt0_config &c);
 // owner tags with RT0_TRI_CULL_BIT) -> pre-order inner nodes + leaf-order
 // triangles; returns the depth (edges root -> deepest leaf), -1 for n <= 0
 int bvh_build_sah(int n, const float *v, const int32_t *model, std::vector<BvhNode> &nodes, std::vector<TriDev> &tris);
+// the binary tree collapsed to 4-wide nodes (grandchildren become children);
+// returns the traversal stack entries a walk can need (pushes along the
+// deepest chain), nodes4 in pre-order
+int bvh4_collapse(const std::vector<BvhNode> &nodes, int n_tris, std::vector<Bvh4Node> &nodes4);
 int parse_config(const char *const *defines, int nd, const char *const *constants, int nc, rt0_config &c,
                  std::string &err);
 }  // namespace rt0h

@@ -72,6 +72,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
   if (k.defer && k.walk) o << "#define RT0_NEE_WALK 1\n";
   if (k.bvh_stack > 0 && k.stack16) o << "#define RT0_BVH_STACK16 1\n";
+  if (k.bvh_stack > 0 && k.bvh4) o << "#define RT0_BVH4 1\n";
   if (k.wf) o << "#define RT0_WAVEFRONT 1\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
@@ -523,6 +524,8 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     const char *w16 = getenv("RT0_BVH_STACK16"), *st = getenv("RT0_JIT_STACK");
     key.stack16 = w16 && atoi(w16) != 0 ? 1 : 0;
     if (st && nm > 0) key.bvh_stack = atoi(st);
+    const char *b4 = getenv("RT0_BVH4");
+    key.bvh4 = nm > 0 && key.bvh_stack > 0 && b4 && atoi(b4) != 0 ? 1 : 0;
     rc = rt0h::jit_compile(rt0h::jit_source(s, key), code, e);
   }
   if (code_size) *code_size = code.size();

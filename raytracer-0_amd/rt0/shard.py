@@ -201,6 +201,29 @@ def interleaved_band(height, world, per_rank=2, halo=24):
     return max(b, (2 * halo + 15) // 16 * 16)
 
 
+def cost_cuts(band_cost, band_rows, height, world, align=16):
+    """Row cuts [0, c1, ..., height] of `world` contiguous blocks of equal
+    measured cost: band_cost[b] is the time of rows [b * band_rows, (b + 1) *
+    band_rows) (a previous pass, or a calibration render); the cost inside a
+    band is taken as uniform and each cut is rounded to `align` rows (the
+    workgroup tile) and kept at least `align` rows after the previous one."""
+    import bisect
+    pre = [0.0]
+    for c in band_cost:
+        pre.append(pre[-1] + max(c, 0.0))
+    total = pre[-1]
+    cuts = [0]
+    for k in range(1, world):
+        target = total * k / world
+        b = min(len(band_cost) - 1, max(0, bisect.bisect_right(pre, target) - 1))
+        frac = (target - pre[b]) / band_cost[b] if band_cost[b] > 0 else 0.0
+        y = int(round((b + frac) * band_rows / align)) * align
+        y = max(cuts[-1] + align, min(y, height - (world - k) * align))
+        cuts.append(y)
+    cuts.append(height)
+    return cuts
+
+
 def block_rows(rank, band, height):
     """Rows of the contiguous block of `rank` (band = block_band)."""
     lo = min(height, rank * band)

@@ -1,6 +1,7 @@
 """One rank's share of a bench step, rendered alone (rank R of N, 16-row
-round-robin bands), for a kernel trace of a sharded launch:
-    rocprofv3 --kernel-trace ... -- python3 scripts/shard_trace.py c4 0 8"""
+round-robin bands; ReSTIR workloads: BAND-row bands, one pass per call), for
+a kernel trace of a sharded launch:
+    rocprofv3 --kernel-trace ... -- python3 scripts/shard_trace.py c4 0 8 [BAND]"""
 import os
 import sys
 
@@ -13,6 +14,14 @@ key, rank, n = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 wl = workloads.get(key)
 r = rt0.Renderer(wl["width"], wl["height"])
 workloads.configure(r, wl)
+if workloads.restir(wl):
+    if n > 1:
+        r.set_shard(rank, n, int(sys.argv[4]) if len(sys.argv) > 4 else 64)
+        r.set_halo(24)
+    for k in range(1, 7):
+        r.render(k, 1)
+        print("pass", k, r.last_kernel_ms(), r.last_render_path(), flush=True)
+    sys.exit(0)
 if n > 1:
     r.set_shard(rank, n, 16)
 for k in range(3):
