@@ -366,7 +366,7 @@ class Progressive:
 
 class Restir:
     """C3/C5: one pass per launch (frame-to-frame reservoir dependency); N>1:
-    two round-robin row bands per rank (the sky rows of C3/C5 cost a fraction
+    two or four round-robin row bands per rank (the sky rows of C3/C5 cost a fraction
     of the geometry rows: contiguous blocks left the slowest of 8 ranks at
     2.2-2.3x the mean, scripts/restir_shard_sim.py) + per-pass halo exchange
     at each band boundary + band gather."""
@@ -383,7 +383,11 @@ class Restir:
         dev = "cuda:%d" % local
         self.order = shard.StreamOrder(self.r, dev)
         if world > 1:
-            band = shard.interleaved_band(H, world)
+            # four round-robin bands per rank where each stays >= 64 rows (C5 at
+            # N=8: the slowest rank 1.48 ms vs 1.82 with two, strong-scaling
+            # ceiling 0.60 vs 0.52, profiles/r05/shard_sim), else two
+            per = 4 if H >= world * 4 * 64 else 2
+            band = shard.interleaved_band(H, world, per_rank=per)
             self.sh = shard.RestirShard(self.r, rank, world, H, W, dev, band=band, staged=staged, order=self.order)
             self.gather = shard.BandGather(H, W, rank, world, band, dev, staged=staged)
             # full-size accumulator padded to whole bands; this rank's bands are

@@ -90,6 +90,20 @@ def _halo_cases():
         yield H, world, shard.block_band(H, world), halo
     for H, world, halo in ((192, 2, 24), (1080, 8, 24), (4096, 8, 24), (200, 3, 16), (1080, 3, 24)):
         yield H, world, shard.interleaved_band(H, world, halo=halo), halo
+    # bench.py's four bands per rank (C5 at N=8: 128-row bands)
+    for H, world, halo in ((4096, 8, 24), (4096, 4, 24), (2048, 2, 24)):
+        yield H, world, shard.interleaved_band(H, world, per_rank=4, halo=halo), halo
+
+
+def test_cost_cuts_equal_cost_blocks():
+    """shard.cost_cuts: contiguous blocks of equal measured cost, aligned to
+    16 rows, every block non-empty, covering the image."""
+    cuts = shard.cost_cuts([1, 1, 1, 1, 4, 4, 1, 1], 512, 4096, 4)
+    assert cuts == [0, 1792, 2432, 2880, 4096]
+    assert shard.cost_cuts([1.0] * 64, 64, 4096, 8) == [512 * k for k in range(9)]
+    # a cost spike in one band: blocks stay >= 16 rows and in order
+    c = shard.cost_cuts([0.0] * 10 + [100.0] + [0.0] * 53, 64, 4096, 8)
+    assert c[0] == 0 and c[-1] == 4096 and all(b - a >= 16 and a % 16 == 0 for a, b in zip(c, c[1:]))
 
 
 def test_halo_plan_pairs_sends_with_recvs():
