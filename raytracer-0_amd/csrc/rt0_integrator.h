@@ -2723,7 +2723,10 @@ struct Integrator {
     } else if (mtype == M_REFR_FRESNEL || mtype == M_REFR_SCHLICK) {
       float nnt = inside < 0.0f ? fdiv(nt_eff, ncr) : fdiv(ncr, nt_eff);
       v3 tdir = refract(rd, nl, nnt);
-      if (length(tdir) == 0.0f) {  // total internal reflection
+      // total internal reflection: length(tdir) == 0 (raytracer.glsl:1844) as dot(tdir, tdir) == 0
+      // -- sqrt(x) == 0 exactly when x == 0 (f32 denormals preserved), one
+      // v_sqrt_f32 less per refraction
+      if (dot(tdir, tdir) == 0.0f) {
         ro = x + nl * EPSILON;
         rd = normalize(e * rdir + reflect(rd, nl));
         ++spec_b;
