@@ -24,7 +24,12 @@ For every workload:
     stream x2, 64-B gathers x1, bilinear 2x2 RGBA32F taps x0.5) + WRITE_SIZE;
     a kernel that mixes shapes gets its accumulator stream at x2 and the rest
     at the factor of its dominant shape, with the x0.5 .. x2 range beside it;
-    over the median kernel time -> GB/s and the fraction of 8 TB/s.
+    over the median kernel time -> GB/s and the fraction of 8 TB/s;
+  * clocks: the GPU clock bench.py sampled during the profiled run (its
+    gpu_clock, pp_dpm_sclk) and during the plain run the driver-style line
+    comes from, and the frac the kernel reaches at the plain run's clock
+    (the profiled median scaled by the clock ratio: these kernels are
+    issue-bound, their time follows the shader clock).
 """
 import json
 import os
@@ -71,6 +76,10 @@ for c in ("c1", "c2", "c3", "c4", "c5"):
                launches_per_step=lps, rocprof_median_ms=med, rocprof_min_ms=kt["min_ms"], rocprof_max_ms=kt["max_ms"],
                hip_event_ms=R["kernel_ms_per_launch"], achieved_tflops=ach, frac_spec=ach / PEAK_SPEC,
                frac_scalar=ach / PEAK_SCALAR, bench_frac=R["frac"])
+    clk_b = (b.get("gpu_clock") or {}).get("median_mhz")
+    clk_p = ((pr or {}).get("gpu_clock") or {}).get("median_mhz")
+    row["bench_clock_mhz"], row["profiled_clock_mhz"] = clk_b, clk_p
+    row["frac_spec_at_bench_clock"] = ach * clk_b / clk_p / PEAK_SPEC if clk_b and clk_p else None
     if pr:
         row["profiled_ms_per_step"] = pr["ms_per_step"]
         # the trace median covers every kept dispatch (warm-up steps included), ms_per_step only the timed ones:
@@ -110,11 +119,12 @@ print("FETCH_SIZE calibration, true bytes / counter bytes (scripts/fetch_calib.h
 print()
 print("| config | Msamples/s | FLOP/sample | kernel ms/launch: rocprof median (min-max) / HIP events | launches x median <= "
       "ms_per_step (profiled run, 1% jitter) | TFLOP/s | frac of 157.3 | frac of scalar peak | clock GHz | VALU busy | "
-      "lane util | HBM bytes/launch est. (range) / algorithmic | GB/s | frac of 8 TB/s |")
-print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+      "lane util | HBM bytes/launch est. (range) / algorithmic | GB/s | frac of 8 TB/s | clock MHz profiled / "
+      "plain run | frac of 157.3 at the plain run's clock |")
+print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
 for r in rows:
     chk = r.get("check_kernel_x_launches_le_step")
-    print("| %s | %.0f | %.0f | %.3f (%.3f-%.3f) / %.3f | %s %s | %.1f | %.3f | %.3f | %s | %s | %s | %s (%s-%s) / %s | %s | %s |" % (
+    print("| %s | %.0f | %.0f | %.3f (%.3f-%.3f) / %.3f | %s %s | %.1f | %.3f | %.3f | %s | %s | %s | %s (%s-%s) / %s | %s | %s | %s / %s | %s |" % (
         r["config"], r["msamples_s"], r["flop_per_sample"], r["rocprof_median_ms"], r["rocprof_min_ms"],
         r["rocprof_max_ms"], r["hip_event_ms"],
         "%.2f x %d = %.2f <= %.2f" % (r["rocprof_median_ms"], r["launches_per_step"],
@@ -123,4 +133,5 @@ for r in rows:
         r["achieved_tflops"], r["frac_spec"], r["frac_scalar"], f(r.get("clock_ghz"), "%.2f"),
         f(r.get("valu_busy"), "%.2f"), f(r.get("lane_util"), "%.2f"), f(r.get("traffic_est"), "%.3g"),
         f(r.get("traffic_lo"), "%.3g"), f(r.get("traffic_hi"), "%.3g"), f(r.get("algorithmic_bytes"), "%.3g"),
-        f(r.get("hbm_gbs"), "%.0f"), f(r.get("hbm_frac"), "%.3f")))
+        f(r.get("hbm_gbs"), "%.0f"), f(r.get("hbm_frac"), "%.3f"), f(r.get("profiled_clock_mhz"), "%.0f"),
+        f(r.get("bench_clock_mhz"), "%.0f"), f(r.get("frac_spec_at_bench_clock"), "%.3f")))
