@@ -205,6 +205,10 @@ class CpuBackend {
   }
 
   lastKernelMs() { return this._ms; }
+
+  setWavefront() {}  // (a HIP-backend scheduling choice: the JS integrator has one path)
+
+  lastRenderPath() { return 'cpu'; }
 }
 
 module.exports = { CpuBackend, parseDefines, parseConstants, sceneLines, sdfKinds };

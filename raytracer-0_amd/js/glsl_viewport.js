@@ -43,6 +43,8 @@ class AddonBackend {
   readAccum() { return this.a.readAccum(this.h); }
   tonemap(cont) { return this.a.tonemap(this.h, cont); }
   lastKernelMs() { return this.a.lastKernelMs(this.h); }
+  setWavefront(mode) { this.a.setWavefront(this.h, mode); }
+  lastRenderPath() { return this.a.lastRenderPath(this.h); }
 }
 
 function readImage(p) { return addonModule().readImage(p); }
@@ -315,6 +317,10 @@ class GlslViewport {
   image() { return this._b.tonemap(this.animatedScene ? 1.0 : 1.0 / Math.max(1, this.passes)); }
 
   lastKernelMs() { return this._b.lastKernelMs(); }
+  // rt0_set_wavefront: 0 off, 1 SDF scenes (the default), 2 also ReSTIR scenes with models
+  setWavefront(mode) { this._b.setWavefront(mode); }
+  // which kernels the last render ran: 'pass', 'deferred', 'wavefront' ('cpu' on the CPU backend)
+  renderPath() { return this._b.lastRenderPath(); }
 }
 
 module.exports = { GlslViewport, Vector3, sceneFromLines, sdfStatement, STATIC_CONSTANTS, ANIMATED_CONSTANTS,

@@ -477,6 +477,29 @@ static napi_value LastKernelMs(napi_env env, napi_callback_info info) {
   return num(env, ms);
 }
 
+// setWavefront(h, mode): rt0_set_wavefront (0 off, 1 SDF scenes, 2 also ReSTIR model scenes)
+static napi_value SetWavefront(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  int32_t mode = 1;
+  napi_get_value_int32(env, argv[1], &mode);
+  RC_OR_THROW(rt0_set_wavefront(c, mode));
+  return nullptr;
+}
+
+// lastRenderPath(h): which kernels the last render ran (rt0_last_render_path)
+static napi_value LastRenderPath(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  static const char *names[] = {"", "aot", "pass", "deferred", "wavefront"};
+  const int k = rt0_last_render_path(c);
+  napi_value v;
+  napi_create_string_utf8(env, k >= 0 && k <= 4 ? names[k] : "", NAPI_AUTO_LENGTH, &v);
+  return v;
+}
+
 static napi_value Version(napi_env env, napi_callback_info) {
   napi_value v;
   napi_create_string_utf8(env, rt0_version(), NAPI_AUTO_LENGTH, &v);
@@ -501,6 +524,8 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"clear", nullptr, Clear, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"resize", nullptr, Resize, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"lastKernelMs", nullptr, LastKernelMs, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setWavefront", nullptr, SetWavefront, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"lastRenderPath", nullptr, LastRenderPath, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setTexture", nullptr, SetTexture, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readPng", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readImage", nullptr, ReadPng, nullptr, nullptr, nullptr, napi_default, nullptr},

@@ -228,3 +228,35 @@ console.log(JSON.stringify(seen));
         py.append(list(vp.viewport))
         vp.updateTile()
     assert js == py and len(py) > 3
+
+
+@pytest.mark.gpu
+def test_js_wavefront_switch_and_render_path(cfgs, gpu_required, tmp_path):
+    """GlslViewport.setWavefront / renderPath (rt0_set_wavefront,
+    rt0_last_render_path through the addon): an SDF scene renders through the
+    wavefront rounds by default and through the pass kernel when switched
+    off, to the same image at the parity tolerance; the CPU backend says 'cpu'."""
+    cfg = [c for c in cfgs["configs"] if c["name"] == "sdf_cone"][0]
+    scene, sdf = rt0.scene_strings(cfg, cfgs)
+    defines, consts = rt0.config_strings(cfg)
+    src = """
+const fs = require('fs');
+const v = require(%r);
+const out = [];
+for (const mode of [1, 0]) {
+  const vp = new v.GlslViewport(null, {width: 32, height: 32});
+  vp.defines = %s; vp.constants = %s; vp.scene = %s; vp.sdf_meshes = %s;
+  vp.setWavefront(mode);
+  vp.render(2);
+  out.push(vp.renderPath());
+  fs.writeFileSync(%r + mode, Buffer.from(vp.accumulator().buffer));
+}
+const c = new v.GlslViewport(null, {width: 4, height: 4, backend: 'cpu'});
+out.push(c.renderPath());
+console.log(JSON.stringify(out));
+""" % (VIEWPORT, json.dumps(defines), json.dumps(consts), json.dumps(scene), json.dumps(sdf), str(tmp_path / "acc"))
+    paths = json.loads(run_node(src).strip().splitlines()[-1])
+    assert paths[:2] == ["wavefront", "pass"], paths
+    a = np.fromfile(str(tmp_path / "acc1"), np.float32).reshape(32, 32, 4)
+    b = np.fromfile(str(tmp_path / "acc0"), np.float32).reshape(32, 32, 4)
+    assert np.isfinite(a).all() and abs(a[..., :3].mean() - b[..., :3].mean()) <= 0.01 * max(1.0, b[..., :3].mean())
