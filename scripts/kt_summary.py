@@ -50,8 +50,20 @@ def main():
         tail = {k: dur[k] for k in TAIL if dur[k]} if dur["rt0_jit_resolve"] else {"rt0_sum_kernel": sums}
         nl = min(len(v) for v in tail.values())
         per = {k: len(dur[k]) // nl for k in WF if dur[k]}
-        pas = [sum(sum(dur[k][i * per[k]:(i + 1) * per[k]]) for k in per) + sum(v[i] for v in tail.values())
-               for i in range(nl)]
+        # a launch's time is its span: from its first dispatch's start to the
+        # end of the dispatch that completes it (rt0_sum_kernel, or resolve) --
+        # the halves on two HIP streams overlap, so the kernels' durations
+        # summed would count the overlap twice (kept as per-kernel busy time)
+        last = "rt0_jit_resolve" if dur["rt0_jit_resolve"] else None
+        ends = [float(r["End_Timestamp"]) for r in rows
+                if (r["Kernel_Name"].strip() == last if last else r["Kernel_Name"].strip().startswith("rt0_sum_kernel"))]
+        mine = set(GROUP)
+        starts = sorted(float(r["Start_Timestamp"]) for r in rows if r["Kernel_Name"].strip() in mine)
+        pas, lo = [], 0
+        for i in range(nl):
+            first = [t for t in starts[lo:] if t < ends[i]]
+            pas.append(ends[i] - first[0] if first else 0.0)
+            lo += len(first)
         per_kernel = {k: statistics.median([sum(dur[k][i * per[k]:(i + 1) * per[k]]) for i in range(skip, nl)]) / 1e6
                       for k in per if nl > skip}
         per_kernel.update({k: statistics.median(v[skip:nl]) / 1e6 for k, v in tail.items() if nl > skip})
