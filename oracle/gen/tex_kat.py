@@ -12,7 +12,10 @@ ReSTIRData, so the fixture holds the exact float32 (u, v) the executor used.
 
 Output: tests/golden/tex_filter_kat.npz -- per case k: tex_k (H x W x 4
 uint8), uv_k (4096 x 2 float32), n_k (4096 x 4 uint16: the sample x 65535,
-which the executor's readback makes an integer).  tests/test_oracle_golden.py
+which the executor's readback makes an integer); and a cubemap case --
+cube_faces (6 x 16 x 16 x 3, order -X -Y -Z +X +Y +Z), cube_dir_* / cube_rgb_*
+(4 096 directions each, spread over the sphere and next to a face edge and
+its corners) -- for the seamless filter's corner rule.  tests/test_oracle_golden.py
 checks the restatement's tex_fetch_ss (oracle/rt0_oracle.c) against it.
 
 usage: python3 oracle/gen/tex_kat.py
@@ -97,6 +100,54 @@ def run(tex, expr, d):
     return n.astype(np.uint16), uv
 
 
+CUBE = """#version 300 es
+precision highp float;
+precision highp int;
+uniform vec2 u_resolution;
+uniform uint u_frame;
+uniform sampler2D u_bufferA;
+uniform samplerCube u_cubemap;
+layout(location = 0) out vec4 FragColor;
+layout(location = 1) out vec4 ReSTIRData;
+layout(location = 2) out vec4 ReSTIRAux;
+void main() {
+  ivec2 p = ivec2(gl_FragCoord.xy);
+  float i = float(p.y * 64 + p.x);
+  vec3 d;
+  if (%s) {  // directions spread over the sphere
+    float z = 1.0 - 2.0 * (i + 0.5) / 4096.0;
+    float r = sqrt(max(0.0, 1.0 - z * z));
+    float a = i * 2.399963;
+    d = vec3(r * cos(a), z, r * sin(a));
+  } else {  // next to the +Z / +X edge and its two corners
+    float a = -1.0 + 2.0 * (float(p.x) + 0.5) / 64.0;
+    float b = 0.9 + 0.1 * (float(p.y) + 0.5) / 64.0;
+    d = vec3(b, a, 1.0);
+  }
+  FragColor = texture(u_cubemap, d);
+  ReSTIRData = vec4(d, 0.0);
+  ReSTIRAux = vec4(0.0);
+}
+"""
+
+
+def run_cube(faces, spread, d):
+    """The cubemap (RGB8, GL_LINEAR, seamless as GLES3 filters it; glrun.c
+    --cube) at 4 096 directions: (RGB, the direction)."""
+    frag = os.path.join(d, "c.frag")
+    with open(frag, "w") as f:
+        f.write(CUBE % ("true" if spread else "false"))
+    cf = os.path.join(d, "cube.rgb8")
+    faces.tofile(cf)
+    prefix = os.path.join(d, "q")
+    subprocess.run([GLRUN, "--frag", frag, "--w", "64", "--h", "64", "--frames", "1", "--single", "--restir-out",
+                    "--out", prefix, "--cube", str(faces.shape[1]), cf], check=True, capture_output=True, text=True,
+                   timeout=300)
+    c = np.fromfile(prefix + "_f1_c.bin", np.float32).reshape(-1, 4)[:, :3].copy()
+    dirs = np.fromfile(prefix + "_f1_r.bin", np.float32).reshape(-1, 4)[:, :3].copy()
+    return c, dirs
+
+
 def main():
     arrays, names = {}, []
     with tempfile.TemporaryDirectory() as d:
@@ -105,6 +156,10 @@ def main():
             arrays["tex_%d" % k], arrays["uv_%d" % k], arrays["n_%d" % k] = tex, uv, n
             names.append(name)
             print(name, tex.shape, n[:2].tolist())
+        faces = np.random.default_rng(7).integers(0, 256, (6, 16, 16, 3), dtype=np.uint8)
+        arrays["cube_faces"] = faces
+        for tag, spread in (("spread", True), ("edge", False)):
+            arrays["cube_rgb_" + tag], arrays["cube_dir_" + tag] = run_cube(faces, spread, d)
     arrays["names"] = np.array(names)
     np.savez_compressed(os.path.join(REPO, "tests", "golden", "tex_filter_kat.npz"), **arrays)
 

@@ -1303,6 +1303,10 @@ DEV T4 cube_sample(const LaunchParams &P, v3 d) {
   const float a = x - fx, b = y - fy;
   const int x0 = (int)fx, y0 = (int)fy;
   uint32_t q00, q10, q01, q11;
+  // a footprint over a cube corner: the texel beyond both edges belongs to no
+  // face; like the reference executor (the cubemap KAT) it is the
+  // average of the three texels that meet there (bit 0..3: which tap)
+  int corner = -1;
   if (x0 >= 0 && y0 >= 0 && x0 + 1 < n && y0 + 1 < n) {  // footprint inside the face (the common case)
     const uint32_t *__restrict__ img = P.cube + ((size_t)face * n + y0) * n + x0;
     q00 = img[0];
@@ -1314,12 +1318,19 @@ DEV T4 cube_sample(const LaunchParams &P, v3 d) {
     q10 = cube_texel(P, face, x0 + 1, y0);
     q01 = cube_texel(P, face, x0, y0 + 1);
     q11 = cube_texel(P, face, x0 + 1, y0 + 1);
+    const bool ox0 = x0 < 0 || x0 >= n, ox1 = x0 + 1 < 0 || x0 + 1 >= n;
+    const bool oy0 = y0 < 0 || y0 >= n, oy1 = y0 + 1 < 0 || y0 + 1 >= n;
+    corner = ox0 && oy0 ? 0 : ox1 && oy0 ? 1 : ox0 && oy1 ? 2 : ox1 && oy1 ? 3 : -1;
   }
   float r[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    const float t00 = (float)((q00 >> (8 * c)) & 255u), t10 = (float)((q10 >> (8 * c)) & 255u);
-    const float t01 = (float)((q01 >> (8 * c)) & 255u), t11 = (float)((q11 >> (8 * c)) & 255u);
+    float t00 = (float)((q00 >> (8 * c)) & 255u), t10 = (float)((q10 >> (8 * c)) & 255u);
+    float t01 = (float)((q01 >> (8 * c)) & 255u), t11 = (float)((q11 >> (8 * c)) & 255u);
+    if (corner == 0) t00 = (t10 + t01 + t11) / 3.0f;
+    else if (corner == 1) t10 = (t00 + t11 + t01) / 3.0f;
+    else if (corner == 2) t01 = (t11 + t00 + t10) / 3.0f;
+    else if (corner == 3) t11 = (t01 + t10 + t00) / 3.0f;
     const float top = t00 + a * (t10 - t00), bot = t01 + a * (t11 - t01);
     r[c] = (top + b * (bot - top)) / 255.0f;
   }

@@ -516,3 +516,29 @@ def test_oracle_executor_texture_filter(name, cfgs):
     ok, _ = pixel_match(got, gold)
     bad = 1.0 - ok[valid].mean()
     assert bad <= TEX_FILTER_BAD[name], (name, bad)
+
+
+def test_cubemap_corner_kat():
+    """The executor's seamless cubemap filter (GL_LINEAR on RGB8 faces,
+    oracle/gen/tex_kat.py): float bilinear across face edges, and a corner
+    footprint's missing texel as the average of the three that meet there
+    (oracle cube_sample; the product's cube_sample the same).  Directions
+    spread over the sphere and next to the +Z/+X edge and its corners: every
+    sample within 5e-4 (the executor's own rounding of the filter)."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(O.__file__), "librt0_oracle.so"))
+    fn = lib.or_cube_probe
+    fn.restype = None
+    K = np.load(os.path.join(GOLD, "tex_filter_kat.npz"))
+    faces = [np.ascontiguousarray(K["cube_faces"][i]) for i in range(6)]
+    ptrs = (ctypes.c_void_p * 6)(*[f.ctypes.data for f in faces])
+    out = (ctypes.c_float * 3)()
+    for tag in ("spread", "edge"):
+        dirs, want = K["cube_dir_" + tag], K["cube_rgb_" + tag]
+        got = np.empty_like(want)
+        for i, d in enumerate(dirs):
+            dd = np.ascontiguousarray(d, np.float32)
+            fn(ptrs, faces[0].shape[0], dd.ctypes.data_as(ctypes.c_void_p), out)
+            got[i] = out[:]
+        err = np.abs(got - want).max()
+        assert err <= 5e-4, (tag, float(err))
