@@ -77,3 +77,40 @@ def test_clock_sampler_reads_the_starred_level(tmp_path):
     none.start()
     none.stop()
     assert none.report() == {"median_mhz": None, "source": None, "error": "no pp_dpm_sclk for PCI 0000:05"}
+
+
+def test_kt_summary_wavefront_launch_is_its_span(tmp_path):
+    """scripts/kt_summary.py on a synthetic kernel trace of two wavefront
+    launches whose halves overlap on two streams: a launch's time is its span
+    (first dispatch start -> rt0_sum_kernel end), not the sum of its kernels'
+    durations; the warm-up launch is skipped."""
+    import csv
+    import json
+    import subprocess
+    rows = []
+
+    def k(name, t0, t1):
+        rows.append({"Kernel_Name": name, "Start_Timestamp": str(int(t0 * 1e6)), "End_Timestamp": str(int(t1 * 1e6))})
+
+    for base in (0.0, 100.0):  # two launches, ms
+        # two halves: shade/plan/march overlapping pairwise
+        for h in (0.0, 0.5):
+            k("rt0_jit_wf_shade", base + h, base + h + 2.0)
+            k("rt0_jit_wf_plan", base + h + 2.0, base + h + 2.1)
+            k("rt0_jit_wf_march", base + h + 2.1, base + h + 6.0)
+        k("rt0_jit_wf_shade", base + 6.5, base + 7.0)
+        k("rt0_jit_wf_shade", base + 6.6, base + 7.1)
+        k("rt0_sum_kernel<>", base + 7.1, base + 7.2)
+    d = tmp_path / "trace"
+    d.mkdir()
+    with open(d / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    out = tmp_path / "kt.json"
+    subprocess.run([sys.executable, os.path.join(REPO, "scripts", "kt_summary.py"), str(out), str(d), "1"],
+                   check=True, capture_output=True)
+    res = json.load(open(out))
+    assert res["kept"] == 1 and res["median_ms"] == pytest.approx(7.2, abs=1e-6)
+    # the per-kernel busy sums still count both halves
+    assert res["per_kernel_median_ms"]["rt0_jit_wf_march"] == pytest.approx(7.8, abs=1e-6)
