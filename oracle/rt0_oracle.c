@@ -187,6 +187,7 @@ typedef struct {
   int scatter0_exit; /* SWIFTSHADER_SCATTER0_EXIT: the executor's first-iteration `continue` (see radiance) */
   int scatter_exit;  /* SWIFTSHADER_SCATTER_EXIT: the executor retires the lane at every scatter `continue` */
   int ss_tex;        /* SWIFTSHADER_TEX_FILTER: the executor's fixed-point RGBA8 bilinear filter (tex_fetch_ss) */
+  int ss_quad_lights; /* SWIFTSHADER_QUAD_LIGHTS: light_index[i] in brdf's light loops read at the quad's first lane's index (rule 7) */
   int dbg_paths;     /* RT0_DEBUG_PATHS: non-ReSTIR reservoir outputs carry per-sample path statistics */
   /* camera uniforms (index.js:421-423) */
   v3 cam_pos, cam_look, cam_params;
@@ -213,6 +214,10 @@ typedef struct {
   int diff_b, spec_b, trans_b, scat_ev;
   int last_depth, first_scat; /* RT0_DEBUG_PATHS */
   float dbg_hist, dbg_ev;      /* RT0_DEBUG_PATHS: depth history (base 16), loop-exit events (base 8) */
+  float dbg_in[2], dbg_sn[2];  /* RT0_DEBUG_PATHS 2: in-scatter / surface NEE radiance (r+g+b) of light slots 0, 1 */
+  int q0_iters;                /* SWIFTSHADER_QUAD_LIGHTS: bounce-loop iterations of the quad's first lane (-1: this is it) */
+  unsigned nee_mask;           /* bounces at which this lane ran brdf's light loop (bit d) */
+  unsigned q0_nee_mask;        /* the quad's first lane's nee_mask */
   float hero;
   /* ReSTIR */
   const float *tex[6]; /* restir_buffer, restir_aux, h1, h1a, h2, h2a */
@@ -1139,6 +1144,25 @@ static inline float spectralIOR(float lambda, float A) {
 }
 
 /* brdf(), raytracer.glsl:1804-1980 */
+/* SWIFTSHADER_QUAD_LIGHTS (mask_kat.py rule 7 on brdf's light loops,
+ * raytracer.glsl:1955-1974): the executor reads the loop-indexed
+ * light_index[i] at the index register of the quad's first lane.  When that
+ * lane runs the same light loop at the same bounce the register holds i; when
+ * it ran the loop at an earlier bounce only (it has left the bounce loop or
+ * took a specular bounce here) the register holds the loop's end, one past
+ * the array, which reads element 0 -- mesh 0; before any run it holds 0.
+ * Fitted on the spectral_vol_2l fixture (tests/golden, two lights): 3.4% of
+ * pixels off by > 5% (19.8% under GLSL semantics); the rejected fits are in
+ * DESIGN.md 4.16. */
+static int quad_light_index(Frag *F, int i, float bounce) {
+  const Oracle *o = F->o;
+  const int d = (int)bounce;
+  if (i == 0) F->nee_mask |= 1u << d;
+  if (!o->ss_quad_lights || o->n_lights < 2 || F->q0_iters < 0 || (F->q0_nee_mask & (1u << d)))
+    return o->light_index[i];
+  if (F->q0_nee_mask & ((1u << d) - 1u)) return 0;
+  return o->light_index[0];
+}
 static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *rd, v3 *mask, v3 *acc,
                  int *spec, float seed, float bounce) {
   const Oracle *o = F->o;
@@ -1249,7 +1273,7 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
     } else if (o->use_mis && o->n_lights > 0) {
       v3 mc = V(0, 0, 0);
       for (int i = 0; i < o->n_lights; ++i) {
-        int idx = o->light_index[i];
+        int idx = quad_light_index(F, i, bounce);
         if (idx < 0) continue;
         const Mesh *L = &o->meshes[idx];
         if (L->mat.t != M_LIGHT) continue;
@@ -1264,10 +1288,11 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
       *acc = add(*acc, mul(mc, *mask));
     } else {
       for (int i = 0; i < o->n_lights; ++i) {
-        int idx = o->light_index[i];
+        int idx = quad_light_index(F, i, bounce);
         if (idx >= 0) {
           v3 ls = calcDirectLighting(F, &o->meshes[idx], x, nl, base + 5681.123f + bounce * 7895.13f);
           *acc = add(*acc, mul(ls, *mask));
+          if (i < 2) { v3 t = mul(ls, *mask); F->dbg_sn[i] += t.x + t.y + t.z; }
         }
       }
     }
@@ -1388,7 +1413,9 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
             float den = 1.0f + g2 - 2.0f * VOL_G * ct;
             float phase = (1.0f - g2) / (FOUR_PI * den * sqrtf(den));
             float Tf = expf(-VOL_SIGMA_T * ts);
-            acc = add(acc, muls(muls(muls(mul(mul(mask, lm->mat.c), lm->mat.e), phase), Tf), PI_F * omega));
+            v3 term = muls(muls(muls(mul(mul(mask, lm->mat.c), lm->mat.e), phase), Tf), PI_F * omega);
+            acc = add(acc, term);
+            if (li < 2) F->dbg_in[li] += term.x + term.y + term.z;
           }
         }
         rd = sampleHG(rd, VOL_G, seed + 8293.7f + (float)depth * 773.3f);
@@ -1506,6 +1533,7 @@ static v3 shade_pixel(Frag *F, int px, int py) {
   F->first_scat = -1;
   F->dbg_hist = 0.0f;
   F->dbg_ev = 0.0f;
+  F->dbg_in[0] = F->dbg_in[1] = F->dbg_sn[0] = F->dbg_sn[1] = 0.0f;
   F->hero = 550.0f;
   float stx = 2.0f * fcx / rx - 1.0f, sty = 2.0f * fcy / ry - 1.0f;
   float aspect = rx / ry;
@@ -1712,6 +1740,7 @@ int or_set_constant(void *h, const char *name, double v) {
   else if (!strcmp(name, "SWIFTSHADER_SCATTER0_EXIT")) o->scatter0_exit = iv;
   else if (!strcmp(name, "SWIFTSHADER_SCATTER_EXIT")) o->scatter_exit = iv;
   else if (!strcmp(name, "SWIFTSHADER_TEX_FILTER")) o->ss_tex = iv;
+  else if (!strcmp(name, "SWIFTSHADER_QUAD_LIGHTS")) o->ss_quad_lights = iv;
   else if (!strcmp(name, "RT0_DEBUG_PATHS")) o->dbg_paths = iv;
   else if (!strcmp(name, "RENDER_MODE")) {
     o->render_mode = iv;
@@ -1784,10 +1813,25 @@ int or_render_frame(void *h, unsigned frame, float *out, const float *const *res
       F.fr_W = 0; F.fr_M = 0; F.fr_ws = 0; F.fr_age = 0; F.fr_idx = -1;
       memset(F.fr_pos, 0, sizeof F.fr_pos);
       memset(F.fr_col, 0, sizeof F.fr_col);
+      F.q0_iters = -1;
+      F.nee_mask = 0;
+      if (o->ss_quad_lights && ((x | y) & 1)) {  /* the quad's first lane's path, rendered aside */
+        Frag Q = F;
+        const uint64_t q0 = Q.n_iter;
+        Q.nee_mask = 0;
+        (void)shade_pixel(&Q, x & ~1, y & ~1);
+        F.q0_iters = (int)(Q.n_iter - q0);
+        F.q0_nee_mask = Q.nee_mask;
+      }
       const uint64_t it0 = F.n_iter;
       v3 col = shade_pixel(&F, x, y);
       size_t p = ((size_t)y * o->w + x) * 4;
       out[p] = col.x; out[p + 1] = col.y; out[p + 2] = col.z; out[p + 3] = 0.0f;
+      if (o->dbg_paths == 2 && !o->use_restir_def && restir_main && restir_aux) {
+        restir_main[p] = F.dbg_in[0]; restir_main[p + 1] = F.dbg_in[1];
+        restir_main[p + 2] = F.dbg_sn[0]; restir_main[p + 3] = F.dbg_sn[1];
+        continue;
+      }
       if (o->dbg_paths && !o->use_restir_def && restir_main && restir_aux) {
         restir_main[p] = (float)(F.n_iter - it0); restir_main[p + 1] = F.dbg_hist;
         restir_main[p + 2] = (float)F.scat_ev; restir_main[p + 3] = (float)F.diff_b;

@@ -542,3 +542,53 @@ def test_cubemap_corner_kat():
             got[i] = out[:]
         err = np.abs(got - want).max()
         assert err <= 5e-4, (tag, float(err))
+
+
+# Two lights: brdf's surface light loop (raytracer.glsl:1955-1974) reads
+# light_index[i] at the index register of the 2x2 quad's first lane
+# (SWIFTSHADER_QUAD_LIGHTS, mask_kat.py rule 7).  Measured bad-pixel fractions
+# per quad lane (first, then the other three) under GLSL semantics -> with the
+# model: spectral_vol_2l (fitted) 0% | 25-27% -> 0% | 4.1-4.9%, 3.4% overall;
+# spectral_2l_novol (held out) 0.02% | 8.5-8.8% -> 0.02% | 1.5-1.7%, 1.2%
+# overall.  One-light fixtures are unchanged by the model (a one-trip loop
+# has no index register).
+QUAD_LIGHTS = {"spectral_vol_2l": (0.04, 0.01), "spectral_2l_novol": (0.015, 2e-3)}
+
+
+def _two_light(name, cfgs, quad_lights):
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    gold = G["samples"][..., :3]
+    frames = G["frames"] if "frames" in G else range(1, gold.shape[0] + 1)
+    o = O.Oracle(cfg, cfgs, width=gold.shape[2], height=gold.shape[1],
+                 overrides={"SWIFTSHADER_GHOST": 1, "SWIFTSHADER_QUAD_LIGHTS": quad_lights})
+    got = np.stack([o.frame(int(k))[0] for k in frames])[..., :3]
+    valid = G["conformant"] if "conformant" in G else G["valid"] if "valid" in G else np.ones(gold.shape[:3], bool)
+    ok, _ = pixel_match(got, gold)
+    return got, gold, valid, ok
+
+
+@pytest.mark.parametrize("name", sorted(QUAD_LIGHTS))
+def test_two_light_quad_first_lane_is_glsl(name, cfgs):
+    """Under GLSL semantics the quad's first lane matches the reference (it is
+    the lane whose index register the loop reads) and the other three depart
+    -- a quad-coupled executor effect, not a restatement error."""
+    if not have(name):
+        pytest.skip("fixture %s not generated" % name)
+    _, _, valid, ok = _two_light(name, cfgs, 0)
+    first = valid[:, 0::2, 0::2]
+    assert 1.0 - ok[:, 0::2, 0::2][first].mean() <= 0.002
+    for ly, lx in ((0, 1), (1, 0), (1, 1)):
+        m = valid[:, ly::2, lx::2]
+        assert 1.0 - ok[:, ly::2, lx::2][m].mean() >= 0.05, (ly, lx)
+
+
+@pytest.mark.parametrize("name", sorted(QUAD_LIGHTS))
+def test_two_light_executor_quad_lights(name, cfgs):
+    if not have(name):
+        pytest.skip("fixture %s not generated" % name)
+    got, gold, valid, ok = _two_light(name, cfgs, 1)
+    bound, mean_tol = QUAD_LIGHTS[name]
+    bad = 1.0 - ok[valid].mean()
+    assert bad <= bound, (name, bad)
+    assert abs(got[valid].mean() - gold[valid].mean()) <= mean_tol * max(1.0, abs(gold[valid].mean()))
