@@ -55,8 +55,8 @@ executor being thread-count dependent): shaders whose GLSL ES
      make_shader.js rewrites it, a light loop over the const light_index array
      calling an intersection() with a mesh loop, inside radiance()'s loop with
      lanes breaking at different iterations) is executed correctly
-     (inscatter_two_lights): the two-light departure is rule 8 (a scatter's
-     `continue` precedes every in-scatter loop of a later bounce).
+     (inscatter_two_lights): the two-light departure is brdf's light loop
+     (rule 11 below), not this one.
 
 QUAD CONTINUE (json key "quad_continue"; 2x2 images, ThreadCount=1): the
 reference's bounce loop reduced to its control flow (radiance(),
@@ -75,16 +75,31 @@ SCATTERING_EVENTS cap `break`, 2049), then a bounce update and the caps
      helpers).  (continue_then_break above, a different body, retires lane 0
      too: the rule depends on the code shape, so this case follows the
      reference's.)
+QUAD LIGHTS (json key "quad_lights"; 8x8, ThreadCount=1): brdf's light loop
+(raytracer.glsl:1955-1974: `for i < light_index.length()` over the const
+light index array) called from a bounce loop whose lanes break at different
+iterations and skip the call in others (a specular bounce's `continue`);
+each lane records, per iteration, 1 + light_index[0] + 4 light_index[1] as
+read (10 when both reads are right):
+ 11. the loop-indexed read uses the index register of the quad's FIRST lane:
+     both reads are right exactly when that lane runs the loop in the same
+     iteration, live or as the ghost call of the iteration it breaks in
+     (rule 1); otherwise both read one stale index.  The stale index depends
+     on the code shape: the end of the loop (out of bounds, reads 0: value 1)
+     in a loop without `continue` before its break (quad_lights_plain), 0
+     (value 6) with a never-taken `continue` there (quad_lights_shape), either
+     with a taken one (quad_lights_scatter, the medium's scatter `continue`).
 Measured on the reference shader itself (make_golden.py instrument_paths):
 this rule is one of several departures in its volumetric loop -- others make
 a lane repeat depth 0, and about a third of 2x2 quads never finish -- so the
 fixture keeps executor path records and marks the lanes that run as GLSL says.
 
-usage: python3 oracle/gen/mask_kat.py
+usage: python3 oracle/gen/mask_kat.py [--only quad_lights]
 """
 import json
 import os
 import subprocess
+import sys
 
 import numpy as np
 
@@ -506,6 +521,51 @@ def run_quad(cms, cov, cwd):
     return out
 
 
+QL_TPL = """
+const lowp int LIDX[2] = int[](1, 2);
+int specOf(ivec2 p) {
+  int lane = (p.x & 1) + 2 * (p.y & 1);
+  int quad = ((p.x >> 1) + (p.y >> 1)) & 3;
+  return (lane * 5 + quad * 3) %% 7;
+}
+int scatOf(ivec2 p) {
+  int lane = (p.x & 1) + 2 * (p.y & 1);
+  int quad = ((p.x >> 1) + (p.y >> 1)) & 3;
+  return %s;
+}
+void nee(int d, inout float rec[4]) {
+  float v = 1.0;
+  for (int i = 0; i < int(LIDX.length()); ++i) {
+    int idx = int(LIDX[i]);
+    if (idx >= 0) v += float(idx) * (i == 0 ? 1.0 : 4.0);
+  }
+  rec[d] = v;
+}
+void main() {
+  g0 = 0.0; g1 = 0.0; g2 = 0.0; g3 = 0.0;
+  ivec2 p = ivec2(gl_FragCoord.xy);
+  int stop = stopOf(p);
+  int sm = specOf(p);
+  int sc = scatOf(p);
+  float rec[4];
+  for (int k = 0; k < 4; ++k) rec[k] = 0.0;
+  for (int d = 0; d < 4; ++d) {
+    %s
+    if (d == stop) break;
+    if (((sm >> d) & 1) != 0) continue;
+    nee(d, rec);
+  }
+  float o0 = rec[0], o1 = rec[1], o2 = rec[2], o3 = float(sm);
+  g0 = rec[3]; g1 = float(sc);
+"""
+# name -> (scatOf body, the statement before the break)
+QL_CASES = {
+    "quad_lights_plain": ("0", ""),
+    "quad_lights_shape": ("0", "if (u_frame > 1000u) continue;"),
+    "quad_lights_scatter": ("((lane * 3 + quad * 5) % 4) << 1", "if (((sc >> d) & 1) != 0) continue;"),
+}
+
+
 def run_case(name, body, cwd=None):
     frag = os.path.join(GEN, name + ".frag")
     with open(frag, "w") as f:
@@ -522,8 +582,34 @@ def run_case(name, body, cwd=None):
              "o": [float(v) for v in o[y, x]]} for y in range(H) for x in range(W)]
 
 
+def threads1_dir():
+    t1 = os.path.join(GEN, "threads1")
+    os.makedirs(t1, exist_ok=True)
+    with open(os.path.join(t1, "SwiftShader.ini"), "w") as f:
+        f.write("[Processor]\nThreadCount=1\n")
+    return t1
+
+
+def quad_lights(t1):
+    out = {}
+    for name, (scat, pre) in QL_CASES.items():
+        rows = run_case(name, QL_TPL % (scat, pre), cwd=t1)
+        out[name] = [{"x": r["x"], "y": r["y"], "stop": r["stop"], "spec": int(r["o"][3]), "scat": int(r["g"][1]),
+                      "rec": r["o"][:3] + [r["g"][0]]} for r in rows]
+        print(name, [r["rec"] for r in out[name][:4]])
+    return out
+
+
 def main():
     os.makedirs(GEN, exist_ok=True)
+    path = os.path.join(REPO, "tests", "golden", "mask_kat.json")
+    if sys.argv[1:] == ["--only", "quad_lights"]:  # refresh that section alone (the others take minutes)
+        with open(path) as f:
+            out = json.load(f)
+        out["quad_lights"] = quad_lights(threads1_dir())
+        with open(path, "w") as f:
+            json.dump(out, f, separators=(",", ":"))
+        return
     out = {"_doc": "per-pixel outputs of the known-answer shaders of oracle/gen/mask_kat.py run by the oracle's "
                    "executor (SwiftShader 4.1); g = FragColor (g0..g3), o = ReSTIRData (o0..o3)",
            "width": W, "height": H, "cases": {}}
@@ -534,10 +620,7 @@ def main():
         for r in rows[:4]:
             print("   x=%d y=%d stop=%d g=%s o=%s" % (r["x"], r["y"], r["stop"], r["g"], r["o"]))
     # departures from GLSL semantics, one executor thread (deterministic)
-    t1 = os.path.join(GEN, "threads1")
-    os.makedirs(t1, exist_ok=True)
-    with open(os.path.join(t1, "SwiftShader.ini"), "w") as f:
-        f.write("[Processor]\nThreadCount=1\n")
+    t1 = threads1_dir()
     out["departures"] = {}
     for name, (body, glsl) in DEPARTURES.items():
         rows = run_case(name, body, cwd=t1)
@@ -550,7 +633,8 @@ def main():
         rows = run_quad(cms, cov, t1)
         out["quad_continue"].append({"cms": list(cms), "cov": list(cov) if cov else None, "lanes": rows})
         print("quad_continue cms %s cov %s: %s" % (cms, cov, [r["exec"] for r in rows]))
-    with open(os.path.join(REPO, "tests", "golden", "mask_kat.json"), "w") as f:
+    out["quad_lights"] = quad_lights(t1)
+    with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))
 
 

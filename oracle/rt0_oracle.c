@@ -214,10 +214,11 @@ typedef struct {
   int diff_b, spec_b, trans_b, scat_ev;
   int last_depth, first_scat; /* RT0_DEBUG_PATHS */
   float dbg_hist, dbg_ev;      /* RT0_DEBUG_PATHS: depth history (base 16), loop-exit events (base 8) */
-  float dbg_in[2], dbg_sn[2];  /* RT0_DEBUG_PATHS 2: in-scatter / surface NEE radiance (r+g+b) of light slots 0, 1 */
   int q0_iters;                /* SWIFTSHADER_QUAD_LIGHTS: bounce-loop iterations of the quad's first lane (-1: this is it) */
   unsigned nee_mask;           /* bounces at which this lane ran brdf's light loop (bit d) */
   unsigned q0_nee_mask;        /* the quad's first lane's nee_mask */
+  unsigned nee_gmask, q0_nee_gmask; /* the same for ghost calls' runs */
+  int cur_depth;               /* radiance()'s bounce-loop iteration (a ghost brdf's light loop marks it) */
   float hero;
   /* ReSTIR */
   const float *tex[6]; /* restir_buffer, restir_aux, h1, h1a, h2, h2a */
@@ -1144,24 +1145,28 @@ static inline float spectralIOR(float lambda, float A) {
 }
 
 /* brdf(), raytracer.glsl:1804-1980 */
-/* SWIFTSHADER_QUAD_LIGHTS (mask_kat.py rule 7 on brdf's light loops,
+/* SWIFTSHADER_QUAD_LIGHTS (mask_kat.py rule 11, brdf's light loop,
  * raytracer.glsl:1955-1974): the executor reads the loop-indexed
- * light_index[i] at the index register of the quad's first lane.  When that
- * lane runs the same light loop at the same bounce the register holds i; when
- * it ran the loop at an earlier bounce only (it has left the bounce loop or
- * took a specular bounce here) the register holds the loop's end, one past
- * the array, which reads element 0 -- mesh 0; before any run it holds 0.
- * Fitted on the spectral_vol_2l fixture (tests/golden, two lights): 3.4% of
- * pixels off by > 5% (19.8% under GLSL semantics); the rejected fits are in
- * DESIGN.md 4.16. */
+ * light_index[i] at the index register of the quad's first lane.  It holds
+ * i when that lane runs the same loop in the same bounce-loop iteration --
+ * live, or as the ghost call of the iteration it breaks in (rule 1; the
+ * plain loop is unrolled, rule 5) -- and is stale otherwise (KATs
+ * quad_lights_*: every pixel).  The stale value depends on the loop's code
+ * shape (the KATs give the end index or 0): without a `continue` before the
+ * breaks it reads as mesh 0 (the end index, one past the array, reads 0);
+ * with the medium's scatter `continue` (USE_VOLUMETRICS) as mesh 0 after a
+ * run of the loop and as element 0 before any, and the ghost run does not
+ * refresh it -- those two choices fitted on spectral_vol_2l, the rest held
+ * out. */
 static int quad_light_index(Frag *F, int i, float bounce) {
   const Oracle *o = F->o;
   const int d = (int)bounce;
   if (i == 0) F->nee_mask |= 1u << d;
-  if (!o->ss_quad_lights || o->n_lights < 2 || F->q0_iters < 0 || (F->q0_nee_mask & (1u << d)))
-    return o->light_index[i];
-  if (F->q0_nee_mask & ((1u << d) - 1u)) return 0;
-  return o->light_index[0];
+  if (!o->ss_quad_lights || o->n_lights < 2 || F->q0_iters < 0) return o->light_index[i];
+  const unsigned m = F->q0_nee_mask | (o->use_vol ? 0u : F->q0_nee_gmask);
+  if (m & (1u << d)) return o->light_index[i];
+  if (o->use_vol && !(m & ((1u << d) - 1u))) return o->light_index[0];
+  return 0;
 }
 static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *rd, v3 *mask, v3 *acc,
                  int *spec, float seed, float bounce) {
@@ -1292,7 +1297,6 @@ static void brdf(Frag *F, const Hit *hit, v3 f, v3 e, float inside, v3 *ro, v3 *
         if (idx >= 0) {
           v3 ls = calcDirectLighting(F, &o->meshes[idx], x, nl, base + 5681.123f + bounce * 7895.13f);
           *acc = add(*acc, mul(ls, *mask));
-          if (i < 2) { v3 t = mul(ls, *mask); F->dbg_sn[i] += t.x + t.y + t.z; }
         }
       }
     }
@@ -1343,6 +1347,10 @@ static void ghost_brdf(Frag *F, const BrdfRegs *g, float seed) {
     float nt_eff = (o->use_spectral && nt < 0.0f) ? spectralIOR(F->hero, fabsf(nt)) : fabsf(nt);
     spec = or_hash(seed) < schlick(g->rd, nl, 1.00029f, nt_eff);
   }
+  /* the plain light loop (constant trip count <= 4, no break/continue:
+   * unrolled, rule 5) runs in the ghost call too (SWIFTSHADER_QUAD_LIGHTS) */
+  if (!spec && o->sample_lights && !o->use_restir && !(o->use_mis && o->n_lights > 0) && o->n_lights <= 4)
+    F->nee_gmask |= 1u << F->cur_depth;
   if (spec || !o->sample_lights || !o->use_restir_def) return;
   if (o->use_restir && o->use_mis) {
     if (o->n_lights <= 8) return;
@@ -1378,6 +1386,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
   BrdfRegs regs; /* SWIFTSHADER_GHOST: brdf()'s parameter registers */
   regs.have = 0;
   for (int depth = 0; depth < o->max_bounces; ++depth) {
+    F->cur_depth = depth;
     F->n_iter++;
     F->last_depth = depth;
     F->dbg_hist = F->dbg_hist * 16.0f + (float)depth;
@@ -1413,9 +1422,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
             float den = 1.0f + g2 - 2.0f * VOL_G * ct;
             float phase = (1.0f - g2) / (FOUR_PI * den * sqrtf(den));
             float Tf = expf(-VOL_SIGMA_T * ts);
-            v3 term = muls(muls(muls(mul(mul(mask, lm->mat.c), lm->mat.e), phase), Tf), PI_F * omega);
-            acc = add(acc, term);
-            if (li < 2) F->dbg_in[li] += term.x + term.y + term.z;
+            acc = add(acc, muls(muls(muls(mul(mul(mask, lm->mat.c), lm->mat.e), phase), Tf), PI_F * omega));
           }
         }
         rd = sampleHG(rd, VOL_G, seed + 8293.7f + (float)depth * 773.3f);
@@ -1533,7 +1540,6 @@ static v3 shade_pixel(Frag *F, int px, int py) {
   F->first_scat = -1;
   F->dbg_hist = 0.0f;
   F->dbg_ev = 0.0f;
-  F->dbg_in[0] = F->dbg_in[1] = F->dbg_sn[0] = F->dbg_sn[1] = 0.0f;
   F->hero = 550.0f;
   float stx = 2.0f * fcx / rx - 1.0f, sty = 2.0f * fcy / ry - 1.0f;
   float aspect = rx / ry;
@@ -1814,24 +1820,20 @@ int or_render_frame(void *h, unsigned frame, float *out, const float *const *res
       memset(F.fr_pos, 0, sizeof F.fr_pos);
       memset(F.fr_col, 0, sizeof F.fr_col);
       F.q0_iters = -1;
-      F.nee_mask = 0;
+      F.nee_mask = F.nee_gmask = 0;
       if (o->ss_quad_lights && ((x | y) & 1)) {  /* the quad's first lane's path, rendered aside */
         Frag Q = F;
         const uint64_t q0 = Q.n_iter;
-        Q.nee_mask = 0;
+        Q.nee_mask = Q.nee_gmask = 0;
         (void)shade_pixel(&Q, x & ~1, y & ~1);
         F.q0_iters = (int)(Q.n_iter - q0);
         F.q0_nee_mask = Q.nee_mask;
+        F.q0_nee_gmask = Q.nee_gmask;
       }
       const uint64_t it0 = F.n_iter;
       v3 col = shade_pixel(&F, x, y);
       size_t p = ((size_t)y * o->w + x) * 4;
       out[p] = col.x; out[p + 1] = col.y; out[p + 2] = col.z; out[p + 3] = 0.0f;
-      if (o->dbg_paths == 2 && !o->use_restir_def && restir_main && restir_aux) {
-        restir_main[p] = F.dbg_in[0]; restir_main[p + 1] = F.dbg_in[1];
-        restir_main[p + 2] = F.dbg_sn[0]; restir_main[p + 3] = F.dbg_sn[1];
-        continue;
-      }
       if (o->dbg_paths && !o->use_restir_def && restir_main && restir_aux) {
         restir_main[p] = (float)(F.n_iter - it0); restir_main[p + 1] = F.dbg_hist;
         restir_main[p + 2] = (float)F.scat_ev; restir_main[p + 3] = (float)F.diff_b;
