@@ -119,6 +119,9 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_WALK_SPEC  // rt0_jit_walk postpones leaf tests until half the busy lanes hold one
 #define RT0_WALK_SPEC 1
 #endif
+#ifndef RT0_CLOSEST_SPEC  // bvh_closest tests leaves once half the walking lanes hold one (while-while)
+#define RT0_CLOSEST_SPEC 0
+#endif
 #ifndef RT0_BVH_STACK16  // BVH traversal stacks as 16-bit LDS entries + high bits in a register
 #define RT0_BVH_STACK16 0
 #endif
@@ -574,6 +577,70 @@ DEV int bvh4_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
 }
 #endif
 
+// bvh_closest with the leaf tests of the walking lanes gathered
+// (RT0_CLOSEST_SPEC; walk_body_spec's while-while scheme): a lane whose node
+// visit finds leaves holds them and visits no further node until the wave's
+// leaf phase, which runs once half the lanes still walking hold leaves (or
+// none can go on without testing its own).  Per lane the visits, the leaf
+// tests and every tmin they see are bvh_closest's, in the same order -- only
+// the wave's schedule changes -- so the hit is the same bit for bit.
+template <bool ANY>
+DEV int bvh_closest_spec(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
+  BvhStack stk;
+  int sp = 0, node = 0, best = -1, pa = -1, pb = -1;  // node -1: no node left; pa/pb: held leaves
+  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
+  const TriDev *__restrict__ tris = P.tris;
+  for (int guard = 2 * P.n_tris + 8;;) {
+    if (pa < 0 && node >= 0) {
+      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
+      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+      float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
+      float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
+      const int cl = lk.x, cr = lk.y;
+      if (tl != F_INF && cl < 0) {
+        pa = ~cl;
+        tl = F_INF;
+      }
+      if (tr != F_INF && cr < 0) {
+        if (pa < 0) pa = ~cr;
+        else pb = ~cr;
+        tr = F_INF;
+      }
+      if (tl != F_INF && tr != F_INF) {
+        const bool lfirst = tl <= tr;
+        stk.put(sp, lfirst ? cr : cl);
+        sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
+        node = lfirst ? cl : cr;
+      } else if (tl != F_INF) {
+        node = cl;
+      } else if (tr != F_INF) {
+        node = cr;
+      } else if (sp == 0) {
+        node = -1;
+      } else {
+        node = stk.get(--sp);
+      }
+      if (--guard <= 0) node = -1;  // a ray visits each node at most once: exit on a corrupt tree
+    }
+    const uint64_t walking = __ballot(1), lf = __ballot(pa >= 0), stuck = __ballot(pa >= 0 || node < 0);
+    if ((2 * __popcll(lf) >= __popcll(walking) || stuck == walking) && pa >= 0) {
+      float t;
+      if (tri_test(tris[pa], o, d, tmin, t)) {
+        tmin = t;
+        best = pa;
+      }
+      if (pb >= 0 && tri_test(tris[pb], o, d, tmin, t)) {
+        tmin = t;
+        best = pb;
+      }
+      pa = pb = -1;
+      if (ANY && best >= 0) break;
+    }
+    if (pa < 0 && node < 0) break;
+  }
+  return best;
+}
+
 // closest triangle hit along (o, d) before tmin: depth-first, nearer child
 // first, the far child on the per-lane LDS stack.  Returns the leaf-order
 // triangle index or -1; tmin is updated.  ANY: stop at the first hit before
@@ -588,6 +655,8 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
                     int budget = 0x7fffffff, bool *complete = nullptr) {
 #if RT0_BVH4
   if (!complete && !cnt) return bvh4_closest<ANY>(P, o, d, inv, tmin);
+#elif RT0_CLOSEST_SPEC
+  if (!complete && !cnt) return bvh_closest_spec<ANY>(P, o, d, inv, tmin);
 #endif
   BvhStack stk;
   int sp = 0, node = 0, best = -1;
