@@ -891,6 +891,62 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   return RT0_OK;
 }
 
+// A deferred ReSTIR pass as two row halves, each running pass -> nee -> walk
+// -> resolve on its own HIP stream.  Within a pass the halves are
+// independent -- every kernel reads the previous passes' reservoirs (rin) and
+// writes per pixel (accumulator, reservoirs, nee_out planes) or into its own
+// record / walk-job ranges -- so one half's kernels fill the other's tails;
+// the next pass starts after both (its spatial taps cross the seam).
+// RT0_RESTIR_SPLIT: 1 always, 0 never; default: scenes with triangle models
+// (the walk kernel's long glass walks leave tails: C5 2 089 vs 2 046
+// Msamples/s), not the quadric-only ones (C3 5 240 vs 5 975: its ~0.1 ms
+// kernels lose more to the halves' smaller grids than the tails cost).
+static bool restir_split_enabled(const rt0_ctx *c) {
+  const char *e = getenv("RT0_RESTIR_SPLIT");  // (read per render: tests switch it)
+  const int v = e ? atoi(e) : -1;
+  return v < 0 ? c->jit.walk != nullptr : v != 0;
+}
+static int restir_split_pass(rt0_ctx *c, const LaunchParams &p, dim3 grid) {
+  if (!c->wf_streams[0]) HIPCHK(c, hipStreamCreateWithFlags(&c->wf_streams[0], hipStreamNonBlocking));
+  if (!c->wf_fork) HIPCHK(c, hipEventCreateWithFlags(&c->wf_fork, hipEventDisableTiming));
+  if (!c->wf_join[0]) HIPCHK(c, hipEventCreateWithFlags(&c->wf_join[0], hipEventDisableTiming));
+  const hipStream_t st[2] = {c->stream, c->wf_streams[0]};
+  const unsigned ya = (grid.y + 1) / 2;  // tile rows of the first half
+  const long R = nee_regions_per_wave();
+  size_t wave0 = 0, nee_wave0 = 0;       // the half's first pass wave / light-sampling wave
+  HIPCHK(c, hipEventRecord(c->wf_fork, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(st[1], c->wf_fork, 0));
+  for (int h = 0; h < 2; h++) {
+    LaunchParams u = p;
+    const dim3 g(grid.x, h == 0 ? ya : grid.y - ya);
+    u.vp_y0 = p.vp_y0 + (h == 0 ? 0 : (int)ya * 16);
+    u.vp_y1 = h == 0 ? std::min(p.vp_y1, p.vp_y0 + (int)ya * 16) : p.vp_y1;
+    const size_t waves = (size_t)g.x * g.y * 4, nee_waves = (waves + R - 1) / R;
+    u.nee_regions = (int32_t)waves;
+    u.nee_rec = p.nee_rec + wave0 * (size_t)p.nee_cap;
+    u.nee_count = p.nee_count + wave0;
+    if (c->jit.walk) {
+      u.walk_jobs = p.walk_jobs + nee_wave0 * 2 * (size_t)R * (size_t)p.nee_cap;
+      u.walk_count = p.walk_count + nee_wave0;
+      u.walk_res = p.walk_res + 2 * wave0 * (size_t)p.nee_cap;
+      u.walk_waves = (int32_t)nee_waves;
+    }
+    HIPCHK(c, hipMemsetAsync(u.nee_count, 0, waves * sizeof(uint32_t), st[h]));
+    auto go = [&](void *fn, unsigned gx, unsigned gy) {
+      return rt0h::jit_launch(fn, &u, gx, gy, 1, st[h]) == RT0_OK ? hipSuccess : hipErrorLaunchFailure;
+    };
+    HIPCHK(c, go(c->jit.pass, g.x, g.y));
+    HIPCHK(c, go(c->jit.nee, (unsigned)((nee_waves + 3) / 4), 1));
+    if (c->jit.walk) HIPCHK(c, go(c->jit.walk, (unsigned)((nee_waves + 3) / 4), 1));
+    HIPCHK(c, go(c->jit.resolve, g.x, g.y));
+    wave0 += waves;
+    nee_wave0 += nee_waves;
+  }
+  HIPCHK(c, hipEventRecord(c->wf_join[0], st[1]));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->wf_join[0], 0));
+  return RT0_OK;
+}
+
 static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sync) {
   if (!c || n < 0) return RT0_E_ARG;
   if (!c->has_scene) return fail(c, RT0_E_STATE, "rt0_render before rt0_set_scene*");
@@ -1024,7 +1080,8 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     p.nee_n = c->d_nee_n;
     if (c->jit.walk) {
       // per light-sampling wave: up to two rays per record of its regions
-      const size_t waves = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave();
+      // (+1: the two halves of a split pass round their wave counts up apart)
+      const size_t waves = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave() + 1;
       const size_t jobs = waves * 2 * (size_t)nee_regions_per_wave() * (size_t)p.nee_cap;
       if (jobs > c->walk_jobs_n || 2 * slots > c->walk_res_n || waves > c->walk_waves_n) {
         for (void **q : {(void **)&c->d_walk_jobs, (void **)&c->d_walk_count, (void **)&c->d_walk_res}) {
@@ -1052,6 +1109,9 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   if (c->counting) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, RT0_N_COUNTERS * sizeof(unsigned long long), c->stream));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   int launches = 0;
+  // two row halves per deferred ReSTIR pass (not with the wavefront rounds,
+  // which split their own work)
+  const bool split = restir && defer && !wf_run && restir_split_enabled(c) && grid.y >= 2;
   if (restir) {
     for (int k = 0; k < n; k++) {
       p.frame0 = first + (uint32_t)k;
@@ -1064,7 +1124,12 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       p.rin[5] = c->d_restir[R_H2A];
       p.rout_main = c->d_restir[R_OUT_MAIN];
       p.rout_aux = c->d_restir[R_OUT_AUX];
-      if (defer) {
+      if (defer && split) {
+        // the pass as two row halves on two streams (restir_split_enabled)
+        int rc = restir_split_pass(c, p, grid);
+        if (rc != RT0_OK) return rc;
+        launches++;
+      } else if (defer) {
         // waves wholly outside the viewport write no count
         HIPCHK(c, hipMemsetAsync(c->d_nee_count, 0, pass_waves * sizeof(uint32_t), c->stream));
         if (wf_run) {  // the pass's paths as wavefront rounds (shade + closest-hit walk)

@@ -201,3 +201,39 @@ def test_deferral_off_beyond_packed_call_index(cfgs, gpu_required):
         out.append(r.read_accum())
     assert np.isfinite(out[0]).all()
     assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,size,viewport", [("c5_spectral_models", (64, 80), None),
+                                                ("c3_outdoor_restir", (64, 48), None),
+                                                ("c3_outdoor_restir", (64, 64), (8, 5, 40, 50))])
+def test_split_pass_is_bit_identical(name, size, viewport, cfgs, monkeypatch, gpu_required):
+    """A deferred ReSTIR pass as two row halves on two streams
+    (rt0_host.cpp restir_split_pass; default for scenes with models) gives
+    the unsplit pass's samples and reservoirs bit for bit: the halves only
+    change which wave holds a record.  An odd number of 16-row tile rows, and
+    a viewport whose rows are not a multiple of 16."""
+    import test_models as T
+    cfg = T.cfg_by_name(cfgs, name)
+    out = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("RT0_RESTIR_SPLIT", split)
+        if name == "c3_outdoor_restir":
+            r = rt0.Renderer(*size)
+            configure(r, cfg, cfgs)
+        else:
+            r = T.make(cfg, cfgs, *size)
+        if viewport:
+            r.set_viewport(*viewport)
+        S, M, A = [], [], []
+        for k in range(1, 5):
+            r.render(k, 1)
+            S.append(r.read_accum())
+            m, a = r.read_restir(0)
+            M.append(m)
+            A.append(a)
+        out.append((np.stack(S), np.stack(M), np.stack(A)))
+        r.close()
+    for x, y in zip(out[0], out[1]):
+        assert np.array_equal(x, y)
+    assert out[1][0][..., :3].mean() > 0.0
