@@ -50,6 +50,16 @@ if [ "${CALIB:-0}" = "1" ]; then
   rc=$?; echo "valu peak rc=$rc"; cat "$O/valu_peak.json"; stop_if_bad $rc
 fi
 
+# dispatches per kernel per ReSTIR pass: 2 where librt0 splits the pass into
+# row halves (rt0_host.cpp restir_split_enabled: scenes with models, i.e. c5,
+# unless RT0_RESTIR_SPLIT says otherwise)
+halves() {
+  if [ -n "${RT0_RESTIR_SPLIT:-}" ]; then
+    { [ "$RT0_RESTIR_SPLIT" != "0" ] && [ "$1" = "c3" -o "$1" = "c5" ]; } && echo 2 || echo 1
+  else
+    [ "$1" = "c5" ] && echo 2 || echo 1
+  fi
+}
 for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do
   if [ "${BENCH:-1}" = "1" ]; then
     extra=""; [ "$cfg" = "c2" ] && extra="--secondary"
@@ -61,7 +71,7 @@ for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$cfg" -o run -- \
       python bench.py --config $cfg --steps $STEPS --warmup $WARMUP --no-cpu-baseline --no-secondary > "$O/prof_$cfg.json" 2> "$O/prof_$cfg.err"
     rc=$?; echo "kernel trace $cfg rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$O/prof_$cfg.err"; exit $rc; }
-    python3 scripts/kt_summary.py "$O/kt_$cfg.json" "$O/kt_$cfg" $skip
+    HALVES=$(halves $cfg) python3 scripts/kt_summary.py "$O/kt_$cfg.json" "$O/kt_$cfg" $skip
     find "$O/kt_$cfg" -name "*kernel_stats.csv" -exec cp {} "$O/kernel_stats_$cfg.csv" \;
     rm -rf "$O/kt_$cfg"
   fi
@@ -79,7 +89,7 @@ for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do
       [ $rc -ne 0 ] && { tail -5 "$O/pmc_${cfg}_$i.log"; exit $rc; }
       dirs="$dirs $O/pmc_${cfg}_$i"
     done
-    python3 scripts/pmc_summary.py "$O/pmc_$cfg.json" ${WH[$cfg]} ${BPP[$cfg]} ${LPS[$cfg]} $dirs
+    HALVES=$(halves $cfg) python3 scripts/pmc_summary.py "$O/pmc_$cfg.json" ${WH[$cfg]} ${BPP[$cfg]} ${LPS[$cfg]} $dirs
     rm -rf $dirs
   fi
 done

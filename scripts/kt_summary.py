@@ -2,15 +2,17 @@
 """Steady-state kernel time of the pass kernel from a rocprofv3 --kernel-trace
 run of bench.py (scripts/gpu_measure.sh).
 
-    kt_summary.py OUT.json TRACE_DIR SKIP
+    [HALVES=2] kt_summary.py OUT.json TRACE_DIR SKIP
 
 Keeps the rt0_jit_pass dispatches after the first SKIP (the warm-up step's
 launches) and reports their median / mean / min / max duration, plus the other
 kernels' totals (rocprofv3's own --stats table averages every dispatch,
 warm-up included).  A deferred ReSTIR pass is three dispatches (rt0_jit_pass,
 rt0_jit_nee, rt0_jit_resolve; rt0_integrator.h), four in scenes with models
-(+ rt0_jit_walk): their kept medians are reported per kernel and "median_ms"
-.. "max_ms" are then per pass, the kernels' durations summed pass by pass.
+(+ rt0_jit_walk), twice when the pass runs as two row halves on two streams
+(restir_split_pass): "median_ms" .. "max_ms" are then per pass, each pass's
+span (first dispatch start to last end), and the per-kernel medians its busy
+time per pass.
 Wavefront launches (rt0_jit_wf_*: shade, plan and march or walk per round)
 are summed launch by launch with what completes them: rt0_sum_kernel, or a
 ReSTIR pass's nee (+ walk) + resolve.
@@ -18,6 +20,7 @@ ReSTIR pass's nee (+ walk) + resolve.
 import csv
 import glob
 import json
+import os
 import statistics
 import sys
 from collections import defaultdict
@@ -35,6 +38,7 @@ TAIL = ("rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve")
 
 def main():
     out, d, skip = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    halves = int(os.environ.get("HALVES", "1"))
     rows = []
     for fn in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
         rows += list(csv.DictReader(open(fn)))
@@ -68,11 +72,27 @@ def main():
                       for k in per if nl > skip}
         per_kernel.update({k: statistics.median(v[skip:nl]) / 1e6 for k, v in tail.items() if nl > skip})
         per_kernel["dispatches_per_launch"] = per
-    elif dur["rt0_jit_nee"]:  # deferred passes: pass + nee (+ walk) + resolve, one of each per pass
-        ks = [k for k in GROUP if dur[k]]
-        n = min(len(dur[k]) for k in ks)
-        pas = [sum(dur[k][i] for k in ks) for i in range(n)]
-        per_kernel = {k: statistics.median(v[skip:]) / 1e6 for k, v in dur.items() if v[skip:]}
+    elif dur["rt0_jit_nee"]:  # deferred passes: pass + nee (+ walk) + resolve per pass, or per half
+        # A pass is one rt0_jit_pass dispatch, or two when it runs as two row
+        # halves on two streams (rt0_host.cpp restir_split_pass; they
+        # overlap): env HALVES = 2 (scripts/gpu_measure.sh sets it); a pass's
+        # time is its span, first start to last end; per kernel: its busy
+        # time per pass (halves summed)
+        groups, seen = [], 0
+        for r in rows:
+            name = r["Kernel_Name"].strip()
+            if name not in GROUP:
+                continue
+            if name == KERNEL:
+                if seen % halves == 0:
+                    groups.append([])
+                seen += 1
+            if groups:
+                groups[-1].append((name, float(r["Start_Timestamp"]), float(r["End_Timestamp"])))
+        pas = [max(g[2] for g in gr) - min(g[1] for g in gr) for gr in groups]
+        per_kernel = {k: statistics.median([sum(g[2] - g[1] for g in gr if g[0] == k) for gr in groups[skip:]]) / 1e6
+                      for k in GROUP if dur[k] and groups[skip:]}
+        per_kernel["dispatches_per_pass"] = {k: sum(1 for g in groups[-1] if g[0] == k) for k in GROUP if dur[k]}
     kept = pas[skip:]
     other = defaultdict(list)
     for r in rows:
