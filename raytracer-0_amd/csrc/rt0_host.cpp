@@ -897,30 +897,38 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
 // writes per pixel (accumulator, reservoirs, nee_out planes) or into its own
 // record / walk-job ranges -- so one half's kernels fill the other's tails;
 // the next pass starts after both (its spatial taps cross the seam).
-// RT0_RESTIR_SPLIT: 1 always, 0 never; default: scenes with triangle models
+// RT0_RESTIR_SPLIT: 0 never, 1 two halves, K (<= 4) K row parts; default:
+// three parts for scenes with triangle models (C5: 2 parts 2 084-2 088, 3
+// parts 2 135-2 138, 4 parts 2 017 Msamples/s)
 // (the walk kernel's long glass walks leave tails: C5 2 089 vs 2 046
 // Msamples/s), not the quadric-only ones (C3 5 240 vs 5 975: its ~0.1 ms
 // kernels lose more to the halves' smaller grids than the tails cost).
-static bool restir_split_enabled(const rt0_ctx *c) {
+// (RT0_RESTIR_SPLIT = K >= 2: K row parts on K streams, at most 4)
+static int restir_split_parts(const rt0_ctx *c) {
   const char *e = getenv("RT0_RESTIR_SPLIT");  // (read per render: tests switch it)
   const int v = e ? atoi(e) : -1;
-  return v < 0 ? c->jit.walk != nullptr : v != 0;
+  return v < 0 ? (c->jit.walk != nullptr ? 3 : 1) : std::max(1, std::min(4, v == 1 ? 2 : v));
 }
-static int restir_split_pass(rt0_ctx *c, const LaunchParams &p, dim3 grid) {
-  if (!c->wf_streams[0]) HIPCHK(c, hipStreamCreateWithFlags(&c->wf_streams[0], hipStreamNonBlocking));
+static int restir_split_pass(rt0_ctx *c, const LaunchParams &p, dim3 grid, int K) {
+  K = std::max(2, std::min(K, std::min(4, (int)grid.y)));
+  for (int k = 0; k < K - 1; k++) {
+    if (!c->wf_streams[k]) HIPCHK(c, hipStreamCreateWithFlags(&c->wf_streams[k], hipStreamNonBlocking));
+    if (!c->wf_join[k]) HIPCHK(c, hipEventCreateWithFlags(&c->wf_join[k], hipEventDisableTiming));
+  }
   if (!c->wf_fork) HIPCHK(c, hipEventCreateWithFlags(&c->wf_fork, hipEventDisableTiming));
-  if (!c->wf_join[0]) HIPCHK(c, hipEventCreateWithFlags(&c->wf_join[0], hipEventDisableTiming));
-  const hipStream_t st[2] = {c->stream, c->wf_streams[0]};
-  const unsigned ya = (grid.y + 1) / 2;  // tile rows of the first half
+  const hipStream_t st[4] = {c->stream, c->wf_streams[0], c->wf_streams[1], c->wf_streams[2]};
   const long R = nee_regions_per_wave();
   size_t wave0 = 0, nee_wave0 = 0;       // the half's first pass wave / light-sampling wave
   HIPCHK(c, hipEventRecord(c->wf_fork, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(st[1], c->wf_fork, 0));
-  for (int h = 0; h < 2; h++) {
+  for (int h = 1; h < K; h++) HIPCHK(c, hipStreamWaitEvent(st[h], c->wf_fork, 0));
+  unsigned y0 = 0;  // the part's first tile row
+  for (int h = 0; h < K; h++) {
     LaunchParams u = p;
-    const dim3 g(grid.x, h == 0 ? ya : grid.y - ya);
-    u.vp_y0 = p.vp_y0 + (h == 0 ? 0 : (int)ya * 16);
-    u.vp_y1 = h == 0 ? std::min(p.vp_y1, p.vp_y0 + (int)ya * 16) : p.vp_y1;
+    const unsigned y1 = (unsigned)(((size_t)grid.y * (h + 1)) / K);  // tile rows [y0, y1)
+    const dim3 g(grid.x, y1 - y0);
+    u.vp_y0 = p.vp_y0 + (int)y0 * 16;
+    u.vp_y1 = h == K - 1 ? p.vp_y1 : p.vp_y0 + (int)y1 * 16;
+    y0 = y1;
     const size_t waves = (size_t)g.x * g.y * 4, nee_waves = (waves + R - 1) / R;
     u.nee_regions = (int32_t)waves;
     u.nee_rec = p.nee_rec + wave0 * (size_t)p.nee_cap;
@@ -942,8 +950,10 @@ static int restir_split_pass(rt0_ctx *c, const LaunchParams &p, dim3 grid) {
     wave0 += waves;
     nee_wave0 += nee_waves;
   }
-  HIPCHK(c, hipEventRecord(c->wf_join[0], st[1]));
-  HIPCHK(c, hipStreamWaitEvent(c->stream, c->wf_join[0], 0));
+  for (int h = 1; h < K; h++) {
+    HIPCHK(c, hipEventRecord(c->wf_join[h - 1], st[h]));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->wf_join[h - 1], 0));
+  }
   return RT0_OK;
 }
 
@@ -1080,8 +1090,8 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     p.nee_n = c->d_nee_n;
     if (c->jit.walk) {
       // per light-sampling wave: up to two rays per record of its regions
-      // (+1: the two halves of a split pass round their wave counts up apart)
-      const size_t waves = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave() + 1;
+      // (+3: the up to 4 parts of a split pass round their wave counts up apart)
+      const size_t waves = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave() + 3;
       const size_t jobs = waves * 2 * (size_t)nee_regions_per_wave() * (size_t)p.nee_cap;
       if (jobs > c->walk_jobs_n || 2 * slots > c->walk_res_n || waves > c->walk_waves_n) {
         for (void **q : {(void **)&c->d_walk_jobs, (void **)&c->d_walk_count, (void **)&c->d_walk_res}) {
@@ -1111,7 +1121,8 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   int launches = 0;
   // two row halves per deferred ReSTIR pass (not with the wavefront rounds,
   // which split their own work)
-  const bool split = restir && defer && !wf_run && restir_split_enabled(c) && grid.y >= 2;
+  const int split_parts = restir && defer && !wf_run ? restir_split_parts(c) : 1;
+  const bool split = split_parts > 1 && grid.y >= 2;
   if (restir) {
     for (int k = 0; k < n; k++) {
       p.frame0 = first + (uint32_t)k;
@@ -1126,7 +1137,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       p.rout_aux = c->d_restir[R_OUT_AUX];
       if (defer && split) {
         // the pass as two row halves on two streams (restir_split_enabled)
-        int rc = restir_split_pass(c, p, grid);
+        int rc = restir_split_pass(c, p, grid, split_parts);
         if (rc != RT0_OK) return rc;
         launches++;
       } else if (defer) {

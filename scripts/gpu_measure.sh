@@ -50,14 +50,15 @@ if [ "${CALIB:-0}" = "1" ]; then
   rc=$?; echo "valu peak rc=$rc"; cat "$O/valu_peak.json"; stop_if_bad $rc
 fi
 
-# dispatches per kernel per ReSTIR pass: 2 where librt0 splits the pass into
-# row halves (rt0_host.cpp restir_split_enabled: scenes with models, i.e. c5,
-# unless RT0_RESTIR_SPLIT says otherwise)
+# dispatches per kernel per ReSTIR pass: K where librt0 splits the pass into
+# K row parts (rt0_host.cpp restir_split_parts: 3 for scenes with models, i.e.
+# c5, unless RT0_RESTIR_SPLIT says otherwise)
 halves() {
   if [ -n "${RT0_RESTIR_SPLIT:-}" ]; then
-    { [ "$RT0_RESTIR_SPLIT" != "0" ] && [ "$1" = "c3" -o "$1" = "c5" ]; } && echo 2 || echo 1
+    k=$RT0_RESTIR_SPLIT; [ "$k" = "1" ] && k=2; [ "$k" -gt 4 ] && k=4
+    { [ "$k" != "0" ] && [ "$1" = "c3" -o "$1" = "c5" ]; } && echo $k || echo 1
   else
-    [ "$1" = "c5" ] && echo 2 || echo 1
+    [ "$1" = "c5" ] && echo 3 || echo 1
   fi
 }
 for cfg in ${CONFIGS:-c2 c1 c3 c4 c5}; do

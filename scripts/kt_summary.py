@@ -2,14 +2,14 @@
 """Steady-state kernel time of the pass kernel from a rocprofv3 --kernel-trace
 run of bench.py (scripts/gpu_measure.sh).
 
-    [HALVES=2] kt_summary.py OUT.json TRACE_DIR SKIP
+    [HALVES=K] kt_summary.py OUT.json TRACE_DIR SKIP
 
 Keeps the rt0_jit_pass dispatches after the first SKIP (the warm-up step's
 launches) and reports their median / mean / min / max duration, plus the other
 kernels' totals (rocprofv3's own --stats table averages every dispatch,
 warm-up included).  A deferred ReSTIR pass is three dispatches (rt0_jit_pass,
 rt0_jit_nee, rt0_jit_resolve; rt0_integrator.h), four in scenes with models
-(+ rt0_jit_walk), twice when the pass runs as two row halves on two streams
+(+ rt0_jit_walk), twice when the pass runs as two row parts on K streams
 (restir_split_pass): "median_ms" .. "max_ms" are then per pass, each pass's
 span (first dispatch start to last end), and the per-kernel medians its busy
 time per pass.
@@ -75,7 +75,7 @@ def main():
     elif dur["rt0_jit_nee"]:  # deferred passes: pass + nee (+ walk) + resolve per pass, or per half
         # A pass is one rt0_jit_pass dispatch, or two when it runs as two row
         # halves on two streams (rt0_host.cpp restir_split_pass; they
-        # overlap): env HALVES = 2 (scripts/gpu_measure.sh sets it); a pass's
+        # overlap): env HALVES = K (scripts/gpu_measure.sh sets it); a pass's
         # time is its span, first start to last end; per kernel: its busy
         # time per pass (halves summed)
         groups, seen = [], 0

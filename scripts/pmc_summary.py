@@ -8,7 +8,7 @@ Per dispatch of rt0_jit_pass (the counting instance bench.py launches
 afterwards is a different kernel and is excluded), dropping the first SKIP
 dispatches (the warm-up step), averaged over the rest -- for a deferred ReSTIR
 pass (rt0_jit_pass + rt0_jit_nee [+ rt0_jit_walk] + rt0_jit_resolve, each
-once per pass or, split into two row halves, twice) the kernels' dispatches
+once per pass or, split into K row parts, twice) the kernels' dispatches
 summed per pass:
   * HBM traffic: FETCH_SIZE x 2 (MI355X_MICROARCH.md: gfx950 reports half the
     bytes of a 16-B/lane streaming read; scripts/fetch_calib.hip measures the
@@ -83,7 +83,7 @@ def main():
             if kernel in WF and nl > skip:
                 per_launch = max(1, len(every) // nl)
             elif kernel not in WF:
-                # env HALVES = 2: ReSTIR passes split into two row halves
+                # env HALVES = K: ReSTIR passes split into K row parts
                 # (rt0_host.cpp restir_split_pass) dispatch each kernel twice
                 per_launch = int(os.environ.get("HALVES", "1"))
             ids = every[skip * per_launch:]

@@ -216,7 +216,7 @@ def test_split_pass_is_bit_identical(name, size, viewport, cfgs, monkeypatch, gp
     import test_models as T
     cfg = T.cfg_by_name(cfgs, name)
     out = []
-    for split in ("0", "1"):
+    for split in ("0", "1", "3"):
         monkeypatch.setenv("RT0_RESTIR_SPLIT", split)
         if name == "c3_outdoor_restir":
             r = rt0.Renderer(*size)
@@ -234,6 +234,7 @@ def test_split_pass_is_bit_identical(name, size, viewport, cfgs, monkeypatch, gp
             A.append(a)
         out.append((np.stack(S), np.stack(M), np.stack(A)))
         r.close()
-    for x, y in zip(out[0], out[1]):
-        assert np.array_equal(x, y)
+    for o in out[1:]:
+        for x, y in zip(out[0], o):
+            assert np.array_equal(x, y)
     assert out[1][0][..., :3].mean() > 0.0
