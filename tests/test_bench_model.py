@@ -114,3 +114,39 @@ def test_kt_summary_wavefront_launch_is_its_span(tmp_path):
     assert res["kept"] == 1 and res["median_ms"] == pytest.approx(7.2, abs=1e-6)
     # the per-kernel busy sums still count both halves
     assert res["per_kernel_median_ms"]["rt0_jit_wf_march"] == pytest.approx(7.8, abs=1e-6)
+
+
+def test_kt_summary_split_restir_pass_is_its_span(tmp_path):
+    """scripts/kt_summary.py with HALVES=3 on a synthetic trace of deferred
+    ReSTIR passes split into three row parts on three streams (rt0_host.cpp
+    restir_split_pass): a pass is its three parts' pass/nee/walk/resolve
+    dispatches, its time their span; per kernel the parts' busy time summed;
+    the warm-up pass is skipped."""
+    import csv
+    import json
+    import subprocess
+    rows = []
+
+    def k(name, t0, t1):
+        rows.append({"Kernel_Name": name, "Start_Timestamp": str(int(t0 * 1e6)), "End_Timestamp": str(int(t1 * 1e6))})
+
+    for base in (0.0, 10.0, 20.0):  # three passes, ms; parts start 0.2 ms apart and overlap
+        for h in range(3):
+            t = base + 0.2 * h
+            k("rt0_jit_pass", t, t + 3.0)
+            k("rt0_jit_nee", t + 3.0, t + 5.0)
+            k("rt0_jit_walk", t + 5.0, t + 6.0)
+            k("rt0_jit_resolve", t + 6.0, t + 6.5)
+    d = tmp_path / "trace"
+    d.mkdir()
+    with open(d / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    out = tmp_path / "kt.json"
+    subprocess.run([sys.executable, os.path.join(REPO, "scripts", "kt_summary.py"), str(out), str(d), "1"],
+                   check=True, capture_output=True, env=dict(os.environ, HALVES="3"))
+    res = json.load(open(out))
+    assert res["kept"] == 2 and res["median_ms"] == pytest.approx(6.9, abs=1e-6)
+    assert res["per_kernel_median_ms"]["rt0_jit_pass"] == pytest.approx(9.0, abs=1e-6)
+    assert res["per_kernel_median_ms"]["dispatches_per_pass"]["rt0_jit_resolve"] == 3
