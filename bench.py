@@ -18,11 +18,14 @@ runs under it; WORLD_SIZE must equal --gpus.  One process per GPU:
     dealt round-robin over ranks (rt0_set_shard); each rank renders its bands
     straight into a band-packed torch buffer (rt0_set_accum_buffer_compact:
     the RCCL send buffer as it stands), and rank 0 gathers the bands over RCCL
-    into one preallocated buffer and reorders them with one index_copy_.  By
-    default a step at N GPUs renders N x spp passes ("weak" scaling: every
-    rank renders its 1/N of the rows for all of them, the per-GPU work of N =
-    1; C4 at N = 8 is then the 64-spp render BASELINE.md quotes);
-    `--scaling strong` splits the N = 1 step N ways instead;
+    into one preallocated buffer and reorders them with one index_copy_.
+    Each workload names its scaling (workloads.json): C1/C2 "strong" -- a
+    step is the N = 1 job split N ways (C2: BASELINE's fixed 1024^2 x 64 spp);
+    C4 "weak" -- a step at N GPUs renders N x spp passes, every rank its 1/N
+    of the rows for all of them (C4 at N = 8 is the 64-spp render BASELINE.md
+    quotes).  At N > 1 the other mode's job is timed after the primary one and
+    reported as secondary_<mode>_Msamples_s (config.job / secondary_job say
+    which job each number is); `--scaling` overrides the primary mode;
   * ReSTIR workloads (C3, C5): two round-robin row bands per rank
     (shard.interleaved_band), a halo exchange of the newest reservoir planes
     at every band boundary after every pass (RCCL point-to-point,
@@ -544,11 +547,14 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N>1: nccl = RCCL over xGMI; gloo = every transfer staged through host memory")
     ap.add_argument("--save-image", default=None, help="rank 0: np.save the last step's HDR image (H x W x 4)")
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
-                    help="progressive workloads (C1, C2, C4) at N GPUs: weak = a step renders N x spp passes, each "
-                         "rank its 1/N of the rows for all of them (per-GPU work fixed; C4 at N = 8 is the 64-spp "
-                         "job BASELINE.md quotes); strong = spp passes split N ways.  ReSTIR workloads are always "
-                         "strong (each pass reads the previous pass's reservoirs).")
+    ap.add_argument("--scaling", default=None, choices=("weak", "strong"),
+                    help="progressive workloads (C1, C2, C4) at N GPUs: strong = the N = 1 step's spp passes split "
+                         "N ways (the fixed job: C2's 1024^2 x 64 spp of BASELINE's metric); weak = a step renders "
+                         "N x spp passes, each rank its 1/N of the rows for all of them (per-GPU work fixed; C4 at "
+                         "N = 8 is the 64-spp job BASELINE.md quotes).  Default: the workload's `scaling` "
+                         "(workloads.json: C1/C2 strong, C4 weak); at N > 1 the other one is timed after it and "
+                         "reported as secondary_<mode>_Msamples_s.  ReSTIR workloads are always strong (each pass "
+                         "reads the previous pass's reservoirs).")
     ap.add_argument("--spp", type=int, default=None, help="passes per step at N = 1 (default: the workload's)")
     args = ap.parse_args()
 
@@ -576,34 +582,57 @@ def main():
     W, H = wl["width"], wl["height"]
 
     base_spp = args.spp or wl["spp"]
-    weak = not workloads.restir(wl) and args.scaling == "weak"
+    mode = "strong" if workloads.restir(wl) else (args.scaling or wl.get("scaling", "strong"))
+    weak = mode == "weak"
     step_spp = base_spp * world if weak else base_spp  # passes per step over the whole image
     wl = dict(wl, spp=step_spp)
-    job = (Restir if workloads.restir(wl) else Progressive)(rt0, torch, wl, rank, world, local, staged=staged)
-    job.r.set_jit(bool(args.jit))
-    job.r.set_executor_compat(args.executor_compat)
-    for i in range(args.warmup):
-        job.step(i)
-    job.kernel_ms.clear()
-    job.gather_ms.clear()
+
+    def make_job(w):
+        j = (Restir if workloads.restir(w) else Progressive)(rt0, torch, w, rank, world, local, staged=staged)
+        j.r.set_jit(bool(args.jit))
+        j.r.set_executor_compat(args.executor_compat)
+        return j
+
+    def timed(j, clock=None):
+        """W untimed steps, then K steps between a barrier + device-wide
+        synchronize on both sides; the max over ranks of the timed span."""
+        for i in range(args.warmup):
+            j.step(i)
+        j.kernel_ms.clear()
+        j.gather_ms.clear()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if clock:
+            clock.start()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            j.step(args.warmup + i)
+        torch.cuda.synchronize()  # device-wide: librt0's stream included
+        if dist:
+            dist.barrier()
+        span = time.perf_counter() - t0
+        if clock:
+            clock.stop()
+        j.collect()  # the last timed step's kernel time, read outside the timed region
+        if dist:
+            t = torch.tensor([span], device="cuda:%d" % local) if not staged else torch.tensor([span])
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            span = float(t.item())
+        return span
+
+    job = make_job(wl)
     clock = ClockSampler(torch, local)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    clock.start()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        job.step(args.warmup + i)
-    torch.cuda.synchronize()  # device-wide: librt0's stream included
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    clock.stop()
-    job.collect()  # the last timed step's kernel time, read outside the timed region
-    if dist:
-        t = torch.tensor([dt], device="cuda:%d" % local) if not staged else torch.tensor([dt])
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = timed(job, clock)
+    # N > 1, progressive: the other scaling mode's job after the primary one,
+    # every rank, so a SCALE record holds both the fixed job and the per-GPU one
+    second = None
+    if world > 1 and not workloads.restir(wl):
+        mode2 = "strong" if weak else "weak"
+        wl2 = dict(wl, spp=base_spp * world if mode2 == "weak" else base_spp)
+        job2 = make_job(wl2)
+        dt2 = timed(job2)
+        second = (mode2, wl2, job2, W * H * wl2["spp"] * args.steps / dt2 / 1e6)
     ms_per_step = dt * 1000.0 / args.steps
     total_samples = W * H * wl["spp"] * args.steps  # every rank's share: the whole image
     value = total_samples / dt / 1e6
@@ -613,6 +642,9 @@ def main():
         return
     if args.save_image:
         np.save(args.save_image, job.final_image().cpu().numpy()[:H])
+        if second:
+            root, ext = os.path.splitext(args.save_image)
+            np.save(root + "_secondary" + (ext or ".npy"), second[2].final_image().cpu().numpy()[:H])
 
     first_timed = 1 + args.warmup * wl["spp"]
     cnt = count_events(rt0, wl, local, first_timed, args.executor_compat)
@@ -701,6 +733,15 @@ def main():
     if wl.get("baseline_spp") and wl["baseline_spp"] != wl["spp"]:
         out["config"]["spp_note"] = ("BASELINE.md quotes this config at %d spp; one bench step renders %d passes "
                                      "(Msamples/s is per sample either way)" % (wl["baseline_spp"], wl["spp"]))
+    out["config"]["job"] = ("%dx%d x %d spp per step over %d GPU(s) (%s scaling: %s)"
+                            % (W, H, wl["spp"], world, "weak" if weak else "strong",
+                               "per-GPU work of the N = 1 step" if weak else "the N = 1 step's job split N ways"))
+    if second:
+        mode2, wl2, _, v2 = second
+        out["secondary_%s_Msamples_s" % mode2] = round(v2, 3)
+        out["config"]["secondary_job"] = ("%dx%d x %d spp per step over %d GPUs (%s scaling), timed after the "
+                                          "primary job with the same steps / warmup"
+                                          % (W, H, wl2["spp"], world, mode2))
     out["gpu_clock"] = clock.report()
     if job.gather_ms:
         out["gather_ms_per_step"] = round(float(np.mean(job.gather_ms)), 3)

@@ -144,7 +144,7 @@ int rt0_obj_read(const char *path, float **positions, int *n_vertices, int32_t *
  * unit 0..3 = TEXTURE0..3, RT0_TEX_NOISE = the noise texture.  rgba8: w*h RGBA
  * bytes, first row = the image's top row (WebGL's upload without FLIP_Y puts
  * it at t = 0); sampled GL_LINEAR with GL_REPEAT at level 0 like the
- * reference.  rgba8 = NULL unbinds the unit (an unbound unit samples
+ * reference, by the filter rt0_set_texture_filter selects.  rgba8 = NULL unbinds the unit (an unbound unit samples
  * (0,0,0,1), the GL value of an incomplete texture).  Copied to the device;
  * the caller keeps ownership. */
 #define RT0_TEX_NOISE 4
@@ -298,11 +298,22 @@ int rt0_set_jit(rt0_ctx *ctx, int enable);
  * 1 = reproduce it (the reservoir chain then matches the reference executor
  * pass after pass); 0 (default) = GLSL semantics.  Radiance of a pass is the
  * same either way; only the reservoirs the next passes read differ.
- * 1 also fetches the RGBA8 asset textures (u_tex0..3, u_rnd_tex) through the
- * executor's fixed-point bilinear filter (16-bit coordinate fraction, 16-bit
- * tap weights; oracle/gen/tex_kat.py measures it, bit-exact on power-of-two
- * sizes) instead of exact fp32 bilinear. */
+ * (The texture filter is its own switch, rt0_set_texture_filter.) */
 int rt0_set_executor_compat(rt0_ctx *ctx, int enable);
+/* GL_LINEAR filtering of the RGBA8 asset textures (u_tex0..3) and the noise
+ * texture (u_rnd_tex), getTexel and value_noise / voronoi (raytracer.glsl:
+ * 393-433, 726-772) on the textures of loadTexture (index.js:699-728).  GLSL
+ * leaves the filter's precision to the implementation; GPU texture units,
+ * like the reference's executor, filter in fixed point.
+ *   RT0_TEX_FILTER_FIXED16 (default): the reference executor's filter -- the
+ *     coordinate as a 16-bit fraction, a 16.16 texel position, texels widened
+ *     to 16 bits, 16-bit tap weights (oracle/gen/tex_kat.py known-answer
+ *     shaders; bit-exact on power-of-two textures, every reference asset);
+ *   RT0_TEX_FILTER_FLOAT: exact fp32 bilinear.
+ * The cubemap is filtered in fp32 either way (the executor does too). */
+#define RT0_TEX_FILTER_FLOAT 0
+#define RT0_TEX_FILTER_FIXED16 1
+int rt0_set_texture_filter(rt0_ctx *ctx, int mode);
 /* Deferred ReSTIR light sampling (scene-specialised kernels): a pass runs its
  * paths with every sampleLightsReSTIR call (raytracer.glsl:1619-1801)
  * appended to a per-wave list, evaluates the list in a second kernel with
@@ -368,8 +379,12 @@ int rt0_last_kernel_ms(const rt0_ctx *ctx, float *ms, int *launches);
 #define RT0_PATH_DEFERRED 3   /* ReSTIR: pass + light sampling (+ walk) + resolve */
 #define RT0_PATH_WAVEFRONT 4  /* wavefront shade + march / walk rounds (rt0_set_wavefront) */
 int rt0_last_render_path(const rt0_ctx *ctx);
-/* Bytes of device scratch the context holds for frame-chunked launches
- * (per-frame sample planes over the launch rectangle; grows on demand). */
+/* Bytes of device scratch the context holds beyond the accumulator and the
+ * reservoir planes: per-frame sample planes of frame-chunked launches (over
+ * the launch rectangle), the wavefront rounds' path state (bounded by
+ * RT0_WF_BYTES, default 8 GiB: a frame that does not fit runs as slot chunks;
+ * released when a render no longer takes the wavefront path), and the
+ * deferred ReSTIR records, result planes and walk jobs.  Grows on demand. */
 int rt0_scratch_bytes(const rt0_ctx *ctx, size_t *bytes);
 
 /* Library version string. */

@@ -74,7 +74,10 @@ class Oracle:
         self._chk(L.or_set_scene_lines(self.h, "\n".join(lines).encode(), karr, len(kinds)))
         for k, v in cfg.get("defines", {}).items():
             self._chk(L.or_set_define(self.h, k.encode(), int(bool(v))))
-        consts = dict(cfg.get("constants", {}))
+        # the reference executor's fixed-point texture filter, as the product's
+        # default (rt0_set_texture_filter; SWIFTSHADER_TEX_FILTER 0 = fp32 bilinear)
+        consts = {"SWIFTSHADER_TEX_FILTER": 1}
+        consts.update(cfg.get("constants", {}))
         consts.update(overrides or {})
         for k, v in consts.items():
             self._chk(L.or_set_constant(self.h, k.encode(), float(v)))

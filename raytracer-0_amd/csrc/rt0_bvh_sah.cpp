@@ -29,7 +29,6 @@
 #include <cmath>
 #include <cstdint>
 #include <thread>
-#include <functional>
 #include <vector>
 
 #include "rt0_device.h"
@@ -245,72 +244,6 @@ int bvh_build_sah(int n, const float *v, const int32_t *model, std::vector<BvhNo
             std::sqrt(d.e1x * d.e1x + d.e1y * d.e1y + d.e1z * d.e1z);
   }
   return depth;
-}
-
-// Collapse of the binary tree to 4-wide nodes: node N's children become its
-// children's children (a leaf child stays a child), in the binary order
-// left.left, left.right, right.left, right.right, so a walk that tests leaves
-// in child order meets them in the binary walk's order.  Pre-order layout
-// (a node's first inner child follows it).  The stack a walk needs: at a node
-// with m inner children it pushes up to m - 1 of them and descends into one.
-int bvh4_collapse(const std::vector<BvhNode> &nodes, int n_tris, std::vector<Bvh4Node> &out) {
-  out.clear();
-  if (n_tris < 2 || nodes.empty()) return -1;
-  struct Kid {
-    int32_t link;
-    float lo[3], hi[3];
-  };
-  auto kids_of = [&](int i, Kid k[2]) {
-    const BvhNode &b = nodes[(size_t)i];
-    k[0] = Kid{b.left, {b.lx0, b.ly0, b.lz0}, {b.lx1, b.ly1, b.lz1}};
-    k[1] = Kid{b.right, {b.rx0, b.ry0, b.rz0}, {b.rx1, b.ry1, b.rz1}};
-  };
-  // returns the node's index and its stack need
-  std::function<std::pair<int, int>(int)> build = [&](int i2) -> std::pair<int, int> {
-    Kid top[2], all[4];
-    kids_of(i2, top);
-    int n = 0;
-    for (const Kid &t : top) {
-      if (t.link >= 0) {
-        Kid g[2];
-        kids_of(t.link, g);
-        all[n++] = g[0];
-        all[n++] = g[1];
-      } else {
-        all[n++] = t;
-      }
-    }
-    const int idx = (int)out.size();
-    out.push_back(Bvh4Node{});
-    Bvh4Node nd;
-    int inner = 0, deepest = 0;
-    for (int k = 0; k < 4; k++) {
-      if (k < n) {
-        nd.lox[k] = all[k].lo[0];
-        nd.loy[k] = all[k].lo[1];
-        nd.loz[k] = all[k].lo[2];
-        nd.hix[k] = all[k].hi[0];
-        nd.hiy[k] = all[k].hi[1];
-        nd.hiz[k] = all[k].hi[2];
-        if (all[k].link >= 0) {
-          const auto c = build(all[k].link);
-          nd.child[k] = c.first;
-          ++inner;
-          deepest = std::max(deepest, c.second);
-        } else {
-          nd.child[k] = all[k].link;
-        }
-      } else {  // an empty box: no ray enters it
-        nd.lox[k] = nd.loy[k] = nd.loz[k] = INFINITY;
-        nd.hix[k] = nd.hiy[k] = nd.hiz[k] = -INFINITY;
-        nd.child[k] = RT0_BVH4_EMPTY;
-      }
-      nd.pad[k] = 0;
-    }
-    out[(size_t)idx] = nd;
-    return {idx, std::max(0, inner - 1) + deepest};
-  };
-  return build(0).second;
 }
 
 }  // namespace rt0h

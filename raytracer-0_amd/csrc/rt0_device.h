@@ -73,19 +73,6 @@ struct BvhNode {
   float rz0, rx1, ry1, rz1;
   int32_t left, right, pad0, pad1;
 };
-// The 4-wide tree the scene-specialised kernels walk (RT0_BVH4; rt0_bvh_sah.cpp
-// bvh4_collapse): each node holds the boxes of up to 4 children, one
-// structure-of-arrays row per bound (child k in lane k of each float4), and
-// their links (>= 0: a 4-wide node, < 0: ~triangle, a leaf; RT0_BVH4_EMPTY:
-// no child, its box empty).  128 B: two cache lines per visit instead of one
-// per level of the binary tree, half the dependent loads along a ray.
-struct Bvh4Node {
-  float lox[4], loy[4], loz[4];
-  float hix[4], hiy[4], hiz[4];
-  int32_t child[4];
-  int32_t pad[4];
-};
-#define RT0_BVH4_EMPTY ((int32_t)0x80000000)
 #ifndef RT0_BVH_STACK
 #define RT0_BVH_STACK 48  // traversal stack entries per lane (LDS); the build checks the bound
 #endif
@@ -165,6 +152,9 @@ enum : uint32_t {
   // the oracle's GLES executor stores g_final_reservoir after a `break` of the
   // bounce loop (oracle/gen/mask_kat.py).  Off = GLSL semantics.
   F_EXEC_GHOST = 1u << 10,
+  // RGBA8 asset / noise textures through the fixed-point bilinear filter the
+  // reference's executor uses (rt0_set_texture_filter, default on)
+  F_TEX_FIXED = 1u << 11,
 };
 
 struct LaunchParams {
@@ -220,7 +210,6 @@ struct LaunchParams {
   int32_t cube_size;
   // Triangle models: LBVH nodes (root 0) and triangles in leaf order; n_tris 0 = none.
   const BvhNode *bvh;
-  const Bvh4Node *bvh4;  // the same tree as 4-wide nodes (null: none; RT0_BVH4 kernels walk it)
   const TriDev *tris;
   int32_t n_tris;
   // RENDER_MODE 1 (F_ANIM): the accumulator is an EMA with weight ema_alpha =

@@ -38,16 +38,8 @@ extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_mo
 // shards, against 0.89 / 0.78 / 0.61 unchunked).
 static const long kTargetWaves = 16384;
 static const long kChunkWaves = 65536;
-// pass-wave record regions per light-sampling wave (JitKey::nee_regions); RT0_NEE_REGIONS overrides
-static long nee_regions_per_wave() {
-  static const long k = getenv("RT0_NEE_REGIONS") ? std::max(1L, atol(getenv("RT0_NEE_REGIONS"))) : 2L;
-  return k;
-}
-// light-sampling calls' triangle occlusion queries in rt0_jit_walk (JitKey::walk); RT0_NEE_WALK=0 keeps them inline
-static bool nee_walk_enabled() {
-  static const bool k = !(getenv("RT0_NEE_WALK") && atoi(getenv("RT0_NEE_WALK")) == 0);
-  return k;
-}
+// pass-wave record regions per light-sampling wave (JitKey::nee_regions)
+static long nee_regions_per_wave() { return 2L; }
 
 enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
 
@@ -69,8 +61,6 @@ struct rt0_ctx {
   std::vector<Model> models;
   bool bvh_dirty = false;
   BvhNode *d_bvh = nullptr;
-  Bvh4Node *d_bvh4 = nullptr;  // the SAH tree collapsed to 4-wide nodes (null: LBVH build or < 2 triangles)
-  int bvh4_stack = 0;           // traversal stack entries a 4-wide walk can need
   TriDev *d_tris = nullptr;
   int n_tris = 0, bvh_depth = 0;
   SceneDev *d_scene = nullptr;
@@ -112,6 +102,7 @@ struct rt0_ctx {
   SceneDev host_scene;   // what d_scene holds (also the JIT's scene data)
   bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
   bool exec_compat = false;  // rt0_set_executor_compat: F_EXEC_GHOST
+  int tex_filter = RT0_TEX_FILTER_FIXED16;  // rt0_set_texture_filter: F_TEX_FIXED
   // the scene-specialised kernel of the current (scene, config): looked up once
   // per change instead of regenerating and hashing its source on every render
   rt0h::JitFns jit;
@@ -296,7 +287,6 @@ void rt0_destroy(rt0_ctx *c) {
     if (t) (void)hipFree(t);
   if (c->d_cube) (void)hipFree(c->d_cube);
   if (c->d_bvh) (void)hipFree(c->d_bvh);
-  if (c->d_bvh4) (void)hipFree(c->d_bvh4);
   if (c->d_tris) (void)hipFree(c->d_tris);
   for (auto &s : c->wf_streams)
     if (s) (void)hipStreamDestroy(s);
@@ -487,14 +477,8 @@ int rt0_set_model(rt0_ctx *c, int model, const float *positions, int n_vertices,
 // one BVH: the binned-SAH tree built on the host (rt0_bvh_sah.cpp, default) or
 // the device LBVH (rt0_bvh.hip; RT0_BVH_BUILD=lbvh).  Runs at the first render
 // after a scene/model change.
-// RT0_BVH4=1: the scene-specialised kernels walk the 4-wide tree.  Measured
-// slower on C5 (9.66 vs 8.32 ms per pass: the pass kernel 5.0 vs 3.9 ms,
-// spilling at 8 waves; profiles/r05/c5_bvh4), so the binary tree stays the
-// default.
-static bool bvh4_enabled() {
-  static const bool on = getenv("RT0_BVH4") && atoi(getenv("RT0_BVH4")) != 0;
-  return on;
-}
+// (A 4-wide collapse of the SAH tree was measured slower on C5 -- 9.66 vs
+// 8.32 ms per pass, profiles/r05/c5_bvh4 -- and removed: scripts/ab_r5_bvh4.patch.)
 static bool bvh_builder_sah() {
   static const bool sah = !(getenv("RT0_BVH_BUILD") && std::string(getenv("RT0_BVH_BUILD")) == "lbvh");
   return sah;
@@ -524,10 +508,7 @@ static int build_bvh(rt0_ctx *c) {
   }
   const int n = (int)owner.size();
   if (c->d_bvh) HIPCHK(c, hipFree(c->d_bvh));
-  if (c->d_bvh4) HIPCHK(c, hipFree(c->d_bvh4));
   if (c->d_tris) HIPCHK(c, hipFree(c->d_tris));
-  c->d_bvh4 = nullptr;
-  c->bvh4_stack = 0;
   c->d_bvh = nullptr;
   c->d_tris = nullptr;
   c->n_tris = 0;
@@ -541,13 +522,6 @@ static int build_bvh(rt0_ctx *c) {
     std::vector<TriDev> tris;
     depth = rt0h::bvh_build_sah(n, v.data(), owner.data(), nodes, tris);
     HIPCHK(c, hipMemcpy(c->d_bvh, nodes.data(), nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
-    std::vector<Bvh4Node> nodes4;
-    const int need = rt0h::bvh4_collapse(nodes, n, nodes4);
-    if (need >= 0 && need + 1 < RT0_BVH_STACK) {
-      HIPCHK(c, hipMalloc(&c->d_bvh4, nodes4.size() * sizeof(Bvh4Node)));
-      HIPCHK(c, hipMemcpy(c->d_bvh4, nodes4.data(), nodes4.size() * sizeof(Bvh4Node), hipMemcpyHostToDevice));
-      c->bvh4_stack = need + 1;
-    }
     HIPCHK(c, hipMemcpy(c->d_tris, tris.data(), tris.size() * sizeof(TriDev), hipMemcpyHostToDevice));
   } else {
     float *d_v = nullptr;
@@ -564,9 +538,6 @@ static int build_bvh(rt0_ctx *c) {
   }
   if (depth >= RT0_BVH_STACK)
     return fail(c, RT0_E_UNSUPPORTED, "BVH depth " + std::to_string(depth) + " exceeds the traversal stack");
-  if (getenv("RT0_BVH_DEBUG"))
-    fprintf(stderr, "rt0 bvh: %s build, %d triangles, depth %d, 4-wide stack %d\n", bvh_builder_sah() ? "sah" : "lbvh",
-            n, depth, c->bvh4_stack);
   c->n_tris = n;
   c->bvh_depth = depth;
   c->jit_dirty = true;  // the scene-specialised kernel's traversal stack follows the depth
@@ -665,7 +636,8 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.uULen = p.aspect * p.uVLen;
   p.aperture = c->cam_params[1];
   p.focal = c->cam_params[2];
-  p.flags = rt0h::flags_from_config(g) | (c->exec_compat ? F_EXEC_GHOST : 0u);
+  p.flags = rt0h::flags_from_config(g) | (c->exec_compat ? F_EXEC_GHOST : 0u) |
+            (c->tex_filter == RT0_TEX_FILTER_FIXED16 ? F_TEX_FIXED : 0u);
   p.max_bounces = g.max_bounces;
   p.max_diff = g.max_diff_bounces;
   p.max_spec = g.max_spec_bounces;
@@ -699,7 +671,6 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.cube = c->d_cube;
   p.cube_size = c->cube_size;
   p.bvh = c->d_bvh;
-  p.bvh4 = c->d_bvh4;
   p.tris = c->d_tris;
   p.n_tris = c->n_tris;
   p.accum = c->acc();
@@ -786,14 +757,17 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   uint32_t kR = 512;
   if (restir) {
     kR = 64;  // the deferred calls' regions are the pass waves'
-  } else if (const char *e = getenv("RT0_WF_REGION")) {
-    kR = (uint32_t)std::max(64, atoi(e)) / 64 * 64;
   } else {
     const size_t waves = (size_t)std::max(1, c->jit.wf_march_blocks) * 4;
     while (kR > 128 && apad * (size_t)p.nframes / K / kR < 4 * waves) kR /= 2;
   }
-  const int fc = (int)std::max<size_t>(1, std::min<size_t>((size_t)p.nframes, budget / (apad * per_slot)));
-  const size_t S = apad * (size_t)fc;                     // slots of a frame chunk
+  // A chunk holds as many whole frames as the budget does; a frame that does
+  // not fit (e.g. 4096^2 with 32 lights: ~36 GB) runs as slot chunks of whole
+  // regions, so RT0_WF_BYTES bounds the allocation (a slot's frame and pixel
+  // follow from its global index, wf_slot0 + slot: any cut is valid)
+  const size_t fit = budget / per_slot, unit = (size_t)K * kR;
+  const int fc = (int)std::max<size_t>(1, std::min<size_t>((size_t)p.nframes, fit / apad));
+  const size_t S = fit >= apad ? apad * (size_t)fc : std::max(unit, fit / unit * unit);  // slots of a chunk
   const size_t Sk = ((S + K - 1) / K + kR - 1) / kR * kR;  // slots of one half (whole regions)
   if (Sk * std::max(1u, L) >= (1ull << 32)) return fail(c, RT0_E_UNSUPPORTED, "wavefront render: too many path slots");
   const size_t NR = Sk / kR, cap = NR * kR;
@@ -853,14 +827,17 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   };
   HIPCHK(c, hipEventRecord(c->wf_fork, c->stream));
   for (int k = 1; k < K; k++) HIPCHK(c, hipStreamWaitEvent(st[k], c->wf_fork, 0));
-  for (int f0 = 0; f0 < p.nframes; f0 += fc) {
-    const size_t Sc = apad * (size_t)std::min(fc, p.nframes - f0);  // this chunk's slots
+  for (size_t ck = 0, nck = (size_t)p.nframes * apad; ck < nck;) {
+    const int f0 = (int)(ck / apad);  // the chunk's first frame
+    const size_t s0 = ck - (size_t)f0 * apad, in_frames = apad * (size_t)std::min(fc, p.nframes - f0) - s0;
+    const size_t Sc = std::min(S, in_frames);  // this chunk's slots
+    ck += Sc;
     int live = 0;
     for (int k = 0; k < K; k++) {
       LaunchParams &u = q[k];
       u.wf_f0 = f0;
-      u.wf_slot0 = (uint32_t)std::min(Sc, (size_t)k * Sk);
-      u.wf_slots = (uint32_t)(std::min(Sc, (size_t)(k + 1) * Sk) - u.wf_slot0);
+      u.wf_slot0 = (uint32_t)(s0 + std::min(Sc, (size_t)k * Sk));
+      u.wf_slots = (uint32_t)(std::min(Sc, (size_t)(k + 1) * Sk) - std::min(Sc, (size_t)k * Sk));
       u.wf_nregions = (int32_t)((u.wf_slots + kR - 1) / kR);
       // plan blocks of >= 256 regions, at most 256 of them (wf_plan_prefix)
       u.wf_plan_span = std::max(256, (u.wf_nregions + 255) / 256);
@@ -1019,10 +996,16 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
   // lights) and RENDER_MODE 0 (Integrator::restir_split), and a grid whose
   // records fit the result tag's 29-bit slot field.  Re-evaluated every render:
   // a viewport or image size change alone can flip it.
-  const bool want_walk = defer && nee_walk_enabled() && c->host_scene.n_models > 0 && c->n_tris > 0 &&
+  const bool want_walk = defer && c->host_scene.n_models > 0 && c->n_tris > 0 &&
                          c->host_scene.n_sdfs == 0 && !c->host_scene.any_tex && c->cfg.render_mode == 0 &&
                          (size_t)grid.x * grid.y * 4 * 64 * (size_t)p.max_bounces < (1u << 29) - 1u;
   const bool want_wf = wf_eligible(c, want_walk);
+  if (!want_wf && c->d_wf) {  // a scene or config the rounds no longer serve: release their state
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(c->d_wf));
+    c->d_wf = nullptr;
+    c->wf_bytes = 0;
+  }
   if (c->use_jit && !c->counting) {
     if (c->jit_dirty || !(c->jit.pass || c->jit.wf_shade) || (defer != (c->jit.nee != nullptr)) ||
         (defer && want_walk != (c->jit.walk != nullptr)) || want_wf != (c->jit.wf_shade != nullptr)) {
@@ -1030,10 +1013,6 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       if (c->exec_compat) key.flags |= F_EXEC_GHOST;
       key.halo_check = c->n_shards > 1 ? 1 : 0;
       key.bvh_stack = (c->host_scene.n_models > 0 && c->n_tris > 0) ? c->bvh_depth + 1 : 0;
-      // the 4-wide tree (RT0_BVH4=1 in the environment); the stack also
-      // serves the binary walks the wavefront rounds keep
-      key.bvh4 = key.bvh_stack > 0 && c->d_bvh4 != nullptr && bvh4_enabled() ? 1 : 0;
-      if (key.bvh4) key.bvh_stack = std::max(key.bvh_stack, c->bvh4_stack);
       key.defer = defer ? 1 : 0;
       {  // 16-bit traversal stack entries + high bits in a 64-bit register (rt0_integrator.h BvhStack)
         const int entries = key.bvh_stack > 0 ? rt0h::jit_stack_entries(key) : 0;
@@ -1091,7 +1070,10 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     if (c->jit.walk) {
       // per light-sampling wave: up to two rays per record of its regions
       // (+3: the up to 4 parts of a split pass round their wave counts up apart)
-      const size_t waves = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave() + 3;
+      // p.walk_waves is the exact count (the walk kernel's guard): the padding
+      // waves of the unsplit launch must not read counts no nee wave wrote
+      const size_t exact = (pass_waves + nee_regions_per_wave() - 1) / nee_regions_per_wave();
+      const size_t waves = exact + 3;
       const size_t jobs = waves * 2 * (size_t)nee_regions_per_wave() * (size_t)p.nee_cap;
       if (jobs > c->walk_jobs_n || 2 * slots > c->walk_res_n || waves > c->walk_waves_n) {
         for (void **q : {(void **)&c->d_walk_jobs, (void **)&c->d_walk_count, (void **)&c->d_walk_res}) {
@@ -1109,7 +1091,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       p.walk_jobs = c->d_walk_jobs;
       p.walk_count = c->d_walk_count;
       p.walk_res = c->d_walk_res;
-      p.walk_waves = (int32_t)waves;
+      p.walk_waves = (int32_t)exact;
     }
   }
   auto launch = [&](const LaunchParams &lp, unsigned gz, dim3 g) -> hipError_t {
@@ -1191,8 +1173,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     // device holds ~16 waves per SIMD; samples go to a scratch buffer and
     // rt0_sum_kernel adds them in frame order (bit-identical accumulation).
     const long waves = (long)grid.x * grid.y * 4;
-    static const long target = getenv("RT0_TARGET_WAVES") ? atol(getenv("RT0_TARGET_WAVES")) : kChunkWaves;
-    static const long min_waves = getenv("RT0_MIN_WAVES") ? atol(getenv("RT0_MIN_WAVES")) : kTargetWaves;
+    const long target = kChunkWaves, min_waves = kTargetWaves;
     const int want = (c->counting || waves >= min_waves)
                          ? 1
                          : (int)std::min<long>(c->max_frames_per_launch, (target + waves - 1) / waves);
@@ -1406,6 +1387,12 @@ int rt0_set_executor_compat(rt0_ctx *c, int enable) {
   return RT0_OK;
 }
 
+int rt0_set_texture_filter(rt0_ctx *c, int mode) {
+  if (!c || (mode != RT0_TEX_FILTER_FLOAT && mode != RT0_TEX_FILTER_FIXED16)) return RT0_E_ARG;
+  c->tex_filter = mode;
+  return RT0_OK;
+}
+
 int rt0_set_accum_buffer(rt0_ctx *c, void *dptr) {
   if (!c) return RT0_E_ARG;
   c->ext_accum = (float4 *)dptr;
@@ -1489,7 +1476,11 @@ int rt0_read_counters_n(rt0_ctx *c, uint64_t *out, int n) {
 
 int rt0_scratch_bytes(const rt0_ctx *c, size_t *bytes) {
   if (!c || !bytes) return RT0_E_ARG;
-  *bytes = c->samples_bytes;
+  // per-frame samples + the wavefront rounds' state + the deferred ReSTIR
+  // records, results and walk jobs
+  *bytes = c->samples_bytes + c->wf_bytes + c->nee_slots * sizeof(NeeRec) + c->nee_waves * sizeof(uint32_t) +
+           c->nee_pixels * (c->nee_planes + 1) * sizeof(float4) + c->nee_pixels * sizeof(int32_t) +
+           c->walk_jobs_n * sizeof(WalkJob) + (c->walk_waves_n + c->walk_res_n) * sizeof(uint32_t);
   return RT0_OK;
 }
 

@@ -110,17 +110,11 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_NEE_WALK  // light-sampling calls' triangle occlusion queries in rt0_jit_walk (models scenes)
 #define RT0_NEE_WALK 0
 #endif
-#ifndef RT0_BVH4  // scene-specialised kernels walk the 4-wide tree (Bvh4Node; rt0_jit.cpp JitKey::bvh4)
-#define RT0_BVH4 0
-#endif
 #ifndef RT0_WALK_ROOT_TEST  // light-sampling kernel drops walk jobs that miss the root's child boxes
 #define RT0_WALK_ROOT_TEST 1
 #endif
 #ifndef RT0_WALK_SPEC  // rt0_jit_walk postpones leaf tests until half the busy lanes hold one
 #define RT0_WALK_SPEC 1
-#endif
-#ifndef RT0_CLOSEST_SPEC  // bvh_closest tests leaves once half the walking lanes hold one (while-while)
-#define RT0_CLOSEST_SPEC 0
 #endif
 #ifndef RT0_BVH_STACK16  // BVH traversal stacks as 16-bit LDS entries + high bits in a register
 #define RT0_BVH_STACK16 0
@@ -401,16 +395,6 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
 // before tmax: then every walk of it ends at its first node with no triangle
 // test (bvh_closest, walk_body), so it needs none
 DEV bool bvh_root_miss(const LaunchParams &P, v3 o, v3 inv, float tmax) {
-#if RT0_BVH4
-  {
-    const float4 *__restrict__ nodes4 = reinterpret_cast<const float4 *>(P.bvh4);
-    const float4 lx = nodes4[0], ly = nodes4[1], lz = nodes4[2], hx = nodes4[3], hy = nodes4[4], hz = nodes4[5];
-    return box_enter(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, o, inv, tmax) == F_INF &&
-           box_enter(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, o, inv, tmax) == F_INF &&
-           box_enter(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, o, inv, tmax) == F_INF &&
-           box_enter(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, o, inv, tmax) == F_INF;  // (empty slots: empty boxes)
-  }
-#endif
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
   const float4 a = nodes[0], b = nodes[1], c = nodes[2];
   return box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmax) == F_INF &&
@@ -472,175 +456,6 @@ DEV uint32_t wave_append(uint32_t *ctr) {
   if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(act));
   return (uint32_t)__shfl((int)base, leader) + rank;
 }
-#if RT0_BVH4
-// A 4-wide node's children: entry distances (F_INF: missed, entered beyond
-// tmin, or no child) by box_enter's arithmetic, and links
-struct Bvh4Kids {
-  float t[4];
-  int c[4];
-};
-DEV Bvh4Kids bvh4_kids(const float4 *__restrict__ nd, v3 o, v3 inv, float tmin) {
-  const float4 lx = nd[0], ly = nd[1], lz = nd[2], hx = nd[3], hy = nd[4], hz = nd[5];
-  const int4 ch = reinterpret_cast<const int4 *>(nd)[6];
-  Bvh4Kids k;
-  k.c[0] = ch.x;
-  k.c[1] = ch.y;
-  k.c[2] = ch.z;
-  k.c[3] = ch.w;
-  k.t[0] = box_enter(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, o, inv, tmin);
-  k.t[1] = box_enter(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, o, inv, tmin);
-  k.t[2] = box_enter(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, o, inv, tmin);
-  k.t[3] = box_enter(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, o, inv, tmin);
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (k.c[j] == RT0_BVH4_EMPTY) k.t[j] = F_INF;
-  return k;
-}
-// The inner children of a visited node still entered before tmin, nearest
-// first (ties in child order): (entry bits << 2 | child slot) keys through a
-// 4-input sorting network.  Returns how many; n0..n3 their links in order.
-DEV int bvh4_order(const Bvh4Kids &k, float tmin, int &n0, int &n1, int &n2, int &n3) {
-  uint64_t key[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const bool in = k.c[j] >= 0 && k.t[j] < tmin;
-    key[j] = in ? (((uint64_t)__float_as_uint(k.t[j]) << 2) | (uint64_t)j) : ~0ull;  // (t >= 0: the bits order like t)
-  }
-  auto cs = [](uint64_t &a, uint64_t &b) {
-    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
-    a = lo;
-    b = hi;
-  };
-  cs(key[0], key[1]);
-  cs(key[2], key[3]);
-  cs(key[0], key[2]);
-  cs(key[1], key[3]);
-  cs(key[1], key[2]);
-  auto link = [&](uint64_t q) {
-    const int j = (int)(q & 3u);
-    return j == 0 ? k.c[0] : j == 1 ? k.c[1] : j == 2 ? k.c[2] : k.c[3];
-  };
-  n0 = link(key[0]);
-  n1 = link(key[1]);
-  n2 = link(key[2]);
-  n3 = link(key[3]);
-  return (key[0] != ~0ull) + (key[1] != ~0ull) + (key[2] != ~0ull) + (key[3] != ~0ull);
-}
-// bvh_closest on the 4-wide tree: leaf children tested in child order (the
-// binary walk's leaf order), then the nearest inner child next and the others
-// on the stack, farthest first.  Every triangle the binary walk could test
-// before tmin is tested or culled by the same boxes, so the closest t is the
-// same; the winner of an exact tie between two triangles can differ.
-template <bool ANY>
-DEV int bvh4_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
-  BvhStack stk;
-  int sp = 0, node = 0, best = -1;
-  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh4);
-  const TriDev *__restrict__ tris = P.tris;
-  // fewer than n_tris 4-wide nodes, each visited at most once (the cap only
-  // guarantees an exit on a corrupt tree)
-  for (int guard = P.n_tris + 8; guard > 0; --guard) {
-    const Bvh4Kids k = bvh4_kids(nodes + 8 * node, o, inv, tmin);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (k.c[j] < 0 && k.c[j] != RT0_BVH4_EMPTY && k.t[j] != F_INF) {
-        float t;
-        if (tri_test(tris[~k.c[j]], o, d, tmin, t)) {
-          tmin = t;
-          best = ~k.c[j];
-        }
-      }
-    }
-    if (ANY && best >= 0) break;
-    int n0, n1, n2, n3;
-    const int m = bvh4_order(k, tmin, n0, n1, n2, n3);
-    if (m > 0) {
-      if (m > 3) {
-        stk.put(sp, n3);
-        sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build sizes the stack (bvh4_collapse)
-      }
-      if (m > 2) {
-        stk.put(sp, n2);
-        sp = min(sp + 1, RT0_BVH_STACK - 1);
-      }
-      if (m > 1) {
-        stk.put(sp, n1);
-        sp = min(sp + 1, RT0_BVH_STACK - 1);
-      }
-      node = n0;
-    } else {
-      if (sp == 0) break;
-      node = stk.get(--sp);
-    }
-  }
-  return best;
-}
-#endif
-
-// bvh_closest with the leaf tests of the walking lanes gathered
-// (RT0_CLOSEST_SPEC; walk_body_spec's while-while scheme): a lane whose node
-// visit finds leaves holds them and visits no further node until the wave's
-// leaf phase, which runs once half the lanes still walking hold leaves (or
-// none can go on without testing its own).  Per lane the visits, the leaf
-// tests and every tmin they see are bvh_closest's, in the same order -- only
-// the wave's schedule changes -- so the hit is the same bit for bit.
-template <bool ANY>
-DEV int bvh_closest_spec(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin) {
-  BvhStack stk;
-  int sp = 0, node = 0, best = -1, pa = -1, pb = -1;  // node -1: no node left; pa/pb: held leaves
-  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
-  const TriDev *__restrict__ tris = P.tris;
-  for (int guard = 2 * P.n_tris + 8;;) {
-    if (pa < 0 && node >= 0) {
-      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
-      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
-      float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
-      float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
-      const int cl = lk.x, cr = lk.y;
-      if (tl != F_INF && cl < 0) {
-        pa = ~cl;
-        tl = F_INF;
-      }
-      if (tr != F_INF && cr < 0) {
-        if (pa < 0) pa = ~cr;
-        else pb = ~cr;
-        tr = F_INF;
-      }
-      if (tl != F_INF && tr != F_INF) {
-        const bool lfirst = tl <= tr;
-        stk.put(sp, lfirst ? cr : cl);
-        sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build guarantees depth < RT0_BVH_STACK
-        node = lfirst ? cl : cr;
-      } else if (tl != F_INF) {
-        node = cl;
-      } else if (tr != F_INF) {
-        node = cr;
-      } else if (sp == 0) {
-        node = -1;
-      } else {
-        node = stk.get(--sp);
-      }
-      if (--guard <= 0) node = -1;  // a ray visits each node at most once: exit on a corrupt tree
-    }
-    const uint64_t walking = __ballot(1), lf = __ballot(pa >= 0), stuck = __ballot(pa >= 0 || node < 0);
-    if ((2 * __popcll(lf) >= __popcll(walking) || stuck == walking) && pa >= 0) {
-      float t;
-      if (tri_test(tris[pa], o, d, tmin, t)) {
-        tmin = t;
-        best = pa;
-      }
-      if (pb >= 0 && tri_test(tris[pb], o, d, tmin, t)) {
-        tmin = t;
-        best = pb;
-      }
-      pa = pb = -1;
-      if (ANY && best >= 0) break;
-    }
-    if (pa < 0 && node < 0) break;
-  }
-  return best;
-}
-
 // closest triangle hit along (o, d) before tmin: depth-first, nearer child
 // first, the far child on the per-lane LDS stack.  Returns the leaf-order
 // triangle index or -1; tmin is updated.  ANY: stop at the first hit before
@@ -653,11 +468,6 @@ DEV int bvh_closest_spec(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin)
 template <bool ANY = false>
 DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsigned long long *cnt = nullptr,
                     int budget = 0x7fffffff, bool *complete = nullptr) {
-#if RT0_BVH4
-  if (!complete && !cnt) return bvh4_closest<ANY>(P, o, d, inv, tmin);
-#elif RT0_CLOSEST_SPEC
-  if (!complete && !cnt) return bvh_closest_spec<ANY>(P, o, d, inv, tmin);
-#endif
   BvhStack stk;
   int sp = 0, node = 0, best = -1;
   const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh);
@@ -1175,8 +985,10 @@ DEV float smoothstep_(float e0, float e1, float x) {
 }
 // GL_LINEAR + GL_REPEAT fetch at level 0 of an RGBA8 asset texture
 // (GlslViewport.loadTexture, index.js:703-708); unbound unit = (0,0,0,1).
-// Executor compatibility (F_EXEC_GHOST): SwiftShader 4.1's fixed-point
-// GL_LINEAR + GL_REPEAT fetch, measured by the known-answer shaders of
+// F_TEX_FIXED (rt0_set_texture_filter, the default): SwiftShader 4.1's
+// fixed-point GL_LINEAR + GL_REPEAT fetch -- GLSL leaves the filter's
+// precision to the implementation, and GPU texture units filter in fixed
+// point too -- measured by the known-answer shaders of
 // oracle/gen/tex_kat.py (tests/golden/tex_filter_kat.npz; restated as
 // tex_fetch_ss in oracle/rt0_oracle.c): the coordinate as a 16-bit fraction
 // (trunc(u * 65536) & 0xFFFF), the half texel taken off in that unit
@@ -1212,7 +1024,7 @@ DEV T4 tex_rgba8(const LaunchParams &P, int unit, float u, float v) {
   const uint32_t *__restrict__ img = P.tex_img[unit];
   if (img == nullptr) return T4{0.f, 0.f, 0.f, 1.f};
   const int w = P.tex_w[unit], h = P.tex_h[unit];
-  if (P.flags & F_EXEC_GHOST) return tex_rgba8_ss(img, w, h, u, v);
+  if (P.flags & F_TEX_FIXED) return tex_rgba8_ss(img, w, h, u, v);
   const float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
   const float fx = floorf(x), fy = floorf(y);
   const float a = x - fx, b = y - fy;
@@ -3386,89 +3198,8 @@ DEV void walk_body_spec(const LaunchParams &P) {
   }
 }
 
-#if RT0_BVH4
-// walk_body on the 4-wide tree: one node (four child boxes, its leaf
-// children's triangle tests) per iteration, refilled lanes as walk_body
-DEV void walk_body4(const LaunchParams &P) {
-  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
-  if (w >= (uint32_t)P.walk_waves) return;
-  const uint32_t n = P.walk_count[w];
-  const WalkJob *__restrict__ jobs = P.walk_jobs + (size_t)w * (2u * RT0_NEE_REGIONS * (uint32_t)P.nee_cap);
-  uint32_t *ctr = nee_wave_counter();
-  *(volatile uint32_t *)ctr = 64u;  // every lane stores the same value: jobs 0..63 go by lane index
-  const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(P.bvh4);
-  const TriDev *__restrict__ tris = P.tris;
-  BvhStack stk;
-  uint32_t j = threadIdx.x & 63u;
-  bool have = false;
-  v3 o = mk(0.f, 0.f, 0.f), d = o, inv = o;
-  float tmax = 0.f;
-  uint32_t slot2 = 0;
-  int node = 0, sp = 0, guard = 0;
-  auto load = [&]() {
-    have = j < n;
-    if (have) {
-      const WalkJob jb = jobs[j];
-      o = mk(jb.ox, jb.oy, jb.oz);
-      d = mk(jb.dx, jb.dy, jb.dz);
-      inv = mk(frcp(d.x), frcp(d.y), frcp(d.z));
-      tmax = jb.tmax;
-      slot2 = jb.slot2;
-      node = 0;
-      sp = 0;
-      guard = 0;  // (stale stack entries are never read: sp restarts at 0)
-    }
-  };
-  load();
-  while (__ballot(have) != 0ull) {
-    if (have) {
-      bool occ = false, done = false;
-      const Bvh4Kids k = bvh4_kids(nodes + 8 * node, o, inv, tmax);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!occ && k.c[q] < 0 && k.c[q] != RT0_BVH4_EMPTY && k.t[q] != F_INF) {
-          float t;
-          occ = tri_test(tris[~k.c[q]], o, d, tmax, t);
-        }
-      }
-      int n0, n1, n2, n3;
-      const int m = occ ? 0 : bvh4_order(k, tmax, n0, n1, n2, n3);
-      if (occ) {
-        done = true;
-      } else if (m > 0) {
-        if (m > 3) {
-          stk.put(sp, n3);
-          sp = min(sp + 1, RT0_BVH_STACK - 1);  // the build sizes the stack (bvh4_collapse)
-        }
-        if (m > 2) {
-          stk.put(sp, n2);
-          sp = min(sp + 1, RT0_BVH_STACK - 1);
-        }
-        if (m > 1) {
-          stk.put(sp, n1);
-          sp = min(sp + 1, RT0_BVH_STACK - 1);
-        }
-        node = n0;
-      } else if (sp == 0) {
-        done = true;
-      } else {
-        node = stk.get(--sp);
-      }
-      if (++guard > P.n_tris + 8) done = true;  // (every wave drains even on a corrupt tree)
-      if (done) {
-        P.walk_res[slot2] = occ ? 1u : 0u;
-        j = atomicAdd(ctr, 1u);
-        load();
-      }
-    }
-  }
-}
-#endif
-
 DEV void walk_body(const LaunchParams &P) {
-#if RT0_BVH4
-  walk_body4(P);
-#elif RT0_WALK_SPEC
+#if RT0_WALK_SPEC
   walk_body_spec(P);
 #else
   const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));

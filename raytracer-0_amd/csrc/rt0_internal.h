@@ -9,7 +9,6 @@
 
 struct BvhNode;
 struct TriDev;
-struct Bvh4Node;
 
 namespace rt0h {
 int lookup_material(const std::string &name, rt0_mesh &m);
@@ -26,7 +25,6 @@ int bvh_build_sah(int n, const float *v, const int32_t *model, std::vector<BvhNo
 // the binary tree collapsed to 4-wide nodes (grandchildren become children);
 // returns the traversal stack entries a walk can need (pushes along the
 // deepest chain), nodes4 in pre-order
-int bvh4_collapse(const std::vector<BvhNode> &nodes, int n_tris, std::vector<Bvh4Node> &nodes4);
 int parse_config(const char *const *defines, int nd, const char *const *constants, int nc, rt0_config &c,
                  std::string &err);
 }  // namespace rt0h

@@ -72,7 +72,6 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
   if (k.defer && k.walk) o << "#define RT0_NEE_WALK 1\n";
   if (k.bvh_stack > 0 && k.stack16) o << "#define RT0_BVH_STACK16 1\n";
-  if (k.bvh_stack > 0 && k.bvh4) o << "#define RT0_BVH4 1\n";
   if (k.wf) o << "#define RT0_WAVEFRONT 1\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
@@ -164,11 +163,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // <= 64 VGPRs (8 waves) and are left alone.  A deferred ReSTIR pass kernel
   // holds no reservoir code and is left to the compiler unless it walks a BVH;
   // its light-sampling kernel takes the ReSTIR targets.
-  const char *w_env = getenv("RT0_JIT_WAVES_PER_EU");  // tuning knobs: occupancy targets
-  const char *wn_env = getenv("RT0_JIT_NEE_WAVES_PER_EU");
-  if (w_env)
-    o << "__attribute__((amdgpu_waves_per_eu(" << atoi(w_env) << "))) ";
-  else if (k.wf && k.restir)  // (the wavefront ReSTIR shade kernel walks no BVH: left to the compiler)
+  // (occupancy targets re-measured in rounds 4 and 5: DESIGN 4.13)
+  if (k.wf && k.restir)  // (the wavefront ReSTIR shade kernel walks no BVH: left to the compiler)
     ;
   else if (s.n_models > 0)  // with 16-bit stack entries the LDS allows 8: C5 9.14 vs 9.38 ms per pass at 6
     o << "__attribute__((amdgpu_waves_per_eu(" << (k.stack16 && k.bvh_stack > 0 ? 8 : 6) << "))) ";
@@ -184,7 +180,6 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_wf_plan(const LaunchParams P) { "
          "rt0::wf_plan_body(P); }\n";
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
-    if (const char *e = getenv("RT0_JIT_MARCH_WAVES_PER_EU")) o << "__attribute__((amdgpu_waves_per_eu(" << atoi(e) << "))) ";
     if (k.restir)
       o << "void rt0_jit_wf_walk(const LaunchParams P) { rt0::wf_walk_body(P); }\n";
     else
@@ -198,9 +193,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   }
   if (k.defer) {
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
-    if (wn_env)
-      o << "__attribute__((amdgpu_waves_per_eu(" << atoi(wn_env) << "))) ";
-    else if (s.n_models > 0 && !k.walk)  // it walks the BVH itself
+    if (s.n_models > 0 && !k.walk)  // it walks the BVH itself
       o << "__attribute__((amdgpu_waves_per_eu(6))) ";
     else
       o << "__attribute__((amdgpu_waves_per_eu(4))) ";
@@ -505,8 +498,7 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     const char *d = getenv("RT0_DEFER_NEE");
     key.defer = key.restir && key.max_bounces > 0 && key.max_bounces <= RT0_NEE_MAX_BOUNCES && (!d || atoi(d) != 0);
     // (the host also needs a built BVH; here the scene's TRIANGLE entries decide)
-    const char *wk = getenv("RT0_NEE_WALK");
-    key.walk = key.defer && nm > 0 && ns == 0 && !s.any_tex && !(key.flags & F_ANIM) && (!wk || atoi(wk) != 0) ? 1 : 0;
+    key.walk = key.defer && nm > 0 && ns == 0 && !s.any_tex && !(key.flags & F_ANIM) ? 1 : 0;
     // (the tree's depth and size are unknown here: RT0_BVH_STACK16=1 and
     // RT0_JIT_STACK=<entries> select what rt0_render would for such a tree)
     // the wavefront rounds rt0_render uses for such a scene (rt0_host.cpp wf_eligible)
@@ -524,8 +516,6 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     const char *w16 = getenv("RT0_BVH_STACK16"), *st = getenv("RT0_JIT_STACK");
     key.stack16 = w16 && atoi(w16) != 0 ? 1 : 0;
     if (st && nm > 0) key.bvh_stack = atoi(st);
-    const char *b4 = getenv("RT0_BVH4");
-    key.bvh4 = nm > 0 && key.bvh_stack > 0 && b4 && atoi(b4) != 0 ? 1 : 0;
     rc = rt0h::jit_compile(rt0h::jit_source(s, key), code, e);
   }
   if (code_size) *code_size = code.size();

@@ -30,6 +30,7 @@ class AddonBackend {
     this.h = this.a.create(width, height, device);
   }
   setExecutorCompat(on) { this.a.setExecutorCompat(this.h, on); }
+  setTextureFilter(mode) { this.a.setTextureFilter(this.h, mode); }
   setCubemap(size, faces) { this.a.setCubemap(this.h, size, faces); }
   setTexture(unit, w, h, data) { this.a.setTexture(this.h, unit, w, h, data); }
   setConfig(defines, constants) { this.a.setConfig(this.h, defines, constants); }
@@ -169,6 +170,12 @@ class GlslViewport {
     // opts.executorCompat: ReSTIR reservoirs as the reference's GLES executor
     // stores them (rt0_set_executor_compat); default GLSL semantics
     if (opts.executorCompat) this._b.setExecutorCompat(true);
+    // opts.textureFilter: 1 the executor's fixed-point filter (the HIP
+    // backend's default), 0 exact fp32 bilinear (rt0_set_texture_filter)
+    if (opts.textureFilter !== undefined) {
+      if (!this._b.setTextureFilter) throw new Error('opts.textureFilter: not supported by the ' + this.backend + ' backend');
+      this._b.setTextureFilter(opts.textureFilter);
+    }
     this._compiled = null;
     this.images = {};
     // index.js:256-296: the RGBA noise image (u_rnd_tex) and opts.textures[0..3]

@@ -273,6 +273,16 @@ static napi_value SetExecutorCompat(napi_env env, napi_callback_info info) {
   return nullptr;
 }
 
+static napi_value SetTextureFilter(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return nullptr;
+  CTX_OR_THROW(argv[0]);
+  int32_t mode = 1;
+  napi_get_value_int32(env, argv[1], &mode);
+  RC_OR_THROW(rt0_set_texture_filter(c, mode));
+  return nullptr;
+}
+
 static napi_value ReadAccum(napi_env env, napi_callback_info info) {
   napi_value argv[1];
   if (!get_args(env, info, 1, argv)) return nullptr;
@@ -518,6 +528,7 @@ static napi_value Init(napi_env env, napi_value exports) {
       {"render", nullptr, Render, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setTemporalFrames", nullptr, SetTemporalFrames, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setExecutorCompat", nullptr, SetExecutorCompat, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setTextureFilter", nullptr, SetTextureFilter, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setViewport", nullptr, SetViewport, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"readAccum", nullptr, ReadAccum, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"tonemap", nullptr, Tonemap, nullptr, nullptr, nullptr, napi_default, nullptr},

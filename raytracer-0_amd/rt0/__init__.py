@@ -29,13 +29,14 @@ EXPORTS = ["rt0_create", "rt0_destroy", "rt0_last_error", "rt0_parse_config", "r
            "rt0_render_async", "rt0_sync", "rt0_read_accum", "rt0_write_accum", "rt0_clear", "rt0_resize",
            "rt0_get_size", "rt0_tonemap", "rt0_read_restir", "rt0_write_restir_inputs", "rt0_set_shard",
            "rt0_device_accum", "rt0_set_accum_buffer", "rt0_set_accum_buffer_compact", "rt0_set_restir_buffers", "rt0_device_restir",
-           "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_set_executor_compat", "rt0_set_defer_light_sampling", "rt0_set_wavefront", "rt0_jit_compile", "rt0_set_counting",
+           "rt0_set_halo", "rt0_read_halo_misses", "rt0_set_jit", "rt0_set_executor_compat", "rt0_set_texture_filter", "rt0_set_defer_light_sampling", "rt0_set_wavefront", "rt0_jit_compile", "rt0_set_counting",
            "rt0_read_counters", "rt0_read_counters_n", "rt0_last_kernel_ms", "rt0_last_render_path", "rt0_version", "rt0_tonemap_ex", "rt0_png_decode", "rt0_png_read",
            "rt0_png_write", "rt0_pfm_write", "rt0_free", "rt0_set_texture", "rt0_set_cubemap", "rt0_jpeg_decode", "rt0_jpeg_read", "rt0_set_model", "rt0_model_info", "rt0_obj_read",
            "rt0_set_temporal_frames", "rt0_set_viewport", "rt0_scratch_bytes"]
 
 TEX_NOISE = 4  # RT0_TEX_NOISE: the u_rnd_tex unit of rt0_set_texture
 TONEMAP_GAMMA, TONEMAP_ACES, TONEMAP_REINHARD = 0, 1, 2
+TEX_FILTER_FLOAT, TEX_FILTER_FIXED16 = 0, 1  # rt0_set_texture_filter
 
 
 class Rt0Error(RuntimeError):
@@ -127,6 +128,7 @@ def lib():
         "rt0_read_halo_misses": (c_int, [c_void_p, P(ctypes.c_uint32), c_int]),
         "rt0_set_jit": (c_int, [c_void_p, c_int]),
         "rt0_set_executor_compat": (c_int, [c_void_p, c_int]),
+        "rt0_set_texture_filter": (c_int, [c_void_p, c_int]),
         "rt0_set_defer_light_sampling": (c_int, [c_void_p, c_int]),
         "rt0_set_wavefront": (c_int, [c_void_p, c_int]),
         "rt0_jit_compile": (c_int, [ctypes.c_char_p, P(ctypes.c_char_p), c_int, P(Config), P(ctypes.c_size_t),
@@ -532,6 +534,12 @@ class Renderer:
         `break` (rt0_set_executor_compat); default off = GLSL semantics."""
         self._chk(lib().rt0_set_executor_compat(self.h, int(bool(on))))
 
+    def set_texture_filter(self, mode):
+        """GL_LINEAR of the RGBA8 asset / noise textures (rt0_set_texture_filter):
+        TEX_FILTER_FIXED16 (default, the reference executor's fixed-point
+        filter) or TEX_FILTER_FLOAT (exact fp32 bilinear)."""
+        self._chk(lib().rt0_set_texture_filter(self.h, int(mode)))
+
     def set_defer_light_sampling(self, on):
         """Deferred ReSTIR light sampling (rt0_set_defer_light_sampling);
         default on."""
@@ -621,6 +629,8 @@ class GlslViewport:
         self.renderer = Renderer(self.width, self.height, device)
         if opts.get("executorCompat"):  # reservoirs as the reference's GLES executor stores them
             self.renderer.set_executor_compat(True)
+        if opts.get("textureFilter") is not None:  # TEX_FILTER_FIXED16 (default) / TEX_FILTER_FLOAT
+            self.renderer.set_texture_filter(opts["textureFilter"])
         self._compiled = None
         self.images = {}
         # index.js:256-296: noise image (u_rnd_tex) + opts.textures[0..3]; paths or uint8 arrays

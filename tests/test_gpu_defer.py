@@ -238,3 +238,58 @@ def test_split_pass_is_bit_identical(name, size, viewport, cfgs, monkeypatch, gp
         for x, y in zip(out[0], o):
             assert np.array_equal(x, y)
     assert out[1][0][..., :3].mean() > 0.0
+
+
+@pytest.mark.gpu
+def test_split_then_unsplit_on_one_context(cfgs, monkeypatch, gpu_required):
+    """One context renders split passes (4 row parts: the walk buffers padded
+    for the parts' rounded wave counts), is resized smaller, renders unsplit
+    passes, then a 16-row tile (grid.y == 1, never split).  The unsplit walk launch rounds its wave
+    count up to whole workgroups; its padding waves must stop at the exact
+    light-sampling wave count and not walk the counts an earlier split pass
+    left in the padded entries.  Each stage equals a fresh context's render."""
+    import test_models as T
+    cfg = T.cfg_by_name(cfgs, "c5_spectral_models")
+    vp = (0, 24, 80, 16)
+
+    def run(r, split, frames, viewport=None):
+        monkeypatch.setenv("RT0_RESTIR_SPLIT", split)
+        if viewport:
+            r.set_viewport(*viewport)
+            r.clear()
+        for k in frames:
+            r.render(k, 1)
+        return r.read_accum(), r.read_restir(0)[0]
+
+    # 80x96: 60 light-sampling waves, all walk counts written by the split
+    # passes; 80x80 then has 50, and its unsplit walk launch 52 waves
+    r = T.make(cfg, cfgs, 80, 96)
+    run(r, "4", (1, 2))
+    r.resize(80, 80)
+    got = run(r, "0", (1, 2, 3))
+    got_tile = run(r, "0", (1, 2), vp)
+    f = T.make(cfg, cfgs, 80, 80)
+    want = run(f, "0", (1, 2, 3))
+    f.close()
+    f = T.make(cfg, cfgs, 80, 80)
+    want_tile = run(f, "0", (1, 2), vp)
+    for x, y in zip(got + got_tile, want + want_tile):
+        assert np.array_equal(x, y)
+    assert want_tile[0][24:40, :, :3].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("streams", ["1", "3", "4"])
+def test_wavefront_stream_count_is_bit_identical(streams, cfgs, monkeypatch, gpu_required):
+    """The wavefront rounds' slot halves on 1, 3 or 4 streams (RT0_WF_STREAMS;
+    default 2) only change which half holds a slot: the same bits."""
+    def go():
+        r = rt0.Renderer(80, 64)
+        configure(r, cfg_by_name(cfgs, "c4_mandelbulb_vol"), cfgs)
+        r.render(1, 3)
+        assert r.last_render_path() == "wavefront"
+        return r.read_accum()
+    monkeypatch.setenv("RT0_WF_STREAMS", "2")
+    a = go()
+    monkeypatch.setenv("RT0_WF_STREAMS", streams)
+    assert np.array_equal(a, go())

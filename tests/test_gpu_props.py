@@ -425,3 +425,30 @@ def test_glslviewport_toggle_restir(cfgs, gpu_required):
     assert np.isfinite(after).all() and not np.array_equal(after, before)
     info = vp.getReSTIRDebugInfo()
     assert info["passes"] == 3 and info["isReSTIREnabled"] is False and info["temporalFrames"] == 5
+
+
+@pytest.mark.parametrize("var,val,name,want", [("RT0_JIT", "0", "c2_cornell_mis_8", "aot"),
+                                               ("RT0_DEFER_NEE", "0", "c3_outdoor_restir", "pass"),
+                                               ("RT0_WAVEFRONT", "0", "sdf_cone", "pass"),
+                                               ("RT0_SEGV_TRACE", "1", "c1_cornell_cos", "pass")])
+def test_environment_switches_at_create(cfgs, monkeypatch, gpu_required, var, val, name, want):
+    """The environment switches include/rt0.h documents, read at rt0_create:
+    RT0_JIT=0 (ahead-of-time kernels), RT0_DEFER_NEE=0 (inline ReSTIR light
+    sampling), RT0_WAVEFRONT=0 (the pass kernel for SDF scenes) and
+    RT0_SEGV_TRACE=1 (a native stack on SIGSEGV; chains to the previous
+    handler) -- each changes which kernels run, never the image beyond the
+    documented tolerances."""
+    cfg = cfg_by_name(cfgs, name)
+
+    def go():
+        r = rt0.Renderer(32, 32)
+        rt0.configure(r, cfg, cfgs)
+        r.render(1, 2)
+        return r.read_accum(), r.last_render_path()
+    base, bp = go()
+    monkeypatch.setenv(var, val)
+    got, gp = go()
+    assert gp == want, (var, gp)
+    assert np.isfinite(got).all() and got[..., :3].any()
+    ok = (np.abs(got - base) <= 1e-3 * np.maximum(1.0, np.abs(base))).all(-1)
+    assert ok.mean() >= 0.97, (var, bp, gp, ok.mean())

@@ -27,11 +27,17 @@ WF_SCENES = ["c4_mandelbulb_vol", "c4_mandelbulb_deep", "c4_mandelbulb_deep_novo
              "page_scene0_slabfirst"]
 
 
-def render(cfgs, name, wf, w=64, h=64, frames=(1, 3), env=None):
+def render(cfgs, name, wf, w=64, h=64, frames=(1, 3), env=None, sample_lights=None, scratch=None):
     r = rt0.Renderer(w, h)
     configure(r, cfg_by_name(cfgs, name), cfgs)
+    if sample_lights is not None:
+        c = r.get_config()
+        c.sample_lights = sample_lights
+        r.set_config(c)
     r.set_wavefront(wf)
     r.render(*frames)
+    if scratch is not None:
+        scratch.append(r.samples_bytes())
     return r.read_accum(), r.last_render_path()
 
 
@@ -95,6 +101,51 @@ def test_wavefront_frame_chunks_exact(cfgs, gpu_required, monkeypatch):
     monkeypatch.setenv("RT0_WF_BYTES", str(64 * 64 * 400))  # ~1 frame per chunk
     b, _ = render(cfgs, name, True, 64, 64, (1, 4))
     assert np.array_equal(a, b)
+
+
+def test_wavefront_slot_chunks_bound_memory(cfgs, gpu_required, monkeypatch):
+    """A frame whose path slots exceed RT0_WF_BYTES (e.g. 4096^2 with 32
+    lights) runs as chunks of whole regions within the frame instead of
+    allocating the frame: the same bits, and the context's scratch stays
+    within the budget (rt0_scratch_bytes counts the rounds' state)."""
+    name = "c4_mandelbulb_deep"
+    a, _ = render(cfgs, name, True, 96, 96, (1, 3))
+    budget = 96 * 96 * 200 // 3  # about a third of one frame's slots
+    monkeypatch.setenv("RT0_WF_BYTES", str(budget))
+    sc = []
+    b, p = render(cfgs, name, True, 96, 96, (1, 3), scratch=sc)
+    assert p == "wavefront"
+    assert np.array_equal(a, b)
+    # state of K halves of a chunk + 3 frames of samples, nothing frame-sized besides
+    assert sc[0] <= 2 * budget + 3 * 96 * 96 * 16, sc
+
+
+def test_wavefront_state_released_on_pass_kernel(cfgs, gpu_required):
+    """A context that leaves the wavefront path frees the rounds' state."""
+    r = rt0.Renderer(64, 64)
+    configure(r, cfg_by_name(cfgs, "sdf_cone"), cfgs)
+    r.render(1, 2)
+    with_wf = r.samples_bytes()
+    r.set_wavefront(0)
+    r.render(3, 1)
+    assert r.last_render_path() == "pass"
+    assert r.samples_bytes() < with_wf - 64 * 64 * 100, (with_wf, r.samples_bytes())
+
+
+@pytest.mark.parametrize("name", ["c4_mandelbulb_deep_novol", "c4_mandelbulb_vol", "menger_coat", "sdf_cone",
+                                  "mis_demo_sdfbox"])
+def test_wavefront_bitwise_without_light_sampling(name, cfgs, gpu_required):
+    """With sample_lights = 0 nothing is summed in another order (no NEE
+    terms): every sample is the march answers (t, calcNormal's normal, the
+    SDF id) fed through the same bounce code, so the wavefront image must
+    equal the pass kernel's bit for bit -- the march kernel's map() steps,
+    bound tests and normal probes are the pass kernel's."""
+    a, pa = render(cfgs, name, True, sample_lights=0)
+    b, pb = render(cfgs, name, False, sample_lights=0)
+    assert pa == "wavefront" and pb == "pass", (pa, pb)
+    assert np.isfinite(a).all() and a[..., :3].any()
+    same = (a[..., :3] == b[..., :3]).all(-1)
+    assert same.all(), (name, same.mean(), np.argwhere(~same)[:5].tolist())
 
 
 def test_wavefront_shards_and_viewport_exact(cfgs, gpu_required):

@@ -200,7 +200,12 @@ def test_jit_walk_module_for_model_scenes(cfgs, tmp_path, monkeypatch):
     # rt0_set_wavefront(2): wavefront rounds (rt0_jit_wf_shade, _wf_plan, the
     # closest-hit walk rt0_jit_wf_walk), then the deferred-pass kernels
     monkeypatch.setenv("RT0_WAVEFRONT", "2")
+    # RT0_JIT_EXTRA: extra hipRTC options (the measurement scripts' probes,
+    # scripts/jit_trans_sites.py), recorded in the source and so in the cache key
+    monkeypatch.setenv("RT0_JIT_EXTRA", "-DRT0_TEST_EXTRA_OPTION=1")
     co, lds = compile_lds()
+    assert "// options: -DRT0_TEST_EXTRA_OPTION=1" in open(co[:-3] + ".hip").read()
+    monkeypatch.delenv("RT0_JIT_EXTRA")
     assert {"rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_walk", "rt0_jit_nee", "rt0_jit_walk",
             "rt0_jit_resolve"} <= set(lds) and "rt0_jit_pass" not in lds, lds
     assert 256 * 24 * 2 <= lds["rt0_jit_wf_walk"] <= 256 * 24 * 2 + 2048  # the stack + the plan prefix
