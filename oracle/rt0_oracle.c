@@ -213,7 +213,11 @@ typedef struct {
   float fcx, fcy; /* gl_FragCoord.xy */
   int diff_b, spec_b, trans_b, scat_ev;
   int last_depth, first_scat; /* RT0_DEBUG_PATHS */
-  float dbg_hist, dbg_ev;      /* RT0_DEBUG_PATHS: depth history (base 16), loop-exit events (base 8) */
+  /* RT0_DEBUG_PATHS: bounce-loop iterations, depth history (base 16, six
+   * iterations per float: dbg_hist[(i-1)/6]) and loop-exit events (base 8,
+   * eight per float: dbg_ev[(i-1)/8]) -- every field an integer < 2^24, exact
+   * in fp32 (make_golden.py instrument_paths writes the same) */
+  float dbg_pit, dbg_hist[3], dbg_ev[2];
   int q0_iters;                /* SWIFTSHADER_QUAD_LIGHTS: bounce-loop iterations of the quad's first lane (-1: this is it) */
   unsigned nee_mask;           /* bounces at which this lane ran brdf's light loop (bit d) */
   unsigned q0_nee_mask;        /* the quad's first lane's nee_mask */
@@ -1377,6 +1381,12 @@ static int trace_pixel(const Frag *F) {
   return tx >= 0 && F->fcx == (float)tx + 0.5f && F->fcy == (float)ty + 0.5f;
 }
 
+/* RT0_DEBUG_PATHS: the exit event of the current bounce-loop iteration */
+static inline void dbg_event(Frag *F, float e) {
+  float *v = &F->dbg_ev[F->dbg_pit <= 8.0f ? 0 : 1];
+  *v = *v * 8.0f + e;
+}
+
 /* radiance(), raytracer.glsl:1986-2105 */
 static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
   const Oracle *o = F->o;
@@ -1389,7 +1399,11 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
     F->cur_depth = depth;
     F->n_iter++;
     F->last_depth = depth;
-    F->dbg_hist = F->dbg_hist * 16.0f + (float)depth;
+    F->dbg_pit += 1.0f;
+    {
+      float *h = &F->dbg_hist[F->dbg_pit <= 6.0f ? 0 : F->dbg_pit <= 12.0f ? 1 : 2];
+      *h = *h * 16.0f + (float)depth;
+    }
     Hit hit;
     float t = intersection(F, ro, rd, &hit);
     if (trace_pixel(F))
@@ -1432,7 +1446,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         if (F->first_scat < 0) F->first_scat = depth;
         int stop = (F->scat_ev >= o->max_scatter || vmaxc(mask) < 0.01f);
         if (o->ghost) ghost_brdf(F, &regs, seed);
-        if (stop) { F->dbg_ev = F->dbg_ev * 8.0f + 6.0f; break; }
+        if (stop) { dbg_event(F, 6.0f); break; }
         /* SWIFTSHADER_SCATTER0_EXIT: the reference executor (SwiftShader 4.1)
          * leaves the bounce loop at this `continue` (raytracer.glsl:2050) when
          * it is executed in the loop's first iteration: the loop body has
@@ -1443,14 +1457,14 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
          * at later iterations the same continue is honoured). */
         if (o->scatter0_exit && depth == 0) break;
         if (o->scatter_exit) break;
-        F->dbg_ev = F->dbg_ev * 8.0f + 1.0f;
+        dbg_event(F, 1.0f);
         continue;
       }
     }
     if (t == INF_T) {
       if (!spec && o->sample_lights) {
         if (o->ghost) ghost_brdf(F, &regs, seed);
-        F->dbg_ev = F->dbg_ev * 8.0f + 2.0f;
+        dbg_event(F, 2.0f);
         break;
       }
       if (o->use_cubemap) {
@@ -1462,7 +1476,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         acc = add(acc, mul(mask, sky));
       }
       if (o->ghost) ghost_brdf(F, &regs, seed);
-      F->dbg_ev = F->dbg_ev * 8.0f + 2.0f;
+      dbg_event(F, 2.0f);
       break;
     }
     const Mesh *mesh = &o->meshes[hit.index];
@@ -1481,7 +1495,7 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
       }
       acc = add(acc, muls(mul(mask, e), w));
       if (o->ghost) ghost_brdf(F, &regs, seed);
-      F->dbg_ev = F->dbg_ev * 8.0f + 3.0f;
+      dbg_event(F, 3.0f);
       break;
     }
     prev_nl = muls(hit.n, inside);
@@ -1491,15 +1505,15 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
       regs.rd = rd; regs.spec = spec;
     }
     if (vmaxc(mask) < 0.01f) {
-      F->dbg_ev = F->dbg_ev * 8.0f + 4.0f;
+      dbg_event(F, 4.0f);
       break;
     }
     if (F->diff_b >= o->max_diff || F->spec_b >= o->max_spec || F->trans_b >= o->max_trans ||
         F->scat_ev >= o->max_scatter) {
-      F->dbg_ev = F->dbg_ev * 8.0f + 5.0f;
+      dbg_event(F, 5.0f);
       break;
     }
-    F->dbg_ev = F->dbg_ev * 8.0f + 7.0f;
+    dbg_event(F, 7.0f);
   }
   return acc;
 }
@@ -1538,8 +1552,9 @@ static v3 shade_pixel(Frag *F, int px, int py) {
   F->diff_b = F->spec_b = F->trans_b = F->scat_ev = 0;
   F->last_depth = -1;
   F->first_scat = -1;
-  F->dbg_hist = 0.0f;
-  F->dbg_ev = 0.0f;
+  F->dbg_pit = 0.0f;
+  F->dbg_hist[0] = F->dbg_hist[1] = F->dbg_hist[2] = 0.0f;
+  F->dbg_ev[0] = F->dbg_ev[1] = 0.0f;
   F->hero = 550.0f;
   float stx = 2.0f * fcx / rx - 1.0f, sty = 2.0f * fcy / ry - 1.0f;
   float aspect = rx / ry;
@@ -1835,10 +1850,12 @@ int or_render_frame(void *h, unsigned frame, float *out, const float *const *res
       size_t p = ((size_t)y * o->w + x) * 4;
       out[p] = col.x; out[p + 1] = col.y; out[p + 2] = col.z; out[p + 3] = 0.0f;
       if (o->dbg_paths && !o->use_restir_def && restir_main && restir_aux) {
-        restir_main[p] = (float)(F.n_iter - it0); restir_main[p + 1] = F.dbg_hist;
-        restir_main[p + 2] = (float)F.scat_ev; restir_main[p + 3] = (float)F.diff_b;
-        restir_aux[p] = F.dbg_ev; restir_aux[p + 1] = (float)F.trans_b;
-        restir_aux[p + 2] = (float)F.first_scat; restir_aux[p + 3] = (float)F.spec_b;
+        (void)it0;
+        restir_main[p] = F.dbg_pit; restir_main[p + 1] = F.dbg_hist[0];
+        restir_main[p + 2] = F.dbg_hist[1]; restir_main[p + 3] = F.dbg_hist[2];
+        restir_aux[p] = F.dbg_ev[0]; restir_aux[p + 1] = F.dbg_ev[1];
+        restir_aux[p + 2] = (float)F.scat_ev + 256.0f * (float)F.diff_b;
+        restir_aux[p + 3] = (float)F.trans_b + 256.0f * (float)F.spec_b;
         continue;
       }
       if (restir_main) {

@@ -200,6 +200,13 @@ struct LaunchParams {
   // null: one chunk, accumulated in registers.
   int32_t frame_chunk;
   float4 *samples;
+  // Executor compatibility, rule 11 (oracle/gen/mask_kat.py QUAD LIGHTS;
+  // Integrator::light_q): per image pixel the bounces at which its path ran
+  // brdf()'s light loop (x) and a ghost call's unrolled loop (y).  quad_mode 1:
+  // this launch records them (its samples are discarded); 2: every lane
+  // reads its 2x2 quad's first lane's record; 0: neither.
+  uint2 *quad_masks;
+  int32_t quad_mode;
   // Asset textures: RGBA8 texels (R in the low byte), row 0 = t 0; null =
   // unbound unit.
   const uint32_t *tex_img[RT0_TEX_UNITS];

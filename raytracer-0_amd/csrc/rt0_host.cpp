@@ -103,6 +103,11 @@ struct rt0_ctx {
   bool use_jit = true;   // scene-specialised kernels (rt0_jit.cpp); RT0_JIT=0 disables
   bool exec_compat = false;  // rt0_set_executor_compat: F_EXEC_GHOST
   int tex_filter = RT0_TEX_FILTER_FIXED16;  // rt0_set_texture_filter: F_TEX_FIXED
+  // executor compatibility, rule 11 (Integrator::light_q): per-pixel light-loop
+  // records of a frame's recording launch, and the accumulator it writes to
+  uint2 *d_quad = nullptr;
+  float4 *d_quad_acc = nullptr;
+  size_t quad_pixels = 0;
   // the scene-specialised kernel of the current (scene, config): looked up once
   // per change instead of regenerating and hashing its source on every render
   rt0h::JitFns jit;
@@ -281,7 +286,7 @@ void rt0_destroy(rt0_ctx *c) {
   for (void *q : {(void *)c->d_walk_jobs, (void *)c->d_walk_count, (void *)c->d_walk_res})
     if (q) (void)hipFree(q);
   for (void *q : {(void *)c->d_nee_rec, (void *)c->d_nee_count, (void *)c->d_nee_out, (void *)c->d_nee_partial,
-                  (void *)c->d_nee_n, c->d_wf})
+                  (void *)c->d_nee_n, c->d_wf, (void *)c->d_quad, (void *)c->d_quad_acc})
     if (q) (void)hipFree(q);
   for (auto &t : c->d_tex)
     if (t) (void)hipFree(t);
@@ -717,10 +722,19 @@ static int choose_variant(const rt0_ctx *c) {
 // models whose light sampling has the occlusion-walk kernel (`restir_walk`:
 // render_impl's want_walk; wf_restir_shade_body).  rt0_set_wavefront(0)
 // keeps the pass kernel.
+// Executor compatibility with two or more lights and no ReSTIR: rule 11's
+// quad-shared light index (Integrator::light_q) -- each frame is a recording
+// launch and the frame's launch proper, on the pass kernel.
+static bool quad_lights_mode(const rt0_ctx *c) {
+  return c->exec_compat && !c->counting && !(c->cfg.defines & RT0_USE_RESTIR) && c->cfg.sample_lights &&
+         c->host_scene.n_lights >= 2;
+}
+
 static bool wf_eligible(const rt0_ctx *c, bool restir_walk) {
   const SceneDev &s = c->host_scene;
   const rt0_config &g = c->cfg;
   if (!c->wavefront || !c->use_jit || c->counting || g.max_bounces < 1 || g.max_bounces > 127) return false;
+  if (quad_lights_mode(c)) return false;  // (the wavefront state holds no light-loop records)
   if (g.defines & RT0_USE_RESTIR) return restir_walk && c->wavefront >= 2;
   if (s.n_sdfs <= 0 || s.n_models > 0 || s.n_lights > 32) return false;
   for (int i = s.n_meshes; i < s.n_meshes + s.n_sdfs; i++)
@@ -1177,6 +1191,43 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
     const int want = (c->counting || waves >= min_waves)
                          ? 1
                          : (int)std::min<long>(c->max_frames_per_launch, (target + waves - 1) / waves);
+    if (quad_lights_mode(c)) {
+      // rule 11: per frame, a launch that records every pixel's light-loop
+      // bounces (its samples go to a scratch accumulator; the rectangle grown
+      // to whole 2x2 quads), then the frame, each lane reading its quad's
+      // first lane's record
+      const size_t pixels = (size_t)c->W * c->H;
+      if (pixels != c->quad_pixels) {
+        for (void **q : {(void **)&c->d_quad, (void **)&c->d_quad_acc}) {
+          if (*q) HIPCHK(c, hipFree(*q));
+          *q = nullptr;
+        }
+        c->quad_pixels = 0;
+        HIPCHK(c, hipMalloc(&c->d_quad, pixels * sizeof(uint2)));
+        HIPCHK(c, hipMalloc(&c->d_quad_acc, pixels * sizeof(float4)));
+        c->quad_pixels = pixels;
+      }
+      LaunchParams rec = p;
+      rec.vp_x0 &= ~1;
+      rec.vp_y0 &= ~1;
+      rec.accum = c->d_quad_acc;
+      rec.compact = 0;
+      rec.quad_masks = c->d_quad;
+      rec.quad_mode = 1;
+      const dim3 rgrid((rec.vp_x1 - rec.vp_x0 + 15) / 16, (rec.vp_y1 - rec.vp_y0 + 15) / 16);
+      p.quad_masks = c->d_quad;
+      p.quad_mode = 2;
+      p.nframes = rec.nframes = 1;
+      p.frame_chunk = rec.frame_chunk = 1;
+      p.samples = rec.samples = nullptr;
+      for (int k = 0; k < n; ++k) {
+        p.frame0 = rec.frame0 = first + (uint32_t)k;
+        HIPCHK(c, launch(rec, 1, rgrid));
+        HIPCHK(c, launch(p, 1, grid));
+        launches++;
+      }
+      n = 0;  // (done: the loop below has nothing left)
+    }
     for (int k = 0; k < n; k += c->max_frames_per_launch) {
       p.frame0 = first + (uint32_t)k;
       p.nframes = (n - k) < c->max_frames_per_launch ? (n - k) : c->max_frames_per_launch;
@@ -1480,7 +1531,8 @@ int rt0_scratch_bytes(const rt0_ctx *c, size_t *bytes) {
   // records, results and walk jobs
   *bytes = c->samples_bytes + c->wf_bytes + c->nee_slots * sizeof(NeeRec) + c->nee_waves * sizeof(uint32_t) +
            c->nee_pixels * (c->nee_planes + 1) * sizeof(float4) + c->nee_pixels * sizeof(int32_t) +
-           c->walk_jobs_n * sizeof(WalkJob) + (c->walk_waves_n + c->walk_res_n) * sizeof(uint32_t);
+           c->walk_jobs_n * sizeof(WalkJob) + (c->walk_waves_n + c->walk_res_n) * sizeof(uint32_t) +
+           c->quad_pixels * (sizeof(uint2) + sizeof(float4));
   return RT0_OK;
 }
 

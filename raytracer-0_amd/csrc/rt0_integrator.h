@@ -1329,6 +1329,12 @@ struct Integrator {
   float gr_bounce;
   int gr_mat;
   bool gr_have, gr_spec;
+  // F_EXEC_GHOST + P.quad_mode (rule 11, light_q): this sample's pixel, the
+  // bounces at which its path ran brdf()'s light loop / a ghost call's, and
+  // its quad's first lane's (q0_on: this lane reads them)
+  int q_px = 0, q_py = 0;
+  uint32_t q_own = 0, q_gown = 0, q0_m = 0, q0_g = 0;
+  bool q0_on = false;
   // the light-sampling kernel's LDS copy of the ReSTIR candidates' light data
   // (candidate_table), or null: read from the scene tables
   const float4 *cand_lds = nullptr;
@@ -2134,7 +2140,7 @@ struct Integrator {
     } else if (flag(F_MIS) && nlights > 0) {
       const float base = nc_seed4(seed, 8652.1f, fr, 5681.123f, bounce, 7895.13f);
       for_lights(sc, [&](int i) {
-        int idx = sc.light(i);
+        int idx = light_q(i, bounce);
         if (idx < 0) return;
         const GeomRec lg = sc.geom(idx);
         const MatRec lmt = sc.mat(idx);
@@ -2155,7 +2161,7 @@ struct Integrator {
     } else {
       const float s = nc_seed4(seed, 8652.1f, fr, 5681.123f, bounce, 7895.13f);
       for_lights(sc, [&](int i) {
-        int idx = sc.light(i);
+        int idx = light_q(i, bounce);
         if (idx >= 0) acc = acc + direct_light(idx, x, nl, s);
       });
     }
@@ -2199,6 +2205,69 @@ struct Integrator {
                  nc_seed3(seed, 1234.567f, fr, gr_bounce, 9876.54f));
   }
   DEV bool ghost_on() const { return RESTIR && (C.flags() & F_EXEC_GHOST) != 0; }
+
+  // ---- executor compatibility, rule 11 (mask_kat.py QUAD LIGHTS; the
+  // restatement's quad_light_index, oracle/rt0_oracle.c): in brdf()'s light
+  // loops (raytracer.glsl:1955-1974) the reference executor reads the
+  // loop-indexed light_index[i] at the index register of the 2x2 quad's FIRST
+  // lane.  That register holds i when the first lane runs the same loop in
+  // the same bounce-loop iteration -- live, or as the ghost brdf() call of
+  // the iteration it breaks in (the plain loop unrolled, rule 5; not counted
+  // under the medium) -- and a stale value otherwise: mesh 0 (the loop's end,
+  // one past the array, reads 0), or with the medium's `continue` before the
+  // breaks (USE_VOLUMETRICS) element 0 before the first lane's first run.
+  // The first lane's record comes from a preceding launch of the same frame
+  // (P.quad_mode 1, rt0_host.cpp render_impl).  Quadric-only modules without
+  // ReSTIR; compiled out unless F_EXEC_GHOST.
+  DEV bool quad_rec() const { return !RESTIR && (C.flags() & F_EXEC_GHOST) != 0 && P.quad_mode != 0; }
+  DEV int light_q(int i, float bounce) {
+    const int li = sc.light(i);
+    if (!quad_rec()) return li;
+    const int d = (int)bounce;
+    if (d >= 32) return li;  // (32 bounces of record)
+    if (i == 0) q_own |= 1u << d;
+    if (!q0_on || sc.n_lights() < 2) return li;
+    const uint32_t m = q0_m | (flag(F_VOL) ? 0u : q0_g);
+    if ((m >> d) & 1u) return li;
+    if (flag(F_VOL) && (m & ((1u << d) - 1u)) == 0u) return sc.light(0);
+    return 0;
+  }
+  // the ghost brdf() of a `break` iteration (see ghost_brdf): its material
+  // branch on the last live call's registers; a non-specular outcome runs the
+  // plain light loop (unrolled: constant trip count <= 4)
+  DEV void quad_ghost(float seed, int depth) {
+    if (!gr_have || depth >= 32) return;
+    const MatRec mt = sc.mat(gr_mat);
+    bool spec = gr_spec;
+    if (mt.type == M_DIFF) {
+      spec = false;
+    } else if (mt.type == M_SPEC || mt.type == M_REFR_FRESNEL || mt.type == M_REFR_SCHLICK) {
+      spec = true;
+    } else if (mt.type == M_COAT) {
+      float nt_eff = fabsf(mt.nt);
+      if constexpr (SPECTRAL) {
+        if (flag(F_SPECTRAL) && mt.nt < 0.0f) nt_eff = spectral_ior(hero, fabsf(mt.nt));
+      }
+      spec = hash(seed) < schlick(gr_rd, gr_nl, 1.00029f, nt_eff);
+    }
+    if (!spec && flag(F_SAMPLE_LIGHTS) && !flag(F_RESTIR) && !(flag(F_MIS) && sc.n_lights() > 0) &&
+        sc.n_lights() <= 4)
+      q_gown |= 1u << depth;
+  }
+  DEV void quad_begin() {
+    if (!quad_rec()) return;
+    q_own = q_gown = 0u;
+    gr_have = false;
+    q0_on = P.quad_mode == 2 && ((q_px | q_py) & 1) != 0;
+    if (q0_on) {
+      const uint2 m = P.quad_masks[(size_t)(q_py & ~1) * P.width + (q_px & ~1)];
+      q0_m = m.x;
+      q0_g = m.y;
+    }
+  }
+  DEV void quad_store() const {
+    if (quad_rec() && P.quad_mode == 1) P.quad_masks[(size_t)q_py * P.width + q_px] = make_uint2(q_own, q_gown);
+  }
 
   // ---- wavefront SDF renders (WF): light sampling as march jobs
   // One shadow ray of light slot l whose answer matters: appended to this
@@ -2404,7 +2473,7 @@ struct Integrator {
       if (flag(F_MIS) && sc.n_lights() > 0) {
         for_lights(sc, [&](int i) {
           if (susp || i < nc.li) return;
-          int idx = sc.light(i);
+          int idx = light_q(i, (float)ps.depth);
           if (idx < 0) return;
           const GeomRec lg = sc.geom(idx);
           const MatRec lmt = sc.mat(idx);
@@ -2422,7 +2491,7 @@ struct Integrator {
       } else {
         for_lights(sc, [&](int i) {
           if (susp || i < nc.li) return;
-          int idx = sc.light(i);
+          int idx = light_q(i, (float)ps.depth);
           if (idx < 0) return;
           v3 dl = direct_light(idx, nc.x, nc.n, nc.seed, mq, &susp);
           if (susp) {
@@ -2520,6 +2589,7 @@ struct Integrator {
           ++scat_ev;
           if (scat_ev >= C.max_scatter() || vmaxc(mask) < 0.01f) {
             if (ghost_on()) ghost_brdf(seed);
+            else if (quad_rec()) quad_ghost(seed, depth);
             return false;
           }
           return ++ps.depth < C.max_bounces();
@@ -2528,6 +2598,7 @@ struct Integrator {
     }
     if (t == INF_T) {
       if (ghost_on()) ghost_brdf(seed);  // 2057 and 2065 both `break`
+      else if (quad_rec()) quad_ghost(seed, depth);
       if (!spec && flag(F_SAMPLE_LIGHTS)) return false;
       if (flag(F_CUBEMAP)) {  // 2059-2060 (USE_CUBEMAP wins over the procedural sky)
         const T4 cm = cube_sample(P, rd);
@@ -2581,6 +2652,7 @@ struct Integrator {
       }
       acc = acc + (mask * e) * w;
       if (ghost_on()) ghost_brdf(seed);
+      else if (quad_rec()) quad_ghost(seed, depth);
       return false;
     }
     prev_nl = hit.n * inside;
@@ -2650,6 +2722,13 @@ struct Integrator {
         ++diff_b;
         spec = false;
       }
+    }
+    if (quad_rec()) {  // brdf()'s registers for a later ghost call (quad_ghost)
+      gr_have = true;
+      gr_nl = nl;
+      gr_rd = rd;
+      gr_spec = spec;
+      gr_mat = hit.index;
     }
     if (!spec && flag(F_CUBEMAP)) {  // environment NEE, 1887-1897
       const float s = nc_addmul(seed, bounce, 965.325f);
@@ -2728,6 +2807,8 @@ struct Integrator {
   // the pixel's gl_FragCoord and the camera offset that depends on it alone
   // (once per pixel: path regeneration starts its samples with begin_sample)
   DEV void set_pixel(int px, int py) {
+    q_px = px;
+    q_py = py;
     fcx = (float)px + 0.5f;
     fcy = (float)py + 0.5f;
     stx = 2.0f * fcx / P.res_x - 1.0f;
@@ -2771,6 +2852,7 @@ struct Integrator {
       gr_have = false;
       nee_k = 0;
     }
+    quad_begin();
     ps = Path{ro, rd, mk(0.f, 0.f, 0.f), mk(1.f, 1.f, 1.f), mk(0.f, 1.f, 0.f), seed, 0, true};
   }
   // main() after radiance(): the spectral weighting (2152-2155)
@@ -2848,6 +2930,7 @@ DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int 
       if (alive && !(It::SUSP && ps.ms.active)) alive = it.step(ps);
       if (!alive) {
         accumulate(it, P, a, it.finish(ps));
+        it.quad_store();  // (rule 11's recording launch: one frame)
         if (++f >= P.nframes) break;
         it.frame = P.frame0 + (uint32_t)f;
         it.begin_sample(ps);  // same pixel: set_pixel's values stand

@@ -345,3 +345,62 @@ def test_gpu_two_light_quad_first_lanes(name, cfgs, gpu_required):
     want = np.stack([o.frame(int(k))[0] for k in frames])[..., :3]
     ok, _ = pixel_match(got, want)
     assert 1.0 - ok.mean() <= bound
+
+
+@pytest.mark.parametrize("name,bound", [("spectral_2l_novol", 0.01), ("spectral_vol_2l", 0.04)])
+def test_gpu_two_light_executor_quad_lights(name, bound, cfgs, gpu_required):
+    """Rule 11 in the product (rt0_set_executor_compat; Integrator::light_q):
+    each frame is a recording launch (every pixel's light-loop bounces) and
+    the frame proper, whose lanes read brdf's light_index[i] as the reference
+    executor does, at their 2x2 quad's first lane's index.  Against the
+    reference on ALL lanes (first lanes and the other three), and against the
+    restatement's model of the same rule (SWIFTSHADER_QUAD_LIGHTS)."""
+    if not have(name):
+        pytest.skip("fixture not generated")
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    gold = G["samples"][..., :3]
+    F, H, W = gold.shape[:3]
+    frames = G["frames"] if "frames" in G else range(1, F + 1)
+    r = make(cfgs, name, W, H)
+    r.set_executor_compat(True)
+    got = np.stack([single(r, int(k)) for k in frames])[..., :3]
+    assert r.last_render_path() == "pass"
+    valid = G["conformant"] if "conformant" in G else G["valid"] if "valid" in G else np.ones(gold.shape[:3], bool)
+    ok, _ = pixel_match(got, gold)
+    bad = 1.0 - ok[valid].mean()
+    per_lane = [1.0 - ok[:, ly::2, lx::2][valid[:, ly::2, lx::2]].mean() for ly in (0, 1) for lx in (0, 1)]
+    print("%s: %.4f of valid samples differ under compat; per quad lane %s" % (name, bad, per_lane))
+    assert bad <= bound, (name, bad, per_lane)
+    o = O.Oracle(cfg_by_name(cfgs, name), cfgs, width=W, height=H,
+                 overrides={"SWIFTSHADER_GHOST": 1, "SWIFTSHADER_QUAD_LIGHTS": 1})
+    want = np.stack([o.frame(int(k))[0] for k in frames])[..., :3]
+    ok, _ = pixel_match(got, want)
+    assert 1.0 - ok.mean() <= bound, (name, 1.0 - ok.mean())
+    # without compat: GLSL semantics, the non-first lanes depart
+    r.set_executor_compat(False)
+    plain = np.stack([single(r, int(k)) for k in frames])[..., :3]
+    okp, _ = pixel_match(plain, gold)
+    assert 1.0 - okp[valid].mean() > bad
+
+
+def test_gpu_quad_lights_tile_and_resume(cfgs, gpu_required):
+    """Rule 11's recording launch covers whole 2x2 quads of a tile whose
+    corner is odd, and a multi-pass call equals its passes one by one."""
+    name = "spectral_2l_novol"
+    cfg = cfg_by_name(cfgs, name)
+    full = make(cfgs, name, 32, 32)
+    full.set_executor_compat(True)
+    full.render(1, 3)
+    ref = full.read_accum()
+    one = make(cfgs, name, 32, 32)
+    one.set_executor_compat(True)
+    for k in (1, 2, 3):
+        one.render(k, 1)
+    assert np.array_equal(one.read_accum(), ref)
+    t = make(cfgs, name, 32, 32)
+    t.set_executor_compat(True)
+    t.set_viewport(5, 7, 20, 14)
+    t.render(1, 3)
+    got = t.read_accum()
+    assert np.array_equal(got[7:21, 5:25], ref[7:21, 5:25])
+    assert cfg["name"] == name
