@@ -230,7 +230,7 @@ void rt0_free(void *p);
 
 /* ReSTIR reservoir MRTs (raytracer.glsl:2171-2179).  which: 0 = current output
  * (restir_buffer/aux of the last pass), 1 = history1, 2 = history2.  main/aux:
- * W*H*4 floats each. */
+ * W*H*4 floats each (planes, de-interleaved from the device pairs). */
 int rt0_read_restir(rt0_ctx *ctx, int which, float *main_out, float *aux_out);
 /* Set the six ReSTIR inputs the NEXT pass reads (spatial = restir_buffer_back,
  * history1, history2; main+aux each); any pointer may be NULL = zeros. */
@@ -268,12 +268,19 @@ int rt0_set_accum_buffer_compact(rt0_ctx *ctx, void *dptr, int *rows);
  * -- one pass per rt0_render call; between passes the caller copies `rows`
  * halo rows of the newest reservoir planes across every band boundary between
  * two shards (rt0/shard.py RestirShard does it over RCCL).
- *   rt0_set_restir_buffers: 8 caller-owned W*H*4 f32 device planes (e.g.
- *     torch tensors the collective reads/writes); NULL returns to
- *     context-owned planes.  All planes are cleared.
+ *   The reservoir textures live as four interleaved main/aux PAIRS: texel i
+ *   of a pair is its main RGBA32F then its aux RGBA32F (32 B), so a
+ *   bilinear tap reads one 32-B segment per texel instead of one line in each
+ *   of two planes (rt0_integrator.h RT0_RES_STRIDE).
+ *   rt0_set_restir_buffers: caller-owned device memory (e.g. torch tensors
+ *     the collective reads/writes) for the 4 pairs, W*H*8 f32 each, given as
+ *     8 plane pointers: planes[2k] = pair k's base (its main plane),
+ *     planes[2k+1] = that base + 16 bytes (its aux plane) -- RT0_E_ARG
+ *     otherwise; NULL returns to context-owned pairs.  All pairs are cleared.
  *   rt0_device_restir: device pointers of the reservoir planes a following
  *     pass reads: which = 0 newest output (spatial input), 1 / 2 the
- *     temporal history levels.
+ *     temporal history levels; aux = main + 16 bytes (one pair; a row range
+ *     of the pair, W*32 B per row, is what a halo exchange moves).
  *   rt0_set_halo: rows of exchanged halo (valid rows around the own block).
  *   rt0_read_halo_misses: bilinear fetches that fell outside own block + halo
  *     since the last reset (non-zero = the halo was too small: the result

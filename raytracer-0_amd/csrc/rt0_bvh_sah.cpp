@@ -246,4 +246,37 @@ int bvh_build_sah(int n, const float *v, const int32_t *model, std::vector<BvhNo
   return depth;
 }
 
+// The LDS treelet (rt0_integrator.h bvh_fetch): whole top levels of the tree,
+// breadth-first, as nodes [0, T); every other node keeps its pre-order place
+// after them.  Only the numbering changes (links follow): the same tree, the
+// same walks.
+int bvh_treelet_order(std::vector<BvhNode> &nodes, int max_nodes) {
+  const int n = (int)nodes.size();
+  if (n == 0 || max_nodes < 1) return 0;
+  std::vector<int> top{0};
+  for (size_t lo = 0;;) {  // top[lo..) is the deepest level taken
+    std::vector<int> next;
+    for (size_t i = lo; i < top.size(); i++)
+      for (int ch : {nodes[(size_t)top[i]].left, nodes[(size_t)top[i]].right})
+        if (ch >= 0) next.push_back(ch);
+    if (next.empty() || top.size() + next.size() > (size_t)max_nodes) break;
+    lo = top.size();
+    top.insert(top.end(), next.begin(), next.end());
+  }
+  std::vector<int> id(n, -1);
+  int k = 0;
+  for (int t : top) id[(size_t)t] = k++;
+  for (int i = 0; i < n; i++)
+    if (id[(size_t)i] < 0) id[(size_t)i] = k++;
+  std::vector<BvhNode> out((size_t)n);
+  for (int i = 0; i < n; i++) {
+    BvhNode b = nodes[(size_t)i];
+    if (b.left >= 0) b.left = id[(size_t)b.left];
+    if (b.right >= 0) b.right = id[(size_t)b.right];
+    out[(size_t)id[(size_t)i]] = b;
+  }
+  nodes.swap(out);
+  return (int)top.size();
+}
+
 }  // namespace rt0h

@@ -207,6 +207,9 @@ struct LaunchParams {
   // reads its 2x2 quad's first lane's record; 0: neither.
   uint2 *quad_masks;
   int32_t quad_mode;
+  // BVH nodes [0, treelet) are the tree's top levels, staged in LDS by the
+  // scene-specialised kernels that walk it (rt0_integrator.h bvh_fetch)
+  int32_t treelet;
   // Asset textures: RGBA8 texels (R in the low byte), row 0 = t 0; null =
   // unbound unit.
   const uint32_t *tex_img[RT0_TEX_UNITS];

@@ -38,10 +38,20 @@ extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_mo
 // shards, against 0.89 / 0.78 / 0.61 unchunked).
 static const long kTargetWaves = 16384;
 static const long kChunkWaves = 65536;
+// BVH nodes staged in LDS by the scene-specialised kernels (rt0_jit.cpp
+// RT0_TREELET): 64 x 64 B = 4 KiB per workgroup, whole top levels (63 nodes:
+// six levels of a full tree) -- with the 12 KiB traversal stack the pass
+// kernel still holds 8 workgroups per CU in 160 KiB
+static const int kTreeletNodes = 64;
 // pass-wave record regions per light-sampling wave (JitKey::nee_regions)
 static long nee_regions_per_wave() { return 2L; }
 
 enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
+// The reservoir textures are four interleaved pair buffers (rt0_integrator.h
+// RT0_RES_STRIDE): d_restir[2k] = a pair's base = its main plane (texel i at
+// float4 2i), d_restir[2k + 1] = base + 1 float4 = its aux plane.  The swap
+// chain moves main and aux pointers together, so every pair stays a pair.
+static float4 *pair_aux(float4 *base) { return base + 1; }
 
 struct rt0_ctx {
   int device = 0;
@@ -63,6 +73,7 @@ struct rt0_ctx {
   BvhNode *d_bvh = nullptr;
   TriDev *d_tris = nullptr;
   int n_tris = 0, bvh_depth = 0;
+  int treelet = 0;  // leading BVH nodes staged in LDS (bvh_treelet_order; 0: LBVH build)
   SceneDev *d_scene = nullptr;
   float cam_pos[3] = {0.f, 0.f, 2.8f}, cam_look[3] = {0.f, 0.f, -1.f}, cam_params[3] = {50.f, 0.f, 3.5f};
   float4 *d_accum = nullptr;
@@ -152,10 +163,9 @@ static int fail(rt0_ctx *c, int code, const std::string &msg) {
 
 static void free_buffers(rt0_ctx *c) {
   if (c->d_accum) (void)hipFree(c->d_accum);
-  for (auto &p : c->d_restir) {
-    if (p && !c->ext_restir) (void)hipFree(p);
-    p = nullptr;
-  }
+  for (int i = 0; i < R_COUNT; i += 2)  // (the pair bases)
+    if (c->d_restir[i] && !c->ext_restir) (void)hipFree(c->d_restir[i]);
+  for (auto &p : c->d_restir) p = nullptr;
   c->ext_restir = false;
   if (c->d_tonemap) (void)hipFree(c->d_tonemap);
   c->d_accum = nullptr;
@@ -165,7 +175,10 @@ static void free_buffers(rt0_ctx *c) {
 static int alloc_buffers(rt0_ctx *c, int w, int h) {
   size_t n = (size_t)w * h;
   HIPCHK(c, hipMalloc(&c->d_accum, n * sizeof(float4)));
-  for (auto &p : c->d_restir) HIPCHK(c, hipMalloc(&p, n * sizeof(float4)));
+  for (int i = 0; i < R_COUNT; i += 2) {
+    HIPCHK(c, hipMalloc(&c->d_restir[i], 2 * n * sizeof(float4)));
+    c->d_restir[i + 1] = pair_aux(c->d_restir[i]);
+  }
   HIPCHK(c, hipMalloc(&c->d_tonemap, n * sizeof(uchar4)));
   c->W = w;
   c->H = h;
@@ -175,7 +188,7 @@ static int alloc_buffers(rt0_ctx *c, int w, int h) {
 static int clear_buffers(rt0_ctx *c) {
   size_t n = (size_t)c->W * c->H * sizeof(float4);
   HIPCHK(c, hipMemsetAsync(c->acc(), 0, (size_t)c->W * c->accum_rows() * sizeof(float4), c->stream));
-  for (auto &p : c->d_restir) HIPCHK(c, hipMemsetAsync(p, 0, n, c->stream));
+  for (int i = 0; i < R_COUNT; i += 2) HIPCHK(c, hipMemsetAsync(c->d_restir[i], 0, 2 * n, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return RT0_OK;
 }
@@ -518,6 +531,7 @@ static int build_bvh(rt0_ctx *c) {
   c->d_tris = nullptr;
   c->n_tris = 0;
   c->bvh_depth = 0;
+  c->treelet = 0;
   if (n == 0) return RT0_OK;
   HIPCHK(c, hipMalloc(&c->d_bvh, (size_t)std::max(1, n - 1) * sizeof(BvhNode)));
   HIPCHK(c, hipMalloc(&c->d_tris, (size_t)n * sizeof(TriDev)));
@@ -526,6 +540,7 @@ static int build_bvh(rt0_ctx *c) {
     std::vector<BvhNode> nodes;
     std::vector<TriDev> tris;
     depth = rt0h::bvh_build_sah(n, v.data(), owner.data(), nodes, tris);
+    c->treelet = rt0h::bvh_treelet_order(nodes, kTreeletNodes);
     HIPCHK(c, hipMemcpy(c->d_bvh, nodes.data(), nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_tris, tris.data(), tris.size() * sizeof(TriDev), hipMemcpyHostToDevice));
   } else {
@@ -678,6 +693,7 @@ static void fill_params(rt0_ctx *c, LaunchParams &p) {
   p.bvh = c->d_bvh;
   p.tris = c->d_tris;
   p.n_tris = c->n_tris;
+  p.treelet = c->treelet;
   p.accum = c->acc();
   p.compact = c->compact ? 1 : 0;
   p.counters = c->d_counters;
@@ -1385,9 +1401,13 @@ int rt0_read_restir(rt0_ctx *c, int which, float *main_out, float *aux_out) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // after the swap, the last pass's output sits in restir_buffer_back (index.js:817-819)
   const int mi = which == 0 ? R_BACK_MAIN : which == 1 ? R_H1 : R_H2;
-  size_t bytes = (size_t)c->W * c->H * sizeof(float4);
-  if (main_out) HIPCHK(c, hipMemcpy(main_out, c->d_restir[mi], bytes, hipMemcpyDeviceToHost));
-  if (aux_out) HIPCHK(c, hipMemcpy(aux_out, c->d_restir[mi + 1], bytes, hipMemcpyDeviceToHost));
+  const size_t n = (size_t)c->W * c->H;
+  std::vector<float4> pair(2 * n);  // the interleaved pair, split on the host
+  HIPCHK(c, hipMemcpy(pair.data(), c->d_restir[mi], 2 * n * sizeof(float4), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n; i++) {
+    if (main_out) memcpy(main_out + 4 * i, &pair[2 * i], sizeof(float4));
+    if (aux_out) memcpy(aux_out + 4 * i, &pair[2 * i + 1], sizeof(float4));
+  }
   return RT0_OK;
 }
 
@@ -1396,12 +1416,19 @@ int rt0_write_restir_inputs(rt0_ctx *c, const float *sm, const float *sa, const 
   if (!c) return RT0_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+  const size_t n = (size_t)c->W * c->H;
   const float *src[6] = {sm, sa, h1m, h1a, h2m, h2a};
   const int dst[6] = {R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A};
-  for (int i = 0; i < 6; i++) {
-    if (src[i]) HIPCHK(c, hipMemcpy(c->d_restir[dst[i]], src[i], bytes, hipMemcpyHostToDevice));
-    else HIPCHK(c, hipMemset(c->d_restir[dst[i]], 0, bytes));
+  std::vector<float4> pair(2 * n);  // interleaved on the host (zeros where a plane is NULL)
+  for (int k = 0; k < 6; k += 2) {
+    for (size_t i = 0; i < n; i++) {
+      pair[2 * i] = src[k] ? make_float4(src[k][4 * i], src[k][4 * i + 1], src[k][4 * i + 2], src[k][4 * i + 3])
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      pair[2 * i + 1] = src[k + 1] ? make_float4(src[k + 1][4 * i], src[k + 1][4 * i + 1], src[k + 1][4 * i + 2],
+                                                 src[k + 1][4 * i + 3])
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    HIPCHK(c, hipMemcpy(c->d_restir[dst[k]], pair.data(), 2 * n * sizeof(float4), hipMemcpyHostToDevice));
   }
   return RT0_OK;
 }
@@ -1466,19 +1493,26 @@ int rt0_set_restir_buffers(rt0_ctx *c, void *const planes[8]) {
   if (!c) return RT0_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const size_t bytes = (size_t)c->W * c->H * sizeof(float4);
+  const size_t bytes = (size_t)c->W * c->H * 2 * sizeof(float4);  // one pair buffer
   if (planes) {
-    for (int i = 0; i < R_COUNT; i++)
-      if (!planes[i]) return fail(c, RT0_E_ARG, "rt0_set_restir_buffers: null plane");
+    for (int i = 0; i < R_COUNT; i += 2) {
+      if (!planes[i] || !planes[i + 1]) return fail(c, RT0_E_ARG, "rt0_set_restir_buffers: null plane");
+      if ((char *)planes[i + 1] != (char *)planes[i] + 16)
+        return fail(c, RT0_E_ARG, "rt0_set_restir_buffers: planes[2k+1] must be planes[2k] + 16 bytes "
+                                  "(interleaved main/aux pairs, W*H*8 floats each)");
+    }
     if (!c->ext_restir)
-      for (auto &p : c->d_restir) (void)hipFree(p);
+      for (int i = 0; i < R_COUNT; i += 2) (void)hipFree(c->d_restir[i]);
     for (int i = 0; i < R_COUNT; i++) c->d_restir[i] = (float4 *)planes[i];
     c->ext_restir = true;
   } else if (c->ext_restir) {  // back to planes owned by the context
-    for (auto &p : c->d_restir) HIPCHK(c, hipMalloc(&p, bytes));
+    for (int i = 0; i < R_COUNT; i += 2) {
+      HIPCHK(c, hipMalloc(&c->d_restir[i], bytes));
+      c->d_restir[i + 1] = pair_aux(c->d_restir[i]);
+    }
     c->ext_restir = false;
   }
-  for (auto &p : c->d_restir) HIPCHK(c, hipMemsetAsync(p, 0, bytes, c->stream));
+  for (int i = 0; i < R_COUNT; i += 2) HIPCHK(c, hipMemsetAsync(c->d_restir[i], 0, bytes, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return RT0_OK;
 }

@@ -116,6 +116,14 @@ DEV float flog(float x) { return __logf(x); }
 #ifndef RT0_WALK_SPEC  // rt0_jit_walk postpones leaf tests until half the busy lanes hold one
 #define RT0_WALK_SPEC 1
 #endif
+// ReSTIR reservoir textures (index.js:149-163) as interleaved pairs: texel i
+// of a main plane at float4 2i of its pair buffer, the aux plane's at 2i + 1
+// (rt0_host.cpp alloc_buffers), so a bilinear tap's main and aux texels share
+// 32-B segments instead of touching two planes' lines
+#define RT0_RES_STRIDE 2
+#ifndef RT0_TREELET  // BVH nodes (top levels) each traversing kernel stages in LDS (bvh_fetch); 0 = none
+#define RT0_TREELET 0
+#endif
 #ifndef RT0_BVH_STACK16  // BVH traversal stacks as 16-bit LDS entries + high bits in a register
 #define RT0_BVH_STACK16 0
 #endif
@@ -391,6 +399,48 @@ DEV float box_enter(float x0, float y0, float z0, float x1, float y1, float z1, 
   const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
   return (tn <= tf && tn < tmin) ? tn : F_INF;
 }
+// The BVH's top levels in LDS (RT0_TREELET nodes of capacity; the
+// scene-specialised modules of scenes with triangle models): the host numbers
+// every node of the top levels breadth-first first (rt0_bvh_sah.cpp
+// bvh_treelet_order: P.treelet of them, the rest in pre-order), every kernel
+// that walks the tree copies them to LDS at its start (treelet_load), and a
+// walk's first dependent node loads -- the same few nodes for every ray --
+// are LDS reads instead of L2 round trips.  Same nodes, same order: the same
+// hits bit for bit.
+DEV float4 *treelet_lds() {
+  __shared__ float4 t[4 * (RT0_TREELET > 0 ? RT0_TREELET : 1)];
+  return t;
+}
+// (every thread of the block, before any leaves: one barrier)
+DEV void treelet_load(const LaunchParams &P) {
+#if RT0_TREELET > 0
+  const int n = 4 * min(P.treelet, RT0_TREELET);
+  float4 *t = treelet_lds();
+  const float4 *__restrict__ g = reinterpret_cast<const float4 *>(P.bvh);
+  for (int i = (int)threadIdx.x; i < n; i += (int)blockDim.x) t[i] = g[i];
+  __syncthreads();
+#else
+  (void)P;
+#endif
+}
+// node `node` of the tree: both child boxes (a, b, c) and the links (lk.x, lk.y)
+DEV void bvh_fetch(const LaunchParams &P, const float4 *__restrict__ nodes, int node, float4 &a, float4 &b,
+                   float4 &c, int4 &lk) {
+#if RT0_TREELET > 0
+  if (node < P.treelet) {
+    const float4 *t = treelet_lds() + 4 * node;
+    a = t[0];
+    b = t[1];
+    c = t[2];
+    lk = reinterpret_cast<const int4 *>(t)[3];
+    return;
+  }
+#endif
+  a = nodes[4 * node];
+  b = nodes[4 * node + 1];
+  c = nodes[4 * node + 2];
+  lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+}
 // whether a ray (1/d = inv) enters neither child box of the BVH's root
 // before tmax: then every walk of it ends at its first node with no triangle
 // test (bvh_closest, walk_body), so it needs none
@@ -479,8 +529,9 @@ DEV int bvh_closest(const LaunchParams &P, v3 o, v3 d, v3 inv, float &tmin, unsi
       *complete = false;
       break;
     }
-    const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
-    const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+    float4 a, b, c;
+    int4 lk;
+    bvh_fetch(P, nodes, node, a, b, c, lk);
     float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
     float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
     const int cl = lk.x, cr = lk.y;
@@ -1614,8 +1665,9 @@ struct Integrator {
     x0 = min(max(x0, 0), P.width - 1);
     y0 = min(max(y0, 0), P.height - 1);
     if (RT0_HALO_CHECK && P.halo_miss && !(row_local(y0) && row_local(y1))) atomicAdd(P.halo_miss, 1u);
-    float4 t00 = t[(size_t)y0 * P.width + x0], t10 = t[(size_t)y0 * P.width + x1];
-    float4 t01 = t[(size_t)y1 * P.width + x0], t11 = t[(size_t)y1 * P.width + x1];
+    const size_t S = RT0_RES_STRIDE;
+    float4 t00 = t[S * ((size_t)y0 * P.width + x0)], t10 = t[S * ((size_t)y0 * P.width + x1)];
+    float4 t01 = t[S * ((size_t)y1 * P.width + x0)], t11 = t[S * ((size_t)y1 * P.width + x1)];
     return bil_lerp(t00, t10, t01, t11, a, b);
   }
   DEV static float4 bil_lerp(float4 t00, float4 t10, float4 t01, float4 t11, float a, float b) {
@@ -1657,8 +1709,9 @@ struct Integrator {
   // the bilinear main/aux reservoir pair of a tap
   DEV static void bil_fetch2(const float4 *__restrict__ tm, const float4 *__restrict__ ta, const Bil &q, float4 &m,
                              float4 &a) {
-    const float4 m00 = tm[q.i00], m10 = tm[q.i10], m01 = tm[q.i01], m11 = tm[q.i11];
-    const float4 a00 = ta[q.i00], a10 = ta[q.i10], a01 = ta[q.i01], a11 = ta[q.i11];
+    constexpr size_t S = RT0_RES_STRIDE;
+    const float4 m00 = tm[S * q.i00], m10 = tm[S * q.i10], m01 = tm[S * q.i01], m11 = tm[S * q.i11];
+    const float4 a00 = ta[S * q.i00], a10 = ta[S * q.i10], a01 = ta[S * q.i01], a11 = ta[S * q.i11];
     m = bil_lerp(m00, m10, m01, m11, q.a, q.b);
     a = bil_lerp(a00, a10, a01, a11, q.a, q.b);
   }
@@ -2944,6 +2997,7 @@ DEV void regen_pixel(const LaunchParams &P, It &it, const Cfg &cfg, int px, int 
 
 template <class Scene, class Cfg, bool RESTIR, bool VOL, bool SDF, bool SPECTRAL, bool COUNT>
 DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  treelet_load(P);
   // (a wavefront module parks pending marches for its march kernel: its SDF
   // paths cannot run here)
   static_assert(!Integrator<Scene, Cfg, RESTIR, VOL, SDF, SPECTRAL, COUNT>::WF &&
@@ -3004,11 +3058,11 @@ DEV void pass_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     if (P.rout_main == nullptr || P.rout_aux == nullptr) return;
     if (it.flag(F_RESTIR_DEF)) {
       const Res &q = it.fin;
-      P.rout_main[pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
-      P.rout_aux[pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+      P.rout_main[RT0_RES_STRIDE * (size_t)pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
+      P.rout_aux[RT0_RES_STRIDE * (size_t)pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
     } else {
-      P.rout_main[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
-      P.rout_aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+      P.rout_main[RT0_RES_STRIDE * (size_t)pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+      P.rout_aux[RT0_RES_STRIDE * (size_t)pix] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   if constexpr (COUNT) {
@@ -3065,6 +3119,7 @@ DEV const float4 *candidate_table(const Scene &sc, const Cfg &cfg) {
 
 template <class Scene, class Cfg, bool VOL, bool SDF, bool SPECTRAL>
 DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  treelet_load(P);
   // one wave per RT0_NEE_REGIONS consecutive regions: their records form one
   // list, so a region's tail chunk does not idle most of a wave (C5 averages
   // ~68 records per region: one region per wave ran a 64-record chunk and a
@@ -3108,8 +3163,8 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   auto store = [&](const NeeRec &r, v3 c, const Res &q) {
     P.nee_out[(size_t)r.k() * plane + r.pix] = make_float4(c.x * r.mr, c.y * r.mg, c.z * r.mb, 0.f);
     if (r.k() == P.nee_n[r.pix] - 1 && P.rout_main != nullptr && P.rout_aux != nullptr) {
-      P.rout_main[r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
-      P.rout_aux[r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+      P.rout_main[RT0_RES_STRIDE * (size_t)r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
+      P.rout_aux[RT0_RES_STRIDE * (size_t)r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
     }
   };
 #if RT0_NEE_WALK
@@ -3151,8 +3206,8 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
             make_float4(sp.f.x * r.mr, sp.f.y * r.mg, sp.f.z * r.mb, __int_as_float(tag));
         if (r.k() == P.nee_n[r.pix] - 1 && P.rout_main != nullptr && P.rout_aux != nullptr) {
           const Res &q = it.fin;
-          P.rout_main[r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, sp.W);
-          P.rout_aux[r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+          P.rout_main[RT0_RES_STRIDE * (size_t)r.pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, sp.W);
+          P.rout_aux[RT0_RES_STRIDE * (size_t)r.pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
         }
         has0 = w0;
         has1 = w1;
@@ -3197,6 +3252,7 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 // property (some triangle in (EPSILON, tmax)): the visiting order does not
 // change it.
 DEV void walk_body_spec(const LaunchParams &P) {
+  treelet_load(P);
   const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
   if (w >= (uint32_t)P.walk_waves) return;
   const uint32_t n = P.walk_count[w];
@@ -3231,8 +3287,9 @@ DEV void walk_body_spec(const LaunchParams &P) {
   while (__ballot(have) != 0ull) {
     // node phase: lanes without pending leaves visit their next node
     if (have && pa < 0 && node >= 0) {
-      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
-      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+      float4 a, b, c;
+      int4 lk;
+      bvh_fetch(P, nodes, node, a, b, c, lk);
       float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmax);
       float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmax);
       const int cl = lk.x, cr = lk.y;
@@ -3285,6 +3342,7 @@ DEV void walk_body(const LaunchParams &P) {
 #if RT0_WALK_SPEC
   walk_body_spec(P);
 #else
+  treelet_load(P);
   const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
   if (w >= (uint32_t)P.walk_waves) return;
   const uint32_t n = P.walk_count[w];
@@ -3311,8 +3369,9 @@ DEV void walk_body(const LaunchParams &P) {
   while (__ballot(have) != 0ull) {
     if (have) {
       bool done = false, occ = false;
-      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
-      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+      float4 a, b, c;
+      int4 lk;
+      bvh_fetch(P, nodes, node, a, b, c, lk);
       float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmax);
       float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmax);
       const int cl = lk.x, cr = lk.y;
@@ -3406,7 +3465,7 @@ DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
       const size_t slot2 = 2u * (size_t)((tag >> 2) - 1u);
       const bool vis = !(tag & 1u) || P.walk_res[slot2] == 0u;
       if (!(vis && (!(tag & 2u) || P.walk_res[slot2 + 1] == 0u))) o = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!vis && k == n - 1 && P.rout_main != nullptr) P.rout_main[pix].w = 0.0f;
+      if (!vis && k == n - 1 && P.rout_main != nullptr) P.rout_main[RT0_RES_STRIDE * (size_t)pix].w = 0.0f;
     }
 #endif
     col = col + mk(o.x, o.y, o.z);
@@ -3642,6 +3701,7 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 // deferred calls so far; 2 (MIS or spectral): previous normal, hero.
 template <class Scene, class Cfg, bool VOL, bool SPECTRAL>
 DEV void wf_restir_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
+  treelet_load(P);
   const SceneTables tabs = scene_tables(sc);  // (one barrier, before any wave leaves)
   if (blockIdx.x == 0 && threadIdx.x < 8) P.wf_ctr[16 * threadIdx.x] = 0u;  // the walk kernel's range counters
   const uint32_t lane = threadIdx.x & 63u;
@@ -3743,11 +3803,11 @@ DEV void wf_restir_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       if (it.nee_k == 0 && P.rout_main != nullptr && P.rout_aux != nullptr) {
         if (it.flag(F_RESTIR_DEF)) {
           const Res q = empty_res();
-          P.rout_main[pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
-          P.rout_aux[pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
+          P.rout_main[RT0_RES_STRIDE * (size_t)pix] = make_float4(q.pos.x, q.pos.y, q.pos.z, q.W);
+          P.rout_aux[RT0_RES_STRIDE * (size_t)pix] = make_float4(q.col.x, q.col.y, q.col.z, pack_alpha(q.age, q.M, q.idx, sc.n_lights()));
         } else {
-          P.rout_main[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
-          P.rout_aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+          P.rout_main[RT0_RES_STRIDE * (size_t)pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+          P.rout_aux[RT0_RES_STRIDE * (size_t)pix] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
     }
@@ -4056,6 +4116,7 @@ DEV void wf_march_body(const LaunchParams &P, Scene sc, Cfg cfg) {
 // whatever the rays' lengths.
 #if RT0_BVH_STACK16 || defined(RT0_BVH_STACK)
 DEV void wf_walk_body(const LaunchParams &P) {
+  treelet_load(P);
   const uint32_t R = (uint32_t)P.wf_R;
   const WfPlan pl = wf_plan_prefix(P);  // (one barrier, before any wave leaves)
   WfQueue Q(P, pl);
@@ -4090,8 +4151,9 @@ DEV void wf_walk_body(const LaunchParams &P) {
     if (__ballot(busy) == 0ull) break;  // the queue is dry and every lane answered
     if (busy) {
       bool done = false;
-      const float4 a = nodes[4 * node], b = nodes[4 * node + 1], c = nodes[4 * node + 2];
-      const int4 lk = reinterpret_cast<const int4 *>(nodes)[4 * node + 3];
+      float4 a, b, c;
+      int4 lk;
+      bvh_fetch(P, nodes, node, a, b, c, lk);
       float tl = box_enter(a.x, a.y, a.z, b.x, b.y, b.z, o, inv, tmin);
       float tr = box_enter(a.w, b.w, c.x, c.y, c.z, c.w, o, inv, tmin);
       const int cl = lk.x, cr = lk.y;

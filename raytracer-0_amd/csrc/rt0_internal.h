@@ -22,9 +22,10 @@ void default_config(rt0_config &c);
 // owner tags with RT0_TRI_CULL_BIT) -> pre-order inner nodes + leaf-order
 // triangles; returns the depth (edges root -> deepest leaf), -1 for n <= 0
 int bvh_build_sah(int n, const float *v, const int32_t *model, std::vector<BvhNode> &nodes, std::vector<TriDev> &tris);
-// the binary tree collapsed to 4-wide nodes (grandchildren become children);
-// returns the traversal stack entries a walk can need (pushes along the
-// deepest chain), nodes4 in pre-order
+// renumber the tree so that every node of its top levels comes first,
+// breadth-first (at most max_nodes of them, whole levels), the rest after in
+// their pre-order; returns how many lead (the LDS treelet, bvh_fetch)
+int bvh_treelet_order(std::vector<BvhNode> &nodes, int max_nodes);
 int parse_config(const char *const *defines, int nd, const char *const *constants, int nc, rt0_config &c,
                  std::string &err);
 }  // namespace rt0h

@@ -72,6 +72,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
   if (k.defer && k.walk) o << "#define RT0_NEE_WALK 1\n";
   if (k.bvh_stack > 0 && k.stack16) o << "#define RT0_BVH_STACK16 1\n";
+  // the tree's top levels in LDS (rt0_integrator.h bvh_fetch; rt0_host.cpp kTreeletNodes)
+  if (k.bvh_stack > 0) o << "#ifndef RT0_TREELET\n#define RT0_TREELET 64\n#endif\n";
   if (k.wf) o << "#define RT0_WAVEFRONT 1\n";
   // ReSTIR scenes without models fetch their reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the

@@ -500,8 +500,11 @@ class Renderer:
         return rows.value
 
     def set_restir_buffers(self, dptrs):
-        """Use 8 caller-owned W*H*4 f32 device planes (e.g. torch tensors) as the
-        ReSTIR reservoir textures; None returns to context-owned planes."""
+        """Use caller-owned device memory (e.g. torch tensors) as the ReSTIR
+        reservoir textures: four interleaved main/aux pair buffers of W*H*8
+        f32, given as 8 plane pointers with dptrs[2k+1] = dptrs[2k] + 16 bytes
+        (a (4, H, W, 2, 4) tensor's [k, :, :, 0] and [k, :, :, 1]); None
+        returns to context-owned planes."""
         if dptrs is None:
             self._chk(lib().rt0_set_restir_buffers(self.h, None))
             return

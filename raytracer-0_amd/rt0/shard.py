@@ -311,16 +311,20 @@ class RestirShard:
         self.rank, self.world, self.halo, self.staged = rank, world, halo, staged
         self.order = order or StreamOrder(renderer, device)
         self.band = band or block_band(height, world)  # default: one contiguous block
-        self.planes = torch.zeros((8, height, width, 4), dtype=torch.float32, device=device)
-        renderer.set_restir_buffers([self.planes[i].data_ptr() for i in range(8)])
-        self.by_ptr = {self.planes[i].data_ptr(): i for i in range(8)}
+        # four interleaved main/aux pairs (rt0_set_restir_buffers): texel (y, x)
+        # of a pair = its main then its aux RGBA32F, so a row range of a pair
+        # tensor is both planes' rows
+        self.pairs = torch.zeros((4, height, width, 2, 4), dtype=torch.float32, device=device)
+        renderer.set_restir_buffers([self.pairs[k, :, :, j].data_ptr() for k in range(4) for j in range(2)])
+        self.by_ptr = {self.pairs[k, :, :, 0].data_ptr(): k for k in range(4)}
         renderer.set_shard(rank, world, self.band)
         renderer.set_halo(halo)
         torch.cuda.synchronize(device)
 
     def newest(self):
-        m, a = self.r.device_restir(0)
-        return [self.planes[self.by_ptr[m]], self.planes[self.by_ptr[a]]]
+        """The pair tensor (H, W, 2, 4) of the newest reservoir planes."""
+        m, _ = self.r.device_restir(0)
+        return [self.pairs[self.by_ptr[m]]]
 
     def render(self, first, n, exchange=None):
         """Passes first..first+n-1, one launch each, halo exchange after each

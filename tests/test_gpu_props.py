@@ -209,11 +209,11 @@ def _restir_shards(cfgs, cfg, W, H, world, halo, band=None):
     for rank in range(world):
         r = rt0.Renderer(W, H)
         rt0.configure(r, cfg, cfgs)
-        planes = torch.zeros((8, H, W, 4), dtype=torch.float32, device="cuda:0")
-        r.set_restir_buffers([planes[i].data_ptr() for i in range(8)])
+        pairs = torch.zeros((4, H, W, 2, 4), dtype=torch.float32, device="cuda:0")  # interleaved main/aux
+        r.set_restir_buffers([pairs[k, :, :, j].data_ptr() for k in range(4) for j in range(2)])
         r.set_shard(rank, world, band)
         r.set_halo(halo)
-        out.append((r, planes, {planes[i].data_ptr(): i for i in range(8)}))
+        out.append((r, pairs, {pairs[k, :, :, 0].data_ptr(): k for k in range(4)}))
     torch.cuda.synchronize()
     return out, band
 
@@ -236,9 +236,9 @@ def test_sharded_restir_matches_whole_image(cfgs, gpu_required, world, halo):
     shards, band = _restir_shards(cfgs, cfg, W, H, world, halo)
 
     def newest(s):
-        r, planes, by_ptr = s
-        m, a = r.device_restir(0)
-        return [planes[by_ptr[m]], planes[by_ptr[a]]]
+        r, pairs, by_ptr = s
+        m, _ = r.device_restir(0)
+        return [pairs[by_ptr[m]]]
 
     for k in range(1, F + 1):
         for r, _, _ in shards:
@@ -274,9 +274,9 @@ def test_sharded_restir_round_robin_bands_match_whole_image(cfgs, gpu_required, 
     shards, band = _restir_shards(cfgs, cfg, W, H, world, halo, band)
 
     def newest(s):
-        r, planes, by_ptr = s
-        m, a = r.device_restir(0)
-        return [planes[by_ptr[m]], planes[by_ptr[a]]]
+        r, pairs, by_ptr = s
+        m, _ = r.device_restir(0)
+        return [pairs[by_ptr[m]]]
 
     for k in range(1, F + 1):
         for r, _, _ in shards:

@@ -208,12 +208,14 @@ def test_jit_walk_module_for_model_scenes(cfgs, tmp_path, monkeypatch):
     monkeypatch.delenv("RT0_JIT_EXTRA")
     assert {"rt0_jit_wf_shade", "rt0_jit_wf_plan", "rt0_jit_wf_walk", "rt0_jit_nee", "rt0_jit_walk",
             "rt0_jit_resolve"} <= set(lds) and "rt0_jit_pass" not in lds, lds
-    assert 256 * 24 * 2 <= lds["rt0_jit_wf_walk"] <= 256 * 24 * 2 + 2048  # the stack + the plan prefix
+    # the stack + the LDS treelet (64 BVH nodes of 64 B, rt0_integrator.h bvh_fetch) + the plan prefix
+    tl = 64 * 64
+    assert 256 * 24 * 2 + tl <= lds["rt0_jit_wf_walk"] <= 256 * 24 * 2 + tl + 2048
     # the default (mode 1: SDF scenes only): the pass kernel
     monkeypatch.setenv("RT0_WAVEFRONT", "1")
     co, lds = compile_lds()
     assert {"rt0_jit_pass", "rt0_jit_nee", "rt0_jit_walk", "rt0_jit_resolve"} <= set(lds), lds
-    assert lds["rt0_jit_walk"] == 256 * 24 * 2 + 16  # the stack + the wave counters
+    assert lds["rt0_jit_walk"] == 256 * 24 * 2 + 16 + tl  # the stack + the wave counters + the treelet
     # the pass and light-sampling kernels also hold LDS copies of the scene
     # tables (rt0_integrator.h scene_tables: geometry, material and clamped
     # material, 32 B each per mesh) and the latter the ReSTIR candidates'
@@ -221,5 +223,5 @@ def test_jit_walk_module_for_model_scenes(cfgs, tmp_path, monkeypatch):
     src = open(co[:-3] + ".hip").read()
     k = {n: int(v) for n, v in re.findall(r"\b(kMeshes|kSdfs|kLights|kModels) = (\d+)", src)}
     tables = 96 * (k["kMeshes"] + k["kSdfs"] + k["kModels"])
-    assert lds["rt0_jit_pass"] <= 256 * 24 * 2 + 16 + tables
-    assert lds["rt0_jit_nee"] == tables + 32 * k["kLights"]  # no BVH walk left in the light-sampling kernel
+    assert lds["rt0_jit_pass"] <= 256 * 24 * 2 + 16 + tables + tl
+    assert lds["rt0_jit_nee"] == tables + 32 * k["kLights"] + tl  # (+ the treelet its walk code could read)
