@@ -124,6 +124,22 @@ def run_config(glrun, cfgs, cfg):
                          for k in ids])
 
     out = {"samples": load("c")}
+    if cfg.get("events") and not restir:
+        # the first-event records: the instrumented shader's run, kept where its
+        # image equals the plain run's bit for bit
+        ifrag = frag[:-len(".frag")] + "_events.frag"
+        with open(ifrag, "w") as f:
+            f.write(instrument_events(open(frag).read()))
+        eprefix = prefix + "_ev"
+        ecmd = list(cmd)
+        ecmd[ecmd.index("--frag") + 1] = ifrag
+        ecmd[ecmd.index("--out") + 1] = eprefix
+        sh(ecmd + ["--restir-out", "--frames", str(frames)], timeout=int(os.environ.get("RT0_GOLDEN_TIMEOUT", "1800")))
+        ev = {tag: np.stack([np.fromfile("%s_f%d_%s.bin" % (eprefix, k, tag), dtype=np.float32).reshape(H, W, 4)
+                             for k in ids]) for tag in "cra"}
+        same = (ev["c"] == out["samples"]).all(-1) | (np.isnan(ev["c"]).all(-1) & np.isnan(out["samples"]).all(-1))
+        out["exec_events"] = np.concatenate([ev["r"], ev["a"]], axis=-1)  # (F, H, W, 8)
+        out["events_valid"] = same
     if cfg.get("frame_timeout"):
         out["frames"] = np.asarray(ids, np.int32)  # u_frame of each samples[i]
     if restir:
@@ -197,6 +213,56 @@ def instrument_paths(src):
         "    ReSTIRData = vec4(g_pit, g_h0, g_h1, g_h2);\n"
         "    ReSTIRAux = vec4(g_e0, g_e1, float(SCATTERING_EVENTS) + 256.0 * float(DIFF_BOUNCES), "
         "float(TRANS_BOUNCES) + 256.0 * float(SPEC_BOUNCES));")
+    return src
+
+
+# ---- first-event records (configs with "events": true) ----
+# For the glossy METAL scenes: what the executor computed along each lane's
+# path, written to the reservoir MRTs (a non-ReSTIR shader leaves them at
+# zero): [0] the first intersection's t, [1] its texel (the METAL value-noise
+# f that sets the glossiness, getTexel 762-768), [2..4] the ray direction
+# brdf() leaves after the first bounce (the SDF normal of calcNormal and the
+# glossy reflection), [5] the second intersection's t, [6] the path's
+# decisions as an integer < 2^24 -- per bounce d < 6 two bits (1 SDF 0 hit,
+# 2 another hit, 3 miss) at 2d, and one bit at 12 + d when brdf() added to
+# the radiance (its environment NEE ray escaped, 1887-1897; the scenes have no
+# lights) -- and [7] the red channel of the first miss's environment sample.
+# Plain statements in radiance() (masked like the code around them,
+# mask_kat.py rule 1; not inside brdf(), whose ghost calls write globals);
+# run_config keeps a pixel-sample only where this image equals the plain one
+# bit for bit.  The restatement writes the same record (RT0_DEBUG_EVENTS), so
+# each departing pixel's first divergent event is named
+# (tests/test_oracle_golden.py test_metal_departures_attributed).
+def instrument_events(src):
+    def sub(old, new):
+        nonlocal src
+        assert src.count(old) == 1, old
+        src = src.replace(old, new)
+    sub("vec3 radiance(Ray r, float seed){",
+        "float g_t0 = -1.0; float g_f0 = -1.0; vec3 g_rd1 = vec3(0.0); float g_t1 = -1.0; float g_dec = 0.0; "
+        "float g_env = -1.0; float g_pw = 1.0; float g_pb = 4096.0;\n"
+        "vec3 radiance(Ray r, float seed){")
+    sub("    Hit hit;\n    float t = intersection(r, hit);\n",
+        "    Hit hit;\n    float t = intersection(r, hit);\n"
+        "    if (depth == 0) { g_t0 = t; g_f0 = hit.texel.r; } else if (depth == 1) { g_t1 = t; }\n"
+        "    if (depth > 0) { g_pw *= 4.0; g_pb *= 2.0; }\n"
+        "    if (depth < 6) g_dec += (t == INFINITY ? 3.0 : (hit.index == NUM_MESHES ? 1.0 : 2.0)) * g_pw;\n")
+    sub("#ifdef USE_CUBEMAP\n        acc += mask * texture(u_cubemap, r.d).rgb;",
+        "#ifdef USE_CUBEMAP\n        acc += mask * texture(u_cubemap, r.d).rgb;\n"
+        "        if (g_env < 0.0) g_env = texture(u_cubemap, r.d).r;")
+    sub("        acc += mask * (vec3(0.5) + vec3(0.5) * cos(TWO_PI * (vec3(0.525, 0.408, 0.409) + vec3(0.9, 0.97, 0.8) * "
+        "clamp(r.d.y * 0.6 + 0.5, 0.3, 1.0))));",
+        "        acc += mask * (vec3(0.5) + vec3(0.5) * cos(TWO_PI * (vec3(0.525, 0.408, 0.409) + vec3(0.9, 0.97, 0.8) * "
+        "clamp(r.d.y * 0.6 + 0.5, 0.3, 1.0))));\n"
+        "        if (g_env < 0.0) g_env = 0.5 + 0.5 * cos(TWO_PI * (0.525 + 0.9 * clamp(r.d.y * 0.6 + 0.5, 0.3, 1.0)));")
+    sub("    brdf(hit, c, e, t, inside, r, mask, acc, bounceIsSpecular, seed, float(depth));\n",
+        "    vec3 g_acc0 = acc;\n"
+        "    brdf(hit, c, e, t, inside, r, mask, acc, bounceIsSpecular, seed, float(depth));\n"
+        "    if (depth == 0) g_rd1 = r.d;\n"
+        "    if (depth < 6 && any(notEqual(acc, g_acc0))) g_dec += g_pb;\n")
+    sub("    ReSTIRData = vec4(0.0);\n    ReSTIRAux = vec4(0.0);",
+        "    ReSTIRData = vec4(g_t0, g_f0, g_rd1.x, g_rd1.y);\n"
+        "    ReSTIRAux = vec4(g_rd1.z, g_t1, g_dec, g_env);")
     return src
 
 

@@ -189,6 +189,7 @@ typedef struct {
   int ss_tex;        /* SWIFTSHADER_TEX_FILTER: the executor's fixed-point RGBA8 bilinear filter (tex_fetch_ss) */
   int ss_quad_lights; /* SWIFTSHADER_QUAD_LIGHTS: light_index[i] in brdf's light loops read at the quad's first lane's index (rule 7) */
   int dbg_paths;     /* RT0_DEBUG_PATHS: non-ReSTIR reservoir outputs carry per-sample path statistics */
+  int dbg_events;    /* RT0_DEBUG_EVENTS: ... carry the first-event record (instrument_events) */
   /* camera uniforms (index.js:421-423) */
   v3 cam_pos, cam_look, cam_params;
   /* asset textures (index.js:256-296): 0..3 u_tex0..3, 4 u_rnd_tex; RGBA8 */
@@ -218,6 +219,11 @@ typedef struct {
    * eight per float: dbg_ev[(i-1)/8]) -- every field an integer < 2^24, exact
    * in fp32 (make_golden.py instrument_paths writes the same) */
   float dbg_pit, dbg_hist[3], dbg_ev[2];
+  /* RT0_DEBUG_EVENTS (make_golden.py instrument_events): the first
+   * intersection's t and texel, the ray direction after the first bounce,
+   * the second intersection's t, the first miss's environment sample */
+  float ev_t0, ev_f0, ev_t1, ev_dec, ev_env;
+  v3 ev_rd1;
   int q0_iters;                /* SWIFTSHADER_QUAD_LIGHTS: bounce-loop iterations of the quad's first lane (-1: this is it) */
   unsigned nee_mask;           /* bounces at which this lane ran brdf's light loop (bit d) */
   unsigned q0_nee_mask;        /* the quad's first lane's nee_mask */
@@ -1406,6 +1412,14 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
     }
     Hit hit;
     float t = intersection(F, ro, rd, &hit);
+    if (depth == 0) {
+      F->ev_t0 = t;
+      F->ev_f0 = hit.texel[0];
+    } else if (depth == 1) {
+      F->ev_t1 = t;
+    }
+    if (depth < 6) /* 1 the first SDF, 2 another hit, 3 a miss; two bits per bounce */
+      F->ev_dec += (t == INF_T ? 3.0f : hit.index == o->n_meshes ? 1.0f : 2.0f) * (float)(1 << (2 * depth));
     if (trace_pixel(F))
       fprintf(stderr, "frame %d depth %d ro (%.9g %.9g %.9g) rd (%.9g %.9g %.9g) t %.9g index %d spec %d\n", F->frame,
               depth, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, t, t == INF_T ? -1 : hit.index, spec);
@@ -1468,12 +1482,15 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
         break;
       }
       if (o->use_cubemap) {
-        acc = add(acc, mul(mask, cube_sample(o, rd)));
+        const v3 env = cube_sample(o, rd);
+        acc = add(acc, mul(mask, env));
+        if (F->ev_env < 0.0f) F->ev_env = env.x;
       } else if (o->use_sky) {
         float k = gclamp(rd.y * 0.6f + 0.5f, 0.3f, 1.0f);
         v3 sky = V(0.5f + 0.5f * cosf(TWO_PI * (0.525f + 0.9f * k)), 0.5f + 0.5f * cosf(TWO_PI * (0.408f + 0.97f * k)),
                    0.5f + 0.5f * cosf(TWO_PI * (0.409f + 0.8f * k)));
         acc = add(acc, mul(mask, sky));
+        if (F->ev_env < 0.0f) F->ev_env = sky.x;
       }
       if (o->ghost) ghost_brdf(F, &regs, seed);
       dbg_event(F, 2.0f);
@@ -1499,7 +1516,11 @@ static v3 radiance(Frag *F, v3 ro, v3 rd, float seed) {
       break;
     }
     prev_nl = muls(hit.n, inside);
+    const v3 acc0 = acc;
     brdf(F, &hit, c, e, inside, &ro, &rd, &mask, &acc, &spec, seed, (float)depth);
+    if (depth == 0) F->ev_rd1 = rd;
+    if (depth < 6 && (acc.x != acc0.x || acc.y != acc0.y || acc.z != acc0.z))  /* brdf() added radiance */
+      F->ev_dec += (float)(4096 << depth);
     if (o->ghost) {
       regs.have = 1; regs.hit = hit; regs.e = e; regs.inside = inside; regs.bounce = (float)depth;
       regs.rd = rd; regs.spec = spec;
@@ -1553,6 +1574,9 @@ static v3 shade_pixel(Frag *F, int px, int py) {
   F->last_depth = -1;
   F->first_scat = -1;
   F->dbg_pit = 0.0f;
+  F->ev_t0 = F->ev_f0 = F->ev_t1 = F->ev_env = -1.0f;
+  F->ev_dec = 0.0f;
+  F->ev_rd1 = V(0, 0, 0);
   F->dbg_hist[0] = F->dbg_hist[1] = F->dbg_hist[2] = 0.0f;
   F->dbg_ev[0] = F->dbg_ev[1] = 0.0f;
   F->hero = 550.0f;
@@ -1763,6 +1787,7 @@ int or_set_constant(void *h, const char *name, double v) {
   else if (!strcmp(name, "SWIFTSHADER_TEX_FILTER")) o->ss_tex = iv;
   else if (!strcmp(name, "SWIFTSHADER_QUAD_LIGHTS")) o->ss_quad_lights = iv;
   else if (!strcmp(name, "RT0_DEBUG_PATHS")) o->dbg_paths = iv;
+  else if (!strcmp(name, "RT0_DEBUG_EVENTS")) o->dbg_events = iv;
   else if (!strcmp(name, "RENDER_MODE")) {
     o->render_mode = iv;
     if (iv != 0 && iv != 1) { snprintf(o->err, sizeof o->err, "RENDER_MODE must be 0 or 1"); return -1; }
@@ -1849,6 +1874,13 @@ int or_render_frame(void *h, unsigned frame, float *out, const float *const *res
       v3 col = shade_pixel(&F, x, y);
       size_t p = ((size_t)y * o->w + x) * 4;
       out[p] = col.x; out[p + 1] = col.y; out[p + 2] = col.z; out[p + 3] = 0.0f;
+      if (o->dbg_events && !o->use_restir_def && restir_main && restir_aux) {
+        restir_main[p] = F.ev_t0; restir_main[p + 1] = F.ev_f0;
+        restir_main[p + 2] = F.ev_rd1.x; restir_main[p + 3] = F.ev_rd1.y;
+        restir_aux[p] = F.ev_rd1.z; restir_aux[p + 1] = F.ev_t1;
+        restir_aux[p + 2] = F.ev_dec; restir_aux[p + 3] = F.ev_env;
+        continue;
+      }
       if (o->dbg_paths && !o->use_restir_def && restir_main && restir_aux) {
         (void)it0;
         restir_main[p] = F.dbg_pit; restir_main[p + 1] = F.dbg_hist[0];

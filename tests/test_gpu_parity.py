@@ -31,9 +31,10 @@ BAD_FRAC = {"default": 0.01, "c4_mandelbulb_vol": 0.03, "spectral_vol_1l": 0.03,
             # oracle/gen/make_golden.py instrument_paths)
             "c4_mandelbulb_deep": 0.03, "c4_mandelbulb_deep_novol": 0.03,
             "mis_demo_sdfbox": 0.02, "restir_mis_demo": 0.02, "c3_outdoor_restir": 0.01,
-            # glossy METAL reflections grazing the slab's front edge: chaotic
-            # under ulp-level changes (attributed per pixel in
-            # test_gpu_metal_departures_attributed)
+            # glossy METAL reflections grazing the slab's front edge: the SDF
+            # marches' decisions and calcNormal's normal, chaotic under
+            # ulp-level changes (each departing pixel's first divergent event:
+            # test_oracle_golden.test_metal_departures_attributed)
             "tex_sdf_metal": 0.05, "cube_sdf_metal": 0.08,
             # the reference's own assets (real rgba_noise256.png, tex0-3.png,
             # Tropical Beach cubemap) with the executor's texture filter (the

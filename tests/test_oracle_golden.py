@@ -652,3 +652,73 @@ def test_two_light_executor_quad_lights(name, cfgs):
     bad = 1.0 - ok[valid].mean()
     assert bad <= bound, (name, bad)
     assert abs(got[valid].mean() - gold[valid].mean()) <= mean_tol * max(1.0, abs(gold[valid].mean()))
+
+
+# First divergent event of every departing pixel of the glossy METAL scenes
+# (make_golden.py instrument_events, the restatement's RT0_DEBUG_EVENTS),
+# measured (bad pixel-samples of 16 384; round 6):
+#   tex_sdf_metal           573: march decisions 401, first-hit normal 171, noise 1
+#   cube_sdf_metal         1007: march 751 (with the environment-NEE shadow
+#                          rays), normal 250, noise 1, no recorded event 5
+#   page_scene0_slabfirst  1035: march 822, normal 195, noise 5, the first
+#                          miss's cube sample 4, no recorded event 9
+# So the departures are the SDF marches' decisions (hit or miss, which box)
+# and calcNormal's four-probe normal, both chaotic under ulp-level map()
+# differences -- not the textures' filters: the noise fetch, the cube fetch
+# and everything no event records explain at most 0.15% of the pixels.
+METAL_EVENTS = ["tex_sdf_metal", "cube_sdf_metal", "page_scene0_slabfirst"]
+
+
+def _first_divergence(e, r):
+    """The first event at which the executor's record e departs from the
+    restatement's r (instrument_events' layout)."""
+    de, dr = int(e[6]), int(r[6])
+    if (de & 3) != (dr & 3):
+        return "march"  # the camera ray: hit or miss, which SDF
+    if abs(e[1] - r[1]) > 1e-5:
+        return "noise"  # the first hit's METAL value noise
+    if (np.abs(e[2:5] - r[2:5]) > 1e-4).any():
+        return "normal"  # the first bounce's direction: calcNormal + the glossy reflection
+    for d in range(6):
+        if ((de >> (2 * d)) & 3) != ((dr >> (2 * d)) & 3):
+            return "march"  # bounce d's ray
+        if ((de >> (12 + d)) & 1) != ((dr >> (12 + d)) & 1):
+            return "march"  # bounce d's environment-NEE shadow ray (escaped or not)
+    if abs(e[7] - r[7]) > 1e-3:
+        return "env"  # the first miss's environment sample
+    return "same"  # every recorded event equal
+
+
+@pytest.mark.parametrize("name", METAL_EVENTS)
+def test_metal_departures_attributed(name, cfgs):
+    if not have(name):
+        pytest.skip("fixture %s not generated" % name)
+    cfg = [c for c in cfgs["configs"] if c["name"] == name][0]
+    G = np.load(os.path.join(GOLD, name + ".npz"))
+    gold, E, ev_ok = G["samples"][..., :3], G["exec_events"], G["events_valid"]
+    assert ev_ok.all()  # the instrumented image equals the plain one everywhere
+    o = O.Oracle(cfg, cfgs, width=gold.shape[2], height=gold.shape[1],
+                 overrides={"SWIFTSHADER_GHOST": 1, "RT0_DEBUG_EVENTS": 1})
+    S, R = [], []
+    for k in range(1, gold.shape[0] + 1):
+        s, m, a = o.frame(k)
+        S.append(s[..., :3])
+        R.append(np.concatenate([m, a], -1))
+    S, R = np.stack(S), np.stack(R)
+    ok, _ = pixel_match(S, gold)
+    bad = ~ok
+    kinds = {}
+    for f, y, x in zip(*np.nonzero(bad)):
+        k = _first_divergence(E[f, y, x], R[f, y, x])
+        kinds[k] = kinds.get(k, 0) + 1
+    n = bad.size
+    print(name, "bad %.4f" % bad.mean(), kinds)
+    assert sum(kinds.values()) == int(bad.sum())
+    # the filters (noise texture, cubemap) and anything no event explains
+    assert kinds.get("noise", 0) + kinds.get("env", 0) + kinds.get("same", 0) <= 0.0015 * n, kinds
+    # the march decisions and the first-hit normal are the departures
+    assert kinds.get("march", 0) + kinds.get("normal", 0) >= bad.sum() - 0.0015 * n
+    # and they are rare where the image agrees: the executor's decisions equal
+    # the restatement's on >= 98% of the matching pixel-samples
+    same_dec = E[..., 6] == R[..., 6]
+    assert same_dec[ok].mean() >= 0.98
