@@ -257,7 +257,11 @@ struct LaunchParams {
   // wf_L per region, wf_sh_cnt); the march kernel takes regions off
   // wf_ctr[16 * k] (one counter per eighth of the regions) and answers them
   // (wf_res; wf_shres[light * wf_slots + slot]).
-  // Path state between rounds: wf_state[k * wf_slots + slot].
+  // Path state between rounds: SDF rounds keep it in list order, beside the
+  // march list: wf_sin[k * wf_cap + entry] is the state of region entry
+  // `entry` of wf_in, and the shade kernel writes wf_sout[k * wf_cap + o] for
+  // the entry o it appends to wf_out (coalesced, like the lists; the two
+  // swap every round); ReSTIR rounds keep wf_state[k * wf_slots + slot].
   int32_t wf_round, wf_R, wf_L, wf_nregions, wf_f0;
   uint32_t wf_apad, wf_slots, wf_gx;
   uint32_t wf_slot0;  // the launch's first slot of this part (a wavefront half on its own stream)
@@ -267,6 +271,8 @@ struct LaunchParams {
   uint32_t *wf_plan, *wf_plan_bn, *wf_plan_bj;
   int32_t wf_plan_blocks, wf_plan_span;
   float4 *wf_state;
+  float4 *wf_sin, *wf_sout;
+  uint32_t wf_cap;  // entries per state component (the half's regions x wf_R)
   float4 *wf_in, *wf_out;
   uint32_t *wf_in_cnt, *wf_out_cnt, *wf_sh_cnt;
   float4 *wf_res;

@@ -771,8 +771,9 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   const bool restir = (c->cfg.defines & RT0_USE_RESTIR) != 0;
   const uint32_t L = restir ? 0u : (uint32_t)std::max(1, c->host_scene.n_lights);
   const bool extra = (p.flags & F_MIS) || ((p.flags & F_SPECTRAL) && (c->cfg.defines & RT0_USE_SPECTRAL));
-  // bytes per slot: state, two march-list entries, the answer + id, L shadow entries + answers
-  const size_t per_slot = (extra ? 48 : 32) + 2 * 32 + 16 + 4 + (size_t)L * (48 + 16);
+  // bytes per slot: state (per slot for ReSTIR; two list-ordered copies for
+  // SDF rounds), two march-list entries, the answer + id, L shadow entries + answers
+  const size_t per_slot = (extra ? 48 : 32) * (restir ? 1 : 2) + 2 * 32 + 16 + 4 + (size_t)L * (48 + 16);
   const size_t budget = getenv("RT0_WF_BYTES") ? (size_t)atoll(getenv("RT0_WF_BYTES")) : (size_t)8 << 30;
   const size_t apad = (size_t)grid.x * grid.y * 256;
   // The slots of a frame chunk run as K independent halves on K HIP streams
@@ -804,7 +805,8 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_state = al(cap * (extra ? 3 : 2) * 16), b_list = al(cap * 32), b_res = al(cap * 16),
                b_id = al(cap * 4), b_sh = al(cap * L * 48), b_shres = al(cap * L * 16), b_cnt = al((NR + 4) * 4);
-  const size_t one = b_state + 2 * b_list + b_res + b_id + b_sh + b_shres + 7 * b_cnt + 512 + 2048;
+  const size_t b_ws = restir ? b_state : 0, b_sl = restir ? 0 : b_state;  // per slot (ReSTIR) / list order (SDF)
+  const size_t one = b_ws + 2 * b_sl + 2 * b_list + b_res + b_id + b_sh + b_shres + 7 * b_cnt + 512 + 2048;
   if ((size_t)K * one > c->wf_bytes) {
     if (c->d_wf) HIPCHK(c, hipFree(c->d_wf));
     c->d_wf = nullptr;
@@ -819,7 +821,7 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
     if (!c->wf_join[k]) HIPCHK(c, hipEventCreateWithFlags(&c->wf_join[k], hipEventDisableTiming));
   hipStream_t st[4] = {c->stream, c->wf_streams[0], c->wf_streams[1], c->wf_streams[2]};
   LaunchParams q[4];
-  float4 *lists[4][2];
+  float4 *lists[4][2], *sts[4][2];
   uint32_t *cnts[4][2];
   for (int k = 0; k < K; k++) {
     LaunchParams &u = q[k];
@@ -830,7 +832,10 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
       m += b;
       return r;
     };
-    u.wf_state = (float4 *)take(b_state);
+    u.wf_state = (float4 *)take(b_ws);
+    sts[k][0] = (float4 *)take(b_sl);
+    sts[k][1] = (float4 *)take(b_sl);
+    u.wf_cap = (uint32_t)cap;
     lists[k][0] = (float4 *)take(b_list);
     lists[k][1] = (float4 *)take(b_list);
     u.wf_res = (float4 *)take(b_res);
@@ -882,6 +887,8 @@ static int wf_render(rt0_ctx *c, LaunchParams &p, dim3 grid) {
         u.wf_in_cnt = cnts[k][r & 1];
         u.wf_out = lists[k][(r + 1) & 1];
         u.wf_out_cnt = cnts[k][(r + 1) & 1];
+        u.wf_sin = sts[k][r & 1];
+        u.wf_sout = sts[k][(r + 1) & 1];
         HIPCHK(c, launch(c->jit.wf_shade, u, (unsigned)((u.wf_nregions + 3) / 4), st[k]));
       }
       if (r + 1 == rounds) break;  // (the last round only finishes samples: nothing to march)

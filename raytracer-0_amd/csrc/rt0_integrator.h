@@ -3605,7 +3605,9 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       ps.phase = 0;
       ps.ms.active = ps.ms.done = false;
     } else {
-      const float4 s0 = P.wf_state[slot], s1 = P.wf_state[(size_t)S + slot];
+      // (the state in list order: the same index as the entry)
+      const size_t cap = P.wf_cap, ei = rbase + e;
+      const float4 s0 = P.wf_sin[ei], s1 = P.wf_sin[cap + ei];
       const uint32_t pk = __float_as_uint(s1.z), bits = __float_as_uint(s1.w);
       ps.ro = ro;
       ps.rd = rd;
@@ -3613,7 +3615,7 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
       ps.mask = mk(s0.w, s1.x, s1.y);
       ps.prev_nl = mk(0.f, 1.f, 0.f);
       if constexpr (kExtra) {
-        const float4 s2 = P.wf_state[2 * (size_t)S + slot];
+        const float4 s2 = P.wf_sin[2 * cap + ei];
         ps.prev_nl = mk(s2.x, s2.y, s2.z);
         it.hero = s2.w;
       } else {
@@ -3658,11 +3660,13 @@ DEV void wf_shade_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     if (pending || it.wf_bits) {
       const uint32_t pk = (uint32_t)ps.depth | (ps.spec ? 1u << 7 : 0u) | ((uint32_t)it.diff_b << 8) |
                           ((uint32_t)it.spec_b << 15) | ((uint32_t)it.scat_ev << 22) | ((uint32_t)it.wf_kind << 29);
-      P.wf_state[slot] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, ps.mask.x);
-      P.wf_state[(size_t)S + slot] = make_float4(ps.mask.y, ps.mask.z, __uint_as_float(pk), __uint_as_float(it.wf_bits));
-      if constexpr (kExtra) P.wf_state[2 * (size_t)S + slot] = make_float4(ps.prev_nl.x, ps.prev_nl.y, ps.prev_nl.z, it.hero);
-      // the next round's entry: the march (bound < 0: none, only light sampling to add)
+      // the next round's entry: the march (bound < 0: none, only light sampling
+      // to add), and beside it in list order the path's state
       const uint32_t o = wave_append(wf_wave_counter(0));
+      const size_t cap = P.wf_cap, oi = rbase + o;
+      P.wf_sout[oi] = make_float4(ps.acc.x, ps.acc.y, ps.acc.z, ps.mask.x);
+      P.wf_sout[cap + oi] = make_float4(ps.mask.y, ps.mask.z, __uint_as_float(pk), __uint_as_float(it.wf_bits));
+      if constexpr (kExtra) P.wf_sout[2 * cap + oi] = make_float4(ps.prev_nl.x, ps.prev_nl.y, ps.prev_nl.z, it.hero);
       const March &m = ps.ms;
       P.wf_out[2 * (rbase + o)] = pending ? make_float4(m.o.x, m.o.y, m.o.z, m.tmin) : make_float4(0.f, 0.f, 0.f, -1.0f);
       P.wf_out[2 * (rbase + o) + 1] = make_float4(m.d.x, m.d.y, m.d.z, __uint_as_float(slot));
