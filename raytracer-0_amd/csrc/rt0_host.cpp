@@ -38,11 +38,13 @@ extern "C" hipError_t rt0_bvh_build(int n, const float *d_v, const int32_t *d_mo
 // shards, against 0.89 / 0.78 / 0.61 unchunked).
 static const long kTargetWaves = 16384;
 static const long kChunkWaves = 65536;
-// BVH nodes staged in LDS by the scene-specialised kernels (rt0_jit.cpp
-// RT0_TREELET): 64 x 64 B = 4 KiB per workgroup, whole top levels (63 nodes:
-// six levels of a full tree) -- with the 12 KiB traversal stack the pass
-// kernel still holds 8 workgroups per CU in 160 KiB
-static const int kTreeletNodes = 64;
+// BVH nodes ordered breadth-first at the top of the tree (whole levels, at
+// most this many): the scene-specialised kernels stage the first RT0_TREELET
+// of them in LDS (rt0_jit.cpp: 64 x 64 B = 4 KiB per workgroup, six levels of
+// a full tree -- with the 12 KiB traversal stack the pass kernel still holds
+// 8 workgroups per CU in 160 KiB); the order itself serves any capacity up to
+// seven levels
+static const int kTreeletNodes = 128;
 // pass-wave record regions per light-sampling wave (JitKey::nee_regions)
 static long nee_regions_per_wave() { return 2L; }
 

@@ -427,7 +427,7 @@ DEV void treelet_load(const LaunchParams &P) {
 DEV void bvh_fetch(const LaunchParams &P, const float4 *__restrict__ nodes, int node, float4 &a, float4 &b,
                    float4 &c, int4 &lk) {
 #if RT0_TREELET > 0
-  if (node < P.treelet) {
+  if (node < min(P.treelet, RT0_TREELET)) {  // (the host may order more levels than this module holds)
     const float4 *t = treelet_lds() + 4 * node;
     a = t[0];
     b = t[1];
