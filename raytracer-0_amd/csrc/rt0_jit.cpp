@@ -176,6 +176,9 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     // wavefront rounds, no pass kernel: SDF scenes (rt0_integrator.h
     // wf_shade_body + wf_march_body) or ReSTIR scenes with triangle models
     // (wf_restir_shade_body + wf_walk_body, then the deferred-pass kernels below)
+    // (the SDF shade kernel's occupancy: RT0_WF_SHADE_WAVES through RT0_JIT_EXTRA, an A/B handle)
+    if (!k.restir)
+      o << "\n#ifdef RT0_WF_SHADE_WAVES\n__attribute__((amdgpu_waves_per_eu(RT0_WF_SHADE_WAVES)))\n#endif\n";
     o << "void rt0_jit_wf_shade(const LaunchParams P) {\n"
       << (k.restir ? "  rt0::wf_restir_shade_body<rt0::JitScene, rt0::JitCfg, " : "  rt0::wf_shade_body<rt0::JitScene, rt0::JitCfg, ")
       << vol << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
