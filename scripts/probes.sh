@@ -15,7 +15,9 @@ cd "$ROOT"
 T=$(mktemp -d)
 tar -C "$ROOT" --exclude=./gpurun_out --exclude=./.git --exclude=./profiles --exclude='*.o' -cf - . | tar -C "$T" -xf -
 patch -s -d "$T" -p1 < "${PROBES_PATCH:-scripts/probes.patch}"
-make -s -j16 -C "$T/raytracer-0_amd" rt0/librt0.so
+( while sleep 30; do echo "probes.sh: building the probe library"; done ) & HB=$!
+make -s -j16 -C "$T/raytracer-0_amd" rt0/librt0.so || { kill $HB; exit 1; }
+kill $HB
 mkdir -p "$T/gpurun_out"
 rc=0
 (cd "$T" && "$@") || rc=$?
