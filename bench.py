@@ -63,7 +63,7 @@ PEAK_FP32_TFLOPS = 157.3  # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
 # profiles/<dir>/ holding the PMC summaries (pmc_<config>.json) of each
 # workload, newest first (scripts/gpu_measure.sh writes them)
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02/final")
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02/final")
 BAND = 16
 
 

@@ -48,7 +48,7 @@ def test_committed_profiles_feed_the_bench_line():
         assert pmc["valu"]["SQ_INSTS_VALU"] > pmc["valu"]["SQ_INSTS_VALU_TRANS_F32"] > 0, c
 
 
-@pytest.mark.parametrize("rd", ["r03", "r04", "r05"])
+@pytest.mark.parametrize("rd", ["r03", "r04", "r05", "r06"])
 def test_roofline_summary_reproduces_committed_table(rd):
     """profiles/<round>/roofline.md is what scripts/roofline_summary.py computes
     from the committed per-workload files (no hand edits)."""
