@@ -264,3 +264,26 @@ def test_lbvh_matches_sah_tree(cfgs, gpu_required, tmp_path):
         got = r.read_accum()
         same = (got == other["arr_%d" % i]).all(-1)
         assert same.mean() >= 0.999, (name, same.mean())
+
+
+@pytest.mark.gpu
+def test_lds_treelet_is_bit_identical(cfgs, gpu_required, monkeypatch):
+    """The BVH's top levels staged in LDS (rt0_integrator.h bvh_fetch; the
+    host's breadth-first numbering, bvh_treelet_order) change where the first
+    node loads come from, not which nodes a walk visits or in what order: a
+    3-pass ReSTIR chain of BASELINE config 5's scene renders the same bits
+    with the module's treelet compiled out (RT0_TREELET=0), and with the
+    seven-level capacity."""
+    cfg = cfg_by_name(cfgs, "c5_spectral_models")
+
+    def chain():
+        r = make(cfg, cfgs, 64, 64)
+        for k in (1, 2, 3):
+            r.render(k, 1)
+        return r.read_accum(), r.read_restir(0)[0]
+    base = chain()
+    for extra in ("-DRT0_TREELET=0", "-DRT0_TREELET=128"):
+        monkeypatch.setenv("RT0_JIT_EXTRA", extra)
+        got = chain()
+        assert np.array_equal(got[0], base[0]) and np.array_equal(got[1], base[1]), extra
+    assert base[0][..., :3].mean() > 0.0
