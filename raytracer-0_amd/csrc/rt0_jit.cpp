@@ -169,7 +169,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   if (k.wf && k.restir)  // (the wavefront ReSTIR shade kernel walks no BVH: left to the compiler)
     ;
   else if (s.n_models > 0)  // with 16-bit stack entries the LDS allows 8: C5 9.14 vs 9.38 ms per pass at 6
-    o << "__attribute__((amdgpu_waves_per_eu(" << (k.stack16 && k.bvh_stack > 0 ? 8 : 6) << "))) ";
+    o << "\n#ifndef RT0_BVH_WAVES\n#define RT0_BVH_WAVES " << (k.stack16 && k.bvh_stack > 0 ? 8 : 6)
+      << "\n#endif\n__attribute__((amdgpu_waves_per_eu(RT0_BVH_WAVES))) ";
   else if (k.restir && !k.defer)
     o << "__attribute__((amdgpu_waves_per_eu(4))) ";
   if (k.wf) {
