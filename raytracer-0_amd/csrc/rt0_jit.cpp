@@ -199,10 +199,9 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   }
   if (k.defer) {
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
-    if (s.n_models > 0 && !k.walk)  // it walks the BVH itself
-      o << "__attribute__((amdgpu_waves_per_eu(6))) ";
-    else
-      o << "__attribute__((amdgpu_waves_per_eu(4))) ";
+    // (RT0_NEE_WAVES through RT0_JIT_EXTRA: an A/B handle)
+    o << "\n#ifndef RT0_NEE_WAVES\n#define RT0_NEE_WAVES " << (s.n_models > 0 && !k.walk ? 6 : 4)  // 6: it walks the BVH itself
+      << "\n#endif\n__attribute__((amdgpu_waves_per_eu(RT0_NEE_WAVES))) ";
     o << "void rt0_jit_nee(const LaunchParams P) {\n"
          "  rt0::nee_body<rt0::JitScene, rt0::JitCfg, "
       << vol << ", " << sdf << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
