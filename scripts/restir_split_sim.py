@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(HERE, "..", "raytracer-0_amd"))
 import rt0  # noqa: E402
 from rt0 import shard, workloads  # noqa: E402
 
-SPLITS = ("0", "2", "3", "4")
+SPLITS = tuple(os.environ.get("SPLITS", "0 2 3 4").split())  # e.g. SPLITS=0 RT0_DEFER_NEE=0
 
 
 def timed(wl, rank=0, n=1, band=None, halo=24):
