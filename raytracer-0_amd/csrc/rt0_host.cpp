@@ -47,6 +47,14 @@ static const long kChunkWaves = 65536;
 static const int kTreeletNodes = 128;
 // pass-wave record regions per light-sampling wave (JitKey::nee_regions)
 static long nee_regions_per_wave() { return 2L; }
+// deferred ReSTIR keys without the walk kernel: rt0_jit_nee completes its
+// pixels' samples (rt0_integrator.h RT0_FUSED_RESOLVE), no resolve launch;
+// RT0_FUSED_RESOLVE=0 keeps rt0_jit_resolve (read when the module is built:
+// a test compares the two bit for bit)
+static bool fused_resolve() {
+  const char *e = getenv("RT0_FUSED_RESOLVE");
+  return !e || atoi(e) != 0;
+}
 
 enum { R_OUT_MAIN = 0, R_OUT_AUX, R_BACK_MAIN, R_BACK_AUX, R_H1, R_H1A, R_H2, R_H2A, R_COUNT };
 // The reservoir textures are four interleaved pair buffers (rt0_integrator.h
@@ -962,7 +970,7 @@ static int restir_split_pass(rt0_ctx *c, const LaunchParams &p, dim3 grid, int K
     HIPCHK(c, go(c->jit.pass, g.x, g.y));
     HIPCHK(c, go(c->jit.nee, (unsigned)((nee_waves + 3) / 4), 1));
     if (c->jit.walk) HIPCHK(c, go(c->jit.walk, (unsigned)((nee_waves + 3) / 4), 1));
-    HIPCHK(c, go(c->jit.resolve, g.x, g.y));
+    if (c->jit.resolve) HIPCHK(c, go(c->jit.resolve, g.x, g.y));  // (null: rt0_jit_nee resolved)
     wave0 += waves;
     nee_wave0 += nee_waves;
   }
@@ -1063,6 +1071,7 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
       }
       key.nee_regions = (int)nee_regions_per_wave();
       key.walk = want_walk ? 1 : 0;
+      key.fused = defer && !want_walk && fused_resolve() ? 1 : 0;
       key.wf = want_wf ? 1 : 0;
       int rc = rt0h::jit_get(c->host_scene, key, c->device, &c->jit, c->jit_err);
       if (rc != RT0_OK) return fail(c, rc, c->jit_err);
@@ -1179,9 +1188,10 @@ static int render_impl(rt0_ctx *c, uint32_t first, int n, float time_ms, bool sy
           HIPCHK(c, rt0h::jit_launch(c->jit.walk, &p, (nee_waves + 3) / 4, 1, 1, c->stream) == RT0_OK
                         ? hipSuccess
                         : hipErrorLaunchFailure);
-        HIPCHK(c, rt0h::jit_launch(c->jit.resolve, &p, grid.x, grid.y, 1, c->stream) == RT0_OK
-                      ? hipSuccess
-                      : hipErrorLaunchFailure);
+        if (c->jit.resolve)  // (null: rt0_jit_nee completed the samples)
+          HIPCHK(c, rt0h::jit_launch(c->jit.resolve, &p, grid.x, grid.y, 1, c->stream) == RT0_OK
+                        ? hipSuccess
+                        : hipErrorLaunchFailure);
         launches++;  // one pass (rt0_last_kernel_ms)
       } else {
         HIPCHK(c, launch(p, 1, grid));

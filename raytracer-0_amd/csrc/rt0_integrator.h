@@ -3117,6 +3117,12 @@ DEV const float4 *candidate_table(const Scene &sc, const Cfg &cfg) {
   return nullptr;
 }
 
+#ifndef RT0_FUSED_RESOLVE  // rt0_jit_nee completes its pixels' samples (no rt0_jit_resolve; no walk kernel)
+#define RT0_FUSED_RESOLVE 0
+#endif
+template <class Cfg, bool SPECTRAL>
+DEV void resolve_pixel(const LaunchParams &P, const Cfg &cfg, int px, int r);
+
 template <class Scene, class Cfg, bool VOL, bool SDF, bool SPECTRAL>
 DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
   treelet_load(P);
@@ -3234,6 +3240,23 @@ DEV void nee_body(const LaunchParams &P, Scene sc, Cfg cfg) {
     const v3 c = it.restir(mk(r.x, r.y, r.z), mk(r.nx, r.ny, r.nz), it.mat_at(r.mat()), sx, sy);
     store(r, c, it.fin);
   }
+#if RT0_FUSED_RESOLVE
+  // Every call of this wave's regions is stored, and a region holds every
+  // call of its pass wave's 64 pixels: the wave completes those pixels'
+  // samples itself (resolve_pixel, rt0_jit_resolve's arithmetic) instead of a
+  // resolve launch.  The stores were this wave's own (one L1): a
+  // workgroup-scope fence orders them before the loads.
+  __threadfence_block();
+  const int lane = (int)(threadIdx.x & 63u), gx = (P.vp_x1 - P.vp_x0 + 15) / 16;
+#pragma unroll
+  for (int q = 0; q < RT0_NEE_REGIONS; ++q) {
+    const uint32_t rg = r0 + (uint32_t)q;  // pass wave (blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave
+    if (rg >= (uint32_t)P.nee_regions) break;
+    const int b = (int)(rg >> 2), wv = (int)(rg & 3u), bx = b % gx, by = b / gx;
+    resolve_pixel<Cfg, SPECTRAL>(P, cfg, P.vp_x0 + bx * 16 + (lane & 7) + ((wv & 1) << 3),
+                                 P.vp_y0 + by * 16 + (lane >> 3) + ((wv >> 1) << 3));
+  }
+#endif
 #endif
 }
 
@@ -3435,11 +3458,9 @@ DEV void walk_body(const LaunchParams &P) {
 // radiance plus its light-sampling results in call order, main()'s spectral
 // weighting (2152-2155), then the accumulator (2157-2169).  Same tile grid as
 // pass_body.
-template <class Scene, class Cfg, bool SPECTRAL>
-DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int px = P.vp_x0 + (int)blockIdx.x * 16 + (lane & 7) + ((wave & 1) << 3);
-  const int r = P.vp_y0 + (int)blockIdx.y * 16 + (lane >> 3) + ((wave >> 1) << 3);
+// (one pixel: launch column px, launch row r)
+template <class Cfg, bool SPECTRAL>
+DEV void resolve_pixel(const LaunchParams &P, const Cfg &cfg, int px, int r) {
   if (px >= P.vp_x1 || r >= P.vp_y1) return;
   const int py = image_row(P, r);
   if (py >= P.height) return;
@@ -3489,6 +3510,12 @@ DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
     a.z += col.z;
   }
   P.accum[apix] = a;
+}
+template <class Scene, class Cfg, bool SPECTRAL>
+DEV void resolve_body(const LaunchParams &P, Scene, Cfg cfg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  resolve_pixel<Cfg, SPECTRAL>(P, cfg, P.vp_x0 + (int)blockIdx.x * 16 + (lane & 7) + ((wave & 1) << 3),
+                               P.vp_y0 + (int)blockIdx.y * 16 + (lane >> 3) + ((wave >> 1) << 3));
 }
 
 // Frame-chunked launches: accumulator += samples of frames 0..nframes-1 in

@@ -71,6 +71,7 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   o << "#define RT0_HALO_CHECK " << k.halo_check << "\n";
   if (k.defer) o << "#define RT0_DEFER_NEE 1\n#define RT0_NEE_REGIONS " << k.nee_regions << "\n";
   if (k.defer && k.walk) o << "#define RT0_NEE_WALK 1\n";
+  if (k.defer && !k.walk && k.fused) o << "#define RT0_FUSED_RESOLVE 1\n";
   if (k.bvh_stack > 0 && k.stack16) o << "#define RT0_BVH_STACK16 1\n";
   // the tree's top levels in LDS (rt0_integrator.h bvh_fetch; rt0_host.cpp kTreeletNodes)
   if (k.bvh_stack > 0) o << "#ifndef RT0_TREELET\n#define RT0_TREELET 64\n#endif\n";
@@ -205,9 +206,10 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
     o << "void rt0_jit_nee(const LaunchParams P) {\n"
          "  rt0::nee_body<rt0::JitScene, rt0::JitCfg, "
       << vol << ", " << sdf << ", " << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
-    o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_resolve(const LaunchParams P) {\n"
-         "  rt0::resolve_body<rt0::JitScene, rt0::JitCfg, "
-      << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
+    if (k.walk || !k.fused)
+      o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_resolve(const LaunchParams P) {\n"
+           "  rt0::resolve_body<rt0::JitScene, rt0::JitCfg, "
+        << spc << ">(P, rt0::JitScene{}, rt0::JitCfg{});\n}\n";
     if (k.walk)
       o << "extern \"C\" __global__ __launch_bounds__(256) void rt0_jit_walk(const LaunchParams P) { rt0::walk_body(P); }\n";
   }
@@ -369,7 +371,7 @@ int jit_get(const SceneDev &s, const JitKey &k, int device, JitFns *fns, std::st
   }
   if (ok && k.defer)
     ok = hipModuleGetFunction(&f[1], e.mod, "rt0_jit_nee") == hipSuccess &&
-         hipModuleGetFunction(&f[2], e.mod, "rt0_jit_resolve") == hipSuccess;
+         (k.fused && !k.walk ? true : hipModuleGetFunction(&f[2], e.mod, "rt0_jit_resolve") == hipSuccess);
   if (ok && k.defer && k.walk)
     ok = hipModuleGetFunction(&f[3], e.mod, "rt0_jit_walk") == hipSuccess;
   if (!ok) {
@@ -504,6 +506,10 @@ extern "C" int rt0_jit_compile(const char *scene_text, const char *const *sdf_me
     key.defer = key.restir && key.max_bounces > 0 && key.max_bounces <= RT0_NEE_MAX_BOUNCES && (!d || atoi(d) != 0);
     // (the host also needs a built BVH; here the scene's TRIANGLE entries decide)
     key.walk = key.defer && nm > 0 && ns == 0 && !s.any_tex && !(key.flags & F_ANIM) ? 1 : 0;
+    {  // (rt0_host.cpp fused_resolve)
+      const char *fr = getenv("RT0_FUSED_RESOLVE");
+      key.fused = key.defer && !key.walk && (!fr || atoi(fr) != 0) ? 1 : 0;
+    }
     // (the tree's depth and size are unknown here: RT0_BVH_STACK16=1 and
     // RT0_JIT_STACK=<entries> select what rt0_render would for such a tree)
     // the wavefront rounds rt0_render uses for such a scene (rt0_host.cpp wf_eligible)

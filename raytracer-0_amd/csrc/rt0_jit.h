@@ -22,6 +22,7 @@ struct JitKey {
   int defer = 0;       // RT0_DEFER_NEE: ReSTIR light sampling in its own kernel (rt0_jit_nee + rt0_jit_resolve)
   int nee_regions = 2;  // RT0_NEE_REGIONS: pass-wave record regions per light-sampling wave
   int walk = 0;         // RT0_NEE_WALK: the light-sampling calls' triangle occlusion queries in rt0_jit_walk
+  int fused = 0;        // RT0_FUSED_RESOLVE: rt0_jit_nee completes the samples (deferred keys without walk)
   int stack16 = 0;      // RT0_BVH_STACK16: every BVH node index fits 16 + 64 / RT0_BVH_STACK bits
   int wf = 0;           // RT0_WAVEFRONT: passes as wavefront rounds (rt0_jit_wf_shade + rt0_jit_wf_march / _walk)
 };

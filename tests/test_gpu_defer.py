@@ -293,3 +293,31 @@ def test_wavefront_stream_count_is_bit_identical(streams, cfgs, monkeypatch, gpu
     a = go()
     monkeypatch.setenv("RT0_WF_STREAMS", streams)
     assert np.array_equal(a, go())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,size,viewport,split", [
+    ("c3_outdoor_restir", 72, None, None),            # ragged tiles
+    ("c3_outdoor_restir", 64, (8, 16, 40, 24), None),  # a tile
+    ("c3_outdoor_restir", 64, None, "3"),              # three row parts
+    ("restir_mis_demo", 64, None, None),
+    ("c5_spectral_sphere", 64, None, None),            # spectral weighting
+    ("anim_restir_demo", 64, None, None),              # RENDER_MODE 1 (EMA)
+])
+def test_fused_resolve_is_bit_identical(name, size, viewport, split, cfgs, monkeypatch, gpu_required):
+    """rt0_jit_nee completing its own pixels' samples (RT0_FUSED_RESOLVE, the
+    default for deferred passes without the occlusion-walk kernel) runs
+    rt0_jit_resolve's arithmetic (resolve_pixel) on the same stored calls,
+    right after them in the same wave: a 4-pass chain equals the one with the
+    resolve launch bit for bit -- samples and reservoirs."""
+    if not have(name):
+        pytest.skip("fixture not generated")
+    if split:
+        monkeypatch.setenv("RT0_RESTIR_SPLIT", split)
+    monkeypatch.setenv("RT0_FUSED_RESOLVE", "0")
+    ref = chain(cfgs, name, "1", n=4, size=size, viewport=viewport)
+    monkeypatch.setenv("RT0_FUSED_RESOLVE", "1")
+    got = chain(cfgs, name, "1", n=4, size=size, viewport=viewport)
+    for what, a, b in zip(("samples", "reservoir main", "reservoir aux"), ref, got):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), what
+    assert got[0][..., :3].mean() > 0.0
