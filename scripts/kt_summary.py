@@ -7,8 +7,8 @@ run of bench.py (scripts/gpu_measure.sh).
 Keeps the rt0_jit_pass dispatches after the first SKIP (the warm-up step's
 launches) and reports their median / mean / min / max duration, plus the other
 kernels' totals (rocprofv3's own --stats table averages every dispatch,
-warm-up included).  A deferred ReSTIR pass is three dispatches (rt0_jit_pass,
-rt0_jit_nee, rt0_jit_resolve; rt0_integrator.h), four in scenes with models
+warm-up included).  A deferred ReSTIR pass is two or three dispatches (rt0_jit_pass,
+rt0_jit_nee [, rt0_jit_resolve]; rt0_integrator.h RT0_FUSED_RESOLVE), four in scenes with models
 (+ rt0_jit_walk), twice when the pass runs as two row parts on K streams
 (restir_split_pass): "median_ms" .. "max_ms" are then per pass, each pass's
 span (first dispatch start to last end), and the per-kernel medians its busy
