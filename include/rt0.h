@@ -328,6 +328,9 @@ int rt0_set_texture_filter(rt0_ctx *ctx, int mode);
  * scenes with triangle models (RENDER_MODE 0, no SDFs, no textured lights)
  * a third kernel between them answers the calls' triangle occlusion queries
  * (the visibility and shadow rays) on dense lanes: four dispatches per pass.
+ * Without that kernel the light-sampling kernel completes its pixels'
+ * samples itself (two dispatches per pass; RT0_FUSED_RESOLVE=0 in the
+ * environment when the module is built keeps the third: bit-identical).
  * Same arguments and arithmetic as the inline calls, but NOT bitwise equal:
  * FMA placement can differ, and a sample's fp32 additions run in another
  * order (the path's own radiance first, then the light-sampling results in
