@@ -76,11 +76,14 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   // the tree's top levels in LDS (rt0_integrator.h bvh_fetch; rt0_host.cpp kTreeletNodes)
   if (k.bvh_stack > 0) o << "#ifndef RT0_TREELET\n#define RT0_TREELET 64\n#endif\n";
   if (k.wf) o << "#define RT0_WAVEFRONT 1\n";
-  // ReSTIR scenes without models fetch their reservoir taps two at a time
+  // ReSTIR light sampling fetches its reservoir taps two at a time
   // (rt0_integrator.h RT0_TAP_BATCH; C3 0.600 vs 0.652 ms per pass at the
-  // occupancy target below); with a BVH the extra registers cost more than
-  // the halved round trips save (C5 22.95 vs 18.39 ms), so 1 there
-  if (k.restir && s.n_models == 0) o << "#ifndef RT0_TAP_BATCH\n#define RT0_TAP_BATCH 2\n#endif\n";
+  // occupancy target below) unless the kernel also walks the BVH, where the
+  // extra registers cost more than the halved round trips save (C5 22.95 vs
+  // 18.39 ms, inline light sampling); with the walks in their own kernel C5's
+  // light-sampling kernel takes the batch at 3 waves per SIMD (2 150-2 158 vs
+  // 2 136-2 141 Msamples/s, profiles/r06/c5_tap_batch)
+  if (k.restir && (s.n_models == 0 || k.walk)) o << "#ifndef RT0_TAP_BATCH\n#define RT0_TAP_BATCH 2\n#endif\n";
   o << "using __hip_internal::int32_t; using __hip_internal::uint16_t; using __hip_internal::uint32_t; using __hip_internal::uint64_t;\n";
   // the embedded device source only: profiling probes build their own
   // library from a patched copy (scripts/probes.sh), none is read at run time
@@ -201,7 +204,8 @@ std::string jit_source(const SceneDev &s, const JitKey &k) {
   if (k.defer) {
     o << "extern \"C\" __global__ __launch_bounds__(256) ";
     // (RT0_NEE_WAVES through RT0_JIT_EXTRA: an A/B handle)
-    o << "\n#ifndef RT0_NEE_WAVES\n#define RT0_NEE_WAVES " << (s.n_models > 0 && !k.walk ? 6 : 4)  // 6: it walks the BVH itself
+    // 6: it walks the BVH itself; 3: batched taps beside the walk kernel's scenes' larger light loops
+    o << "\n#ifndef RT0_NEE_WAVES\n#define RT0_NEE_WAVES " << (s.n_models > 0 ? (k.walk ? 3 : 6) : 4)
       << "\n#endif\n__attribute__((amdgpu_waves_per_eu(RT0_NEE_WAVES))) ";
     o << "void rt0_jit_nee(const LaunchParams P) {\n"
          "  rt0::nee_body<rt0::JitScene, rt0::JitCfg, "

@@ -321,3 +321,42 @@ def test_fused_resolve_is_bit_identical(name, size, viewport, split, cfgs, monke
     for what, a, b in zip(("samples", "reservoir main", "reservoir aux"), ref, got):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), what
     assert got[0][..., :3].mean() > 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,size", [("c5_spectral_models", (64, 80)), ("c3_outdoor_restir", (72, 64)),
+                                       ("restir_mis_demo", (64, 64))])
+def test_tap_batch_is_bit_identical(name, size, cfgs, monkeypatch, gpu_required):
+    """The light-sampling kernel issues the loads of RT0_TAP_BATCH reservoir
+    taps before it lerps any (rt0_integrator.h bil_at / Bil; 2 by default,
+    also beside the walk kernel since round 6): the same texels, weights and
+    arithmetic as one tap at a time, so a 4-pass chain matches
+    RT0_TAP_BATCH=1 bit for bit -- samples and reservoirs."""
+    import test_models as T
+    if name != "c5_spectral_models" and not have(name):
+        pytest.skip("fixture not generated")
+    cfg = T.cfg_by_name(cfgs, name)
+    out = []
+    for extra in ("-DRT0_TAP_BATCH=1", None):
+        if extra:
+            monkeypatch.setenv("RT0_JIT_EXTRA", extra)
+        else:
+            monkeypatch.delenv("RT0_JIT_EXTRA", raising=False)
+        if name == "c5_spectral_models":
+            r = T.make(cfg, cfgs, *size)
+        else:
+            r = rt0.Renderer(*size)
+            configure(r, cfg, cfgs)
+            r.set_temporal_frames(cfg.get("temporal_frames", 5))
+        S, M, A = [], [], []
+        for k in range(1, 5):
+            r.render(k, 1)
+            S.append(r.read_accum())
+            m, a = r.read_restir(0)
+            M.append(m)
+            A.append(a)
+        out.append((np.stack(S), np.stack(M), np.stack(A)))
+        r.close()
+    for what, a, b in zip(("samples", "reservoir main", "reservoir aux"), out[0], out[1]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), what
+    assert out[1][0][..., :3].mean() > 0.0
